@@ -1,0 +1,199 @@
+/*
+ * mfnerf.h -- C ABI of libmfnerf_hip.so, the MI355X (gfx950) kernels behind MF-NeRF's
+ * volumetric-rendering training step.
+ *
+ * Conventions (every entry point):
+ *   - plain device pointers + sizes, row-major contiguous arrays, no torch types;
+ *   - the last argument is the HIP stream the work is enqueued on (NULL = legacy default);
+ *   - return 0 on success, a nonzero MFN_ERR_* code otherwise; mfnerf_last_error()
+ *     returns a message for the calling thread's last failure;
+ *   - no entry point allocates, frees or synchronises: callers pass workspace, so every
+ *     call is legal inside hipStreamBeginCapture (HIP graphs);
+ *   - outputs are NOT pre-zeroed by the library unless stated ("zero-fills").
+ *
+ * Reference interfaces replaced (lly00412/MF-NeRF, paths relative to the repo root):
+ *   vren pybind module: models/csrc/binding.cpp:234-250 (C++ signatures binding.cpp:4-231,
+ *   models/csrc/include/utils.h:9-126); tiny-cuda-nn HashGrid / SphericalHarmonics /
+ *   FullyFusedMLP as configured in models/networks.py:36-79; apex FusedAdam (train.py:136).
+ */
+#ifndef MFNERF_H
+#define MFNERF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* mfnerf_stream_t; /* == hipStream_t */
+
+#define MFN_OK 0
+#define MFN_ERR_INVALID 1 /* bad argument (null pointer, bad size, unsupported config) */
+#define MFN_ERR_LAUNCH 2  /* HIP launch error */
+
+const char* mfnerf_last_error(void);
+int mfnerf_abi_version(void);
+
+/* ---------------------------------------------------------------- vren ops */
+
+/* vren.ray_aabb_intersect (binding.cpp:4-16, intersection.cu:59-100).
+ * rays_o, rays_d (n_rays,3) f32; centers, half_sizes (n_voxels,3) f32.
+ * Writes hit_cnt (n_rays) i32, hits_t (n_rays,max_hits,2) f32, hits_voxel_idx (n_rays,max_hits) i64;
+ * zero-fills / -1-fills all three.  Hits are kept in voxel order and sorted near->far by t1. */
+int mfnerf_ray_aabb_intersect(const float* rays_o, const float* rays_d, const float* centers,
+                              const float* half_sizes, int64_t n_rays, int64_t n_voxels, int max_hits,
+                              int32_t* hit_cnt, float* hits_t, int64_t* hits_voxel_idx, mfnerf_stream_t stream);
+
+/* vren.morton3D (binding.cpp:46-50, raymarching.cu:62-88): coords (n,3) i32 -> out (n) i32. */
+int mfnerf_morton3d(const int32_t* coords, int64_t n, int32_t* out, mfnerf_stream_t stream);
+
+/* vren.morton3D_invert (binding.cpp:53-57, raymarching.cu:90-119): idx (n) i32 -> coords (n,3) i32. */
+int mfnerf_morton3d_invert(const int32_t* idx, int64_t n, int32_t* coords, mfnerf_stream_t stream);
+
+/* vren.packbits (binding.cpp:34-43, raymarching.cu:122-161): bit i of byte n = grid[8n+i] > thr.
+ * grid (8*n_bytes) f32.  thr_dev, when non-NULL, is a device f32 read instead of `thr`
+ * (keeps the occupancy update free of host syncs). */
+int mfnerf_packbits(const float* grid, int64_t n_bytes, float thr, const float* thr_dev, uint8_t* bitfield,
+                    mfnerf_stream_t stream);
+
+/* Workspace bytes mfnerf_raymarching_train needs for n_rays rays. */
+int64_t mfnerf_raymarching_train_workspace(int64_t n_rays);
+
+/* vren.raymarching_train (binding.cpp:60-85, raymarching.cu:166-332).
+ * hits_t: (n_rays,2) f32 rows (t1,t2) with row stride hits_stride floats.
+ * Outputs: rays_a (n_rays,3) i64 -- row r = (r, start, count), start = exclusive prefix sum
+ *          (canonical order; the reference's atomicAdd order is nondeterministic);
+ *          xyzs, dirs (capacity,3), deltas, ts (capacity) f32 -- samples [0, counter[0]);
+ *          counter (2) i32 = (total samples, n_rays).  Samples beyond `capacity` are dropped
+ *          (their rays' counts are clipped).  Device-resident count: no host sync. */
+int mfnerf_raymarching_train(const float* rays_o, const float* rays_d, const float* hits_t, int64_t hits_stride,
+                             const uint8_t* bitfield, int cascades, float scale, float exp_step_factor,
+                             const float* noise, int grid_size, int max_samples, int64_t n_rays, int64_t capacity,
+                             int64_t* rays_a, float* xyzs, float* dirs, float* deltas, float* ts, int32_t* counter,
+                             void* workspace, mfnerf_stream_t stream);
+
+/* vren.raymarching_test (binding.cpp:88-115, raymarching.cu:335-454), including the reference's
+ * calc_dt(..., cascades) quirk.  hits_t (n_rays,2 with row stride hits_stride) is updated in place
+ * (column 0).  Zero-fills xyzs, dirs (n_alive,N_samples,3), deltas, ts (n_alive,N_samples), n_eff (n_alive) i32. */
+int mfnerf_raymarching_test(const float* rays_o, const float* rays_d, float* hits_t, int64_t hits_stride,
+                            const int64_t* alive_indices, int64_t n_alive, const uint8_t* bitfield, int cascades,
+                            float scale, float exp_step_factor, int grid_size, int max_samples, int N_samples,
+                            float* xyzs, float* dirs, float* deltas, float* ts, int32_t* n_eff,
+                            mfnerf_stream_t stream);
+
+/* vren.composite_train_fw (binding.cpp:118-136, volumerendering.cu:6-84).
+ * sigmas (n_samples), rgbs (n_samples,3), deltas, ts f32; rays_a (n_rays,3) i64.
+ * Writes total_samples (indexed by ray id) i64, opacity, depth (n_rays), rgb (n_rays,3) and ws for every
+ * sample of every listed ray (0 after the ray terminates); no memset of n_samples-sized buffers. */
+int mfnerf_composite_train_fw(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
+                              const int64_t* rays_a, int64_t n_rays, int64_t n_samples, float T_threshold,
+                              int64_t* total_samples, float* opacity, float* depth, float* rgb, float* ws,
+                              mfnerf_stream_t stream);
+
+/* vren.composite_train_bw (binding.cpp:139-173, volumerendering.cu:87-202).  Writes dL_dsigmas (n_samples)
+ * and dL_drgbs (n_samples,3) for every sample of every listed ray (0 after the ray terminates).
+ * The per-ray scan of dL_dws*ws (host-side + thrust in the reference) is done in-kernel. */
+int mfnerf_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, const float* dL_drgb,
+                              const float* dL_dws, const float* sigmas, const float* rgbs, const float* ws,
+                              const float* deltas, const float* ts, const int64_t* rays_a, const float* opacity,
+                              const float* depth, const float* rgb, int64_t n_rays, int64_t n_samples,
+                              float T_threshold, float* dL_dsigmas, float* dL_drgbs, mfnerf_stream_t stream);
+
+/* vren.composite_test_fw (binding.cpp:176-201, volumerendering.cu:205-285).  sigmas (n_alive,N_samples),
+ * rgbs (n_alive,N_samples,3), deltas, ts (n_alive,N_samples); in place on alive_indices, opacity,
+ * depth, rgb (indexed by ray). */
+int mfnerf_composite_test_fw(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
+                             int64_t* alive_indices, int64_t n_alive, int N_samples, float T_threshold,
+                             const int32_t* n_eff, float* opacity, float* depth, float* rgb,
+                             mfnerf_stream_t stream);
+
+/* vren.distortion_loss_fw (binding.cpp:204-216, losses.cu:9-109).  Zero-fills loss (n_rays) and
+ * writes ws_inclusive_scan, wts_inclusive_scan (n_samples). */
+int mfnerf_distortion_loss_fw(const float* ws, const float* deltas, const float* ts, const int64_t* rays_a,
+                              int64_t n_rays, int64_t n_samples, float* loss, float* ws_incl, float* wts_incl,
+                              mfnerf_stream_t stream);
+
+/* vren.distortion_loss_bw (binding.cpp:219-231, losses.cu:112-175).  Zero-fills dL_dws (n_samples). */
+int mfnerf_distortion_loss_bw(const float* dL_dloss, const float* ws_incl, const float* wts_incl,
+                              const float* ws, const float* deltas, const float* ts, const int64_t* rays_a,
+                              int64_t n_rays, int64_t n_samples, float* dL_dws, mfnerf_stream_t stream);
+
+/* ---------------------------------------------------------------- grid encoding (tcnn HashGrid / MF) */
+
+/* Level table of a multiresolution grid (tcnn GridEncodingTemplated, networks.py:39-49).
+ * Host-computed once; per level: scale = exp2f(l*log2f(b))*N_min - 1, res = ceil(scale)+1,
+ * offset/size in entries (of n_features values each).  table_kind: 0 own table (dense when
+ * res^3 <= size, else coherent prime hash), 1 MixedFeature shared table (canonical-grid index). */
+#define MFN_MAX_LEVELS 32
+typedef struct {
+    int32_t n_levels;
+    int32_t n_features;         /* F: only 2 is supported by the kernels */
+    int32_t canon_res;          /* MixedFeature canonical grid resolution */
+    int32_t pad_;
+    float scale[MFN_MAX_LEVELS];
+    uint32_t res[MFN_MAX_LEVELS];
+    uint32_t offset[MFN_MAX_LEVELS];
+    uint32_t size[MFN_MAX_LEVELS];
+    int32_t table_kind[MFN_MAX_LEVELS];
+} mfnerf_grid_desc;
+
+/* Encode points x (n,3) f32.  The kernel first normalises x' = (x - x_min) / x_range exactly as
+ * NGP.density does in torch (networks.py:105: (x-xyz_min)/(xyz_max-xyz_min); pass 0, 1 for inputs
+ * already in [0,1]^3).  table (n_entries*F) f16.  out (n, n_levels*F) f16 row-major.
+ * n_dev (optional, device i32): live row count <= n (rows beyond it are skipped). */
+int mfnerf_grid_encode_fw(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                          const mfnerf_grid_desc* desc, const void* table_f16, void* out_f16,
+                          mfnerf_stream_t stream);
+
+/* Scatter dL/dout (n, n_levels*F) f32 into grad_table (n_entries*F) f32 by float atomics
+ * (accumulates; caller zeroes). */
+int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                          const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
+                          mfnerf_stream_t stream);
+
+/* ---------------------------------------------------------------- NGP field head (MFMA) */
+
+/* Weight blob for the two FullyFusedMLPs of NGP (networks.py:50-79) in this library's MFMA
+ * fragment order (f16).  Built from fp32 tcnn-layout params by mfnerf_field_pack_weights. */
+int64_t mfnerf_field_packed_bytes(int rgb_width);
+
+/* params_xyz: (64*32 + 16*64) f32, row-major [out][in] per layer (tcnn layout, bias-free);
+ * params_rgb: (W*32 + W*W + 16*W) f32.  Writes packed (mfnerf_field_packed_bytes). */
+int mfnerf_field_pack_weights(const float* params_xyz, const float* params_rgb, int rgb_width, void* packed,
+                              mfnerf_stream_t stream);
+
+/* NGP.forward (networks.py:134-155) on encoded features:
+ *   h = xyz_mlp(feat); sigma = exp(h[0]); rgb = sigmoid(rgb_mlp([SH4((d/|d|+1)/2), h])).
+ * feat (n,32) f16, dirs (n,3) f32 (ignored when density_only) -> sigma (n) f32, rgb (n,3) f32. */
+int mfnerf_field_fw(const void* feat_f16, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
+                    int rgb_width, int density_only, float* sigma, float* rgb, mfnerf_stream_t stream);
+
+/* Backward of mfnerf_field_fw (recomputes the forward).  dL_dsigma (n), dL_drgb (n,3) f32 ->
+ * dL_dfeat (n,32) f32, and ADDS the weight grads into grad_xyz / grad_rgb (tcnn layout f32).
+ * grad_scale: power-of-two factor applied to the incoming grads before the fp16 MFMA products
+ * and removed from every output (keeps O(1e-6) per-sample grads out of the fp16 subnormals).
+ * workspace: mfnerf_field_bw_workspace() bytes (per-workgroup weight-grad slab). */
+int64_t mfnerf_field_bw_workspace(int64_t n, int rgb_width);
+int mfnerf_field_bw(const void* feat_f16, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
+                    int rgb_width, const float* dL_dsigma, const float* dL_drgb, float grad_scale, float* dL_dfeat,
+                    float* grad_xyz, float* grad_rgb, void* workspace, mfnerf_stream_t stream);
+
+/* Debug: one v_mfma_f32_32x32x16_f16 with A (32x16) and B (16x32) f16 row-major -> D (32x32) f32,
+ * through the lane maps the field kernels assume (pins them on the device). */
+int mfnerf_debug_mfma_probe(const void* A, const void* B, float* D, mfnerf_stream_t stream);
+
+/* ---------------------------------------------------------------- optimizer */
+
+/* Adam (apex FusedAdam semantics, adam_w_mode=False, no weight decay; train.py:136):
+ * m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= lr * (m/(1-b1^t)) / (sqrt(v/(1-b2^t)) + eps).
+ * g is read as grad*grad_scale.  Optionally mirrors p into p_f16 (the fp16 compute copy).
+ * step_dev (optional device i32): step counter incremented by the kernel (graph-replay safe). */
+int mfnerf_adam_step(float* params, const float* grads, float* m, float* v, void* p_f16, int64_t n, float lr,
+                     float beta1, float beta2, float eps, float grad_scale, int step, const int32_t* step_dev,
+                     mfnerf_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MFNERF_H */

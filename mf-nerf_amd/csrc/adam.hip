@@ -1,0 +1,75 @@
+// adam.hip -- fused Adam step (apex FusedAdam semantics as used at train.py:136: adam_w_mode
+// off, weight_decay 0, eps 1e-15) over the flat fp32 master params, optionally refreshing the
+// fp16 compute copy of the hash table in the same pass (one read of p/g/m/v, one write of
+// p/m/v/p16: 4+4+4+4 read + 4+4+4+2 write bytes per param, float4-vectorised).
+#include "common.hpp"
+#include "../../include/mfnerf.h"
+
+namespace {
+
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, __half* __restrict__ p16, int64_t n, float lr, float b1, float b2,
+                            float eps, float gscale, int step, const int32_t* __restrict__ step_dev) {
+    const int st = step_dev ? *step_dev : step;
+    // apex multi_tensor_adam (ADAM_MODE, decay 0): m/(1-b1^t), v/(1-b2^t), p -= lr*m_hat/(sqrt(v_hat)+eps)
+    const float bc1 = 1.0f - powf(b1, (float)st);
+    const float bc2 = 1.0f - powf(b2, (float)st);
+    const int64_t n4 = n / 4;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        float4 pp = reinterpret_cast<float4*>(p)[i];
+        const float4 gg = reinterpret_cast<const float4*>(g)[i];
+        float4 mm = reinterpret_cast<float4*>(m)[i];
+        float4 vv = reinterpret_cast<float4*>(v)[i];
+        float* pa = &pp.x; const float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float gk = ga[k] * gscale;
+            ma[k] = b1 * ma[k] + (1.0f - b1) * gk;
+            va[k] = b2 * va[k] + (1.0f - b2) * gk * gk;
+            const float denom = sqrtf(va[k] / bc2) + eps;
+            pa[k] = pa[k] - lr * ((ma[k] / bc1) / denom);
+        }
+        reinterpret_cast<float4*>(p)[i] = pp;
+        reinterpret_cast<float4*>(m)[i] = mm;
+        reinterpret_cast<float4*>(v)[i] = vv;
+        if (p16) {
+            __half2 a = __floats2half2_rn(pp.x, pp.y), b = __floats2half2_rn(pp.z, pp.w);
+            uint2 u; u.x = *reinterpret_cast<uint32_t*>(&a); u.y = *reinterpret_cast<uint32_t*>(&b);
+            reinterpret_cast<uint2*>(p16)[i] = u;
+        }
+    }
+    // tail
+    for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float gk = g[i] * gscale;
+        m[i] = b1 * m[i] + (1.0f - b1) * gk;
+        v[i] = b2 * v[i] + (1.0f - b2) * gk * gk;
+        const float denom = sqrtf(v[i] / bc2) + eps;
+        p[i] = p[i] - lr * ((m[i] / bc1) / denom);
+        if (p16) p16[i] = __float2half_rn(p[i]);
+    }
+}
+
+__global__ void bump_step_kernel(int32_t* s) { *s += 1; }
+
+}  // namespace
+
+extern "C" int mfnerf_adam_step(float* params, const float* grads, float* m, float* v, void* p_f16, int64_t n,
+                                float lr, float beta1, float beta2, float eps, float grad_scale, int step,
+                                const int32_t* step_dev, mfnerf_stream_t stream) {
+    if (n < 0) { mfn_set_error("adam_step: bad size"); return MFN_ERR_INVALID; }
+    if (n == 0) return MFN_OK;
+    if (!params || !grads || !m || !v) { mfn_set_error("adam_step: null pointer"); return MFN_ERR_INVALID; }
+    if ((((uintptr_t)params) | ((uintptr_t)grads) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) {
+        mfn_set_error("adam_step: buffers must be 16-byte aligned"); return MFN_ERR_INVALID;
+    }
+    if (p_f16 && (((uintptr_t)p_f16) & 7)) { mfn_set_error("adam_step: fp16 copy must be 8-byte aligned"); return MFN_ERR_INVALID; }
+    if (!step_dev && step < 1) { mfn_set_error("adam_step: step must be >= 1"); return MFN_ERR_INVALID; }
+    const int threads = 256;
+    const int64_t want = mfn::div_up<int64_t>(mfn::div_up<int64_t>(n, 4), threads);
+    const unsigned blocks = (unsigned)(want < 4096 ? (want < 1 ? 1 : want) : 4096);
+    if (step_dev) hipLaunchKernelGGL(bump_step_kernel, dim3(1), dim3(1), 0, stream, (int32_t*)step_dev);
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(threads), 0, stream, params, grads, m, v, (__half*)p_f16, n, lr,
+                       beta1, beta2, eps, grad_scale, step, step_dev);
+    return mfn_check_launch("adam_step");
+}

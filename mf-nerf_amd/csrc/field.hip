@@ -1,0 +1,586 @@
+// field.hip -- NGP field head on gfx950 MFMA: the two tiny-cuda-nn FullyFusedMLPs of
+// models/networks.py:36-79 (xyz: 32->64->16, rgb: [SH4(16) | h(16)] -> 64 -> 64 -> 3, ReLU,
+// bias-free, fp16 operands / fp32 accumulation), TruncExp on h[0] and the SH4 direction
+// encoding, forward and backward.
+//
+// Layout (one wave = one tile of 32 samples, v_mfma_f32_32x32x16_f16):
+//   activations are kept TRANSPOSED -- channel on the MFMA row, sample on the lane (col = lane&31)
+//   -- so layer k's fp32 accumulator, ReLU'd and packed to f16, IS layer k+1's B operand with no
+//   LDS round trip (cdna_hip_programming.md section 3, "An accumulator tile as the next MFMA's
+//   operand").  The weights are the A operands, pre-permuted once per optimizer step by
+//   mfnerf_field_pack_weights into 1-KiB lane-linear fragments (ds_read_b128, conflict-free).
+//   Backward-data products (dX = W^T dY) chain the same way; only the weight gradients
+//   (a reduction over samples = over lanes) go through a per-wave LDS transpose.  Weight
+//   gradients accumulate in registers across all tiles a wave processes (persistent grid),
+//   then one LDS block reduction and one slab row per workgroup, summed by a second kernel
+//   (deterministic, no float atomics).
+#include "common.hpp"
+#include "../../include/mfnerf.h"
+
+using namespace mfn;
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+constexpr int RGB_W = 64;        // rgb_channels supported by this build of the fused head
+constexpr int N_XYZ_PARAMS = 64 * 32 + 16 * 64;
+constexpr int N_RGB_PARAMS = RGB_W * 32 + RGB_W * RGB_W + 16 * RGB_W;
+constexpr int N_FRAGS = 44;
+constexpr int FRAG_HALFS = 64 * 8;  // one A fragment: 64 lanes x 8 f16
+constexpr int FIELD_BLOCK = 256;    // 4 waves
+
+// fragment ids (see frag_spec)
+enum : int {
+    F1 = 0,   // W1  (64x32)  [mt*2+q]     natural, kbase 16q
+    F2 = 4,   // W2  (16x64)  [t*2+q]      perm,    kbase 32t+16q
+    F3 = 8,   // Wr1 (64x32)  [mt*2+q]     q=0 natural kbase 0 (SH); q=1 perm kbase 16 (h)
+    F4 = 12,  // Wr2 (64x64)  [mt*4+t*2+q] perm
+    F5 = 20,  // Wr3 (16x64)  [t*2+q]      perm
+    B5 = 24,  // Wr3^T (64x16) [mt]        perm kbase 0
+    B4 = 26,  // Wr2^T         [mt*4+t*2+q]
+    B3 = 34,  // Wr1^T (32x64) [t*2+q]
+    B2 = 38,  // W2^T  (64x16) [mt]        perm kbase 0
+    B1 = 40,  // W1^T  (32x64) [t*2+q]
+};
+
+struct FragSpec { int mat, trans, mtile, kbase, perm; };
+
+__device__ FragSpec frag_spec(int f) {
+    FragSpec s{0, 0, 0, 0, 1};
+    if (f < 4) { s.mat = 0; s.mtile = f >> 1; s.kbase = 16 * (f & 1); s.perm = 0; }
+    else if (f < 8) { int i = f - 4; s.mat = 1; s.kbase = 32 * (i >> 1) + 16 * (i & 1); }
+    else if (f < 12) { int i = f - 8; s.mat = 2; s.mtile = i >> 1; s.kbase = 16 * (i & 1); s.perm = i & 1; }
+    else if (f < 20) { int i = f - 12; s.mat = 3; s.mtile = i >> 2; s.kbase = 16 * (i & 3); }
+    else if (f < 24) { int i = f - 20; s.mat = 4; s.kbase = 16 * i; }
+    else if (f < 26) { s.mat = 4; s.trans = 1; s.mtile = f - 24; s.kbase = 0; }
+    else if (f < 34) { int i = f - 26; s.mat = 3; s.trans = 1; s.mtile = i >> 2; s.kbase = 16 * (i & 3); }
+    else if (f < 38) { int i = f - 34; s.mat = 2; s.trans = 1; s.kbase = 16 * i; }
+    else if (f < 40) { s.mat = 1; s.trans = 1; s.mtile = f - 38; s.kbase = 0; }
+    else { int i = f - 40; s.mat = 0; s.trans = 1; s.kbase = 16 * i; }
+    return s;
+}
+
+// weight matrices, row-major (out, in) in the tcnn params vectors
+__device__ __forceinline__ void mat_info(int mat, const float* px, const float* pr, const float** p, int* rows,
+                                         int* cols) {
+    switch (mat) {
+        case 0: *p = px; *rows = 64; *cols = 32; break;
+        case 1: *p = px + 64 * 32; *rows = 16; *cols = 64; break;
+        case 2: *p = pr; *rows = RGB_W; *cols = 32; break;
+        case 3: *p = pr + RGB_W * 32; *rows = RGB_W; *cols = RGB_W; break;
+        default: *p = pr + RGB_W * 32 + RGB_W * RGB_W; *rows = 16; *cols = RGB_W; break;
+    }
+}
+
+// k index carried by element j of lane half h (natural B order, or accumulator-as-operand order)
+__device__ __forceinline__ int k_of(int j, int h, int perm) { return perm ? 8 * (j >> 2) + 4 * h + (j & 3) : 8 * h + j; }
+
+__global__ void pack_kernel(const float* __restrict__ px, const float* __restrict__ pr, _Float16* __restrict__ out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= N_FRAGS * FRAG_HALFS) return;
+    const int f = t / FRAG_HALFS, lane = (t / 8) & 63, j = t & 7;
+    const FragSpec s = frag_spec(f);
+    const int r = lane & 31, h = lane >> 5;
+    const int m = 32 * s.mtile + r, k = s.kbase + k_of(j, h, s.perm);
+    const float* p; int rows, cols;
+    mat_info(s.mat, px, pr, &p, &rows, &cols);
+    float v = 0.0f;
+    if (!s.trans) { if (m < rows && k < cols) v = p[m * cols + k]; }
+    else { if (k < rows && m < cols) v = p[k * cols + m]; }
+    out[t] = (_Float16)v;
+}
+
+__device__ __forceinline__ f32x16 mfma(const half8& a, const half8& b, const f32x16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+template <int BASE, bool RELU>
+__device__ __forceinline__ half8 pack8(const f32x16& a) {
+    half8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        float v = a[BASE + j];
+        if (RELU) v = fmaxf(v, 0.0f);
+        r[j] = (_Float16)v;
+    }
+    return r;
+}
+
+// zero dY where the forward activation (stored f16, post-ReLU) is not positive
+template <int BASE>
+__device__ __forceinline__ void relu_mask(f32x16& d, const half8& y) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[BASE + j] = ((float)y[j] > 0.0f) ? d[BASE + j] : 0.0f;
+}
+
+__device__ __forceinline__ half8 lds_frag(const _Float16* lds, int f, int lane) {
+    return *reinterpret_cast<const half8*>(lds + (f * 64 + lane) * 8);
+}
+
+// tcnn SphericalHarmonics degree 4 on in = (d/|d| + 1)/2, mapped back x = in*2-1 (networks.py:145-146)
+__device__ __forceinline__ void sh4(float dx, float dy, float dz, float* o) {
+    const float nrm = sqrtf(dx * dx + dy * dy + dz * dz);
+    float x = dx / nrm, y = dy / nrm, z = dz / nrm;
+    x = ((x + 1.0f) / 2.0f) * 2.0f - 1.0f;
+    y = ((y + 1.0f) / 2.0f) * 2.0f - 1.0f;
+    z = ((z + 1.0f) / 2.0f) * 2.0f - 1.0f;
+    const float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
+    o[0] = 0.28209479177387814f;
+    o[1] = -0.48860251190291987f * y;
+    o[2] = 0.48860251190291987f * z;
+    o[3] = -0.48860251190291987f * x;
+    o[4] = 1.0925484305920792f * xy;
+    o[5] = -1.0925484305920792f * yz;
+    o[6] = 0.94617469575755997f * z2 - 0.31539156525251999f;
+    o[7] = -1.0925484305920792f * xz;
+    o[8] = 0.54627421529603959f * x2 - 0.54627421529603959f * y2;
+    o[9] = 0.59004358992664352f * y * (-3.0f * x2 + y2);
+    o[10] = 2.8906114426405538f * xy * z;
+    o[11] = 0.45704579946446572f * y * (1.0f - 5.0f * z2);
+    o[12] = 0.3731763325901154f * z * (5.0f * z2 - 3.0f);
+    o[13] = 0.45704579946446572f * x * (1.0f - 5.0f * z2);
+    o[14] = 1.4453057213202769f * z * (x2 - y2);
+    o[15] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
+}
+
+// Forward state of one tile that the backward needs again.
+struct FwdTile {
+    half8 x[2];      // B operands of layer 1 (natural order, features 16q+8h+j)
+    half8 y1[2][2];  // relu(Y1) as B operands [t][q]
+    half8 hb;        // h (16 features, perm order) = rgb-input k-step 1
+    half8 sh;        // SH (natural order 8h+j)    = rgb-input k-step 0
+    half8 r1[2][2];
+    half8 r2[2][2];
+    float h0;        // h[0] (f16-rounded) on lanes h==0
+    float rgb[3];    // sigmoid outputs on lanes h==0 (fp32)
+};
+
+template <bool DENSITY_ONLY>
+__device__ __forceinline__ void forward_tile(const _Float16* lds, int lane, const _Float16* __restrict__ feat,
+                                             const float* __restrict__ dirs, int64_t s, bool valid, FwdTile& T) {
+    const int h = lane >> 5;
+    const f32x16 z = {};
+    if (valid) {
+        const half8* row = reinterpret_cast<const half8*>(feat + s * 32);
+        T.x[0] = row[h];
+        T.x[1] = row[2 + h];
+    } else {
+        T.x[0] = half8{}; T.x[1] = half8{};
+    }
+    // xyz layer 1: Y1^T = W1 X^T
+    f32x16 y1a = mfma(lds_frag(lds, F1 + 0, lane), T.x[0], z);
+    y1a = mfma(lds_frag(lds, F1 + 1, lane), T.x[1], y1a);
+    f32x16 y1b = mfma(lds_frag(lds, F1 + 2, lane), T.x[0], z);
+    y1b = mfma(lds_frag(lds, F1 + 3, lane), T.x[1], y1b);
+    T.y1[0][0] = pack8<0, true>(y1a); T.y1[0][1] = pack8<8, true>(y1a);
+    T.y1[1][0] = pack8<0, true>(y1b); T.y1[1][1] = pack8<8, true>(y1b);
+    // xyz layer 2: H^T = W2 relu(Y1)^T (rows 0..15 valid)
+    f32x16 ha = mfma(lds_frag(lds, F2 + 0, lane), T.y1[0][0], z);
+    ha = mfma(lds_frag(lds, F2 + 1, lane), T.y1[0][1], ha);
+    ha = mfma(lds_frag(lds, F2 + 2, lane), T.y1[1][0], ha);
+    ha = mfma(lds_frag(lds, F2 + 3, lane), T.y1[1][1], ha);
+    T.hb = pack8<0, false>(ha);   // the fp16 network output of tcnn
+    T.h0 = (float)T.hb[0];        // row 0 on lanes h==0
+    if (DENSITY_ONLY) return;
+    float shv[16];
+    if (valid) sh4(dirs[3 * s], dirs[3 * s + 1], dirs[3 * s + 2], shv);
+    else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) shv[i] = 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) T.sh[j] = (_Float16)(h ? shv[8 + j] : shv[j]);
+    // rgb layer 1
+    f32x16 r1a = mfma(lds_frag(lds, F3 + 0, lane), T.sh, z);
+    r1a = mfma(lds_frag(lds, F3 + 1, lane), T.hb, r1a);
+    f32x16 r1b = mfma(lds_frag(lds, F3 + 2, lane), T.sh, z);
+    r1b = mfma(lds_frag(lds, F3 + 3, lane), T.hb, r1b);
+    T.r1[0][0] = pack8<0, true>(r1a); T.r1[0][1] = pack8<8, true>(r1a);
+    T.r1[1][0] = pack8<0, true>(r1b); T.r1[1][1] = pack8<8, true>(r1b);
+    // rgb layer 2
+    f32x16 r2a = z, r2b = z;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            r2a = mfma(lds_frag(lds, F4 + 0 * 4 + t * 2 + q, lane), T.r1[t][q], r2a);
+            r2b = mfma(lds_frag(lds, F4 + 1 * 4 + t * 2 + q, lane), T.r1[t][q], r2b);
+        }
+    T.r2[0][0] = pack8<0, true>(r2a); T.r2[0][1] = pack8<8, true>(r2a);
+    T.r2[1][0] = pack8<0, true>(r2b); T.r2[1][1] = pack8<8, true>(r2b);
+    // rgb layer 3 (rows 0..2 = rgb logits on lanes h==0)
+    f32x16 o = z;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) o = mfma(lds_frag(lds, F5 + t * 2 + q, lane), T.r2[t][q], o);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) T.rgb[c] = 1.0f / (1.0f + __expf(-o[c]));
+}
+
+__device__ __forceinline__ void load_frags(_Float16* lds, const _Float16* __restrict__ packed, int n_frags) {
+    const uint4* src = reinterpret_cast<const uint4*>(packed);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    for (int i = threadIdx.x; i < n_frags * 64; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+}
+
+template <bool DENSITY_ONLY>
+__global__ __launch_bounds__(FIELD_BLOCK) void field_fw_kernel(const _Float16* __restrict__ feat,
+                                                                const float* __restrict__ dirs, int64_t n,
+                                                                const int32_t* __restrict__ n_dev,
+                                                                const _Float16* __restrict__ packed,
+                                                                float* __restrict__ sigma, float* __restrict__ rgb) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    _Float16* lds = reinterpret_cast<_Float16*>(smem);
+    load_frags(lds, packed, DENSITY_ONLY ? 8 : 24);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
+    const int64_t tiles = div_up<int64_t>(nn, 32);
+    for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile < tiles; tile += (int64_t)gridDim.x * 4) {
+        const int64_t s = tile * 32 + r;
+        const bool valid = s < nn;
+        FwdTile T;
+        forward_tile<DENSITY_ONLY>(lds, lane, feat, dirs, s, valid, T);
+        if (valid && h == 0) {
+            sigma[s] = __expf(T.h0);  // TruncExp forward (custom_functions.py:166)
+            if (!DENSITY_ONLY) {
+                // tcnn returns fp16 rgb; the reference casts it to fp32 for compositing
+                rgb[3 * s] = (float)(_Float16)T.rgb[0];
+                rgb[3 * s + 1] = (float)(_Float16)T.rgb[1];
+                rgb[3 * s + 2] = (float)(_Float16)T.rgb[2];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- backward
+
+constexpr int TP_STRIDE = 40;  // halfs per LDS transpose row (32 samples + 8 pad: 80 B)
+
+// write an accumulator tile (rows = channels 32*mt + (i&3)+8(i>>2)+4h, col = sample r) as f16 [ch][sample]
+template <int I0, int I1>
+__device__ __forceinline__ void tp_store_acc(_Float16* buf, const f32x16& a, int ch0, int r, int h) {
+#pragma unroll
+    for (int i = I0; i < I1; ++i) buf[(ch0 + (i & 3) + 8 * (i >> 2) + 4 * h) * TP_STRIDE + r] = (_Float16)a[i];
+}
+// write a packed operand (element j = channel kbase + k_of(j,h,perm)) as [ch][sample]
+__device__ __forceinline__ void tp_store_op(_Float16* buf, const half8& v, int kbase, int perm, int r, int h) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) buf[(kbase + k_of(j, h, perm)) * TP_STRIDE + r] = v[j];
+}
+__device__ __forceinline__ half8 tp_frag(const _Float16* buf, int row0, int q, int lane) {
+    const int r = lane & 31, h = lane >> 5;
+    return *reinterpret_cast<const half8*>(buf + (row0 + r) * TP_STRIDE + 16 * q + 8 * h);
+}
+__device__ __forceinline__ void lds_sync_wave() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// dW tile accumulate with v_mfma_f32_16x16x32_f16 (K = the tile's 32 samples in one instruction):
+// acc[16x16] += A(buf_a rows 16*MT.., samples) x B(buf_b rows 16*NT.., samples)^T
+__device__ __forceinline__ half8 tp_frag16(const _Float16* buf, int row0, int lane) {
+    return *reinterpret_cast<const half8*>(buf + (row0 + (lane & 15)) * TP_STRIDE + 8 * (lane >> 4));
+}
+#define DW16(ACC, BA, MT, BB, NT) \
+    ACC = __builtin_amdgcn_mfma_f32_16x16x32_f16(tp_frag16(BA, 16 * (MT), lane), tp_frag16(BB, 16 * (NT), lane), ACC, 0, 0, 0)
+
+constexpr int N_DW = N_XYZ_PARAMS + N_RGB_PARAMS;  // 10240 floats per slab row
+
+// add one 16x16 dW tile (D row = 4*(lane>>4)+i, col = lane&15) into a row-major fp32 LDS image
+__device__ __forceinline__ void dw_add16(float* img, const f32x4& a, int mt, int nt, int rows, int cols, int lane) {
+    const int col = 16 * nt + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = 16 * mt + 4 * (lane >> 4) + i;
+        if (row < rows && col < cols) atomicAdd(img + row * cols + col, a[i]);
+    }
+}
+
+__global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
+    const _Float16* __restrict__ feat, const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev,
+    const _Float16* __restrict__ packed, const float* __restrict__ dL_dsigma, const float* __restrict__ dL_drgb,
+    float grad_scale, float* __restrict__ dL_dfeat, float* __restrict__ slab) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    _Float16* lds = reinterpret_cast<_Float16*>(smem);
+    load_frags(lds, packed, N_FRAGS);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    // per-wave transpose buffers: A (64 ch x 40) and B (64 ch x 40) f16
+    _Float16* ta = lds + N_FRAGS * FRAG_HALFS + wid * (2 * 64 * TP_STRIDE);
+    _Float16* tb = ta + 64 * TP_STRIDE;
+    const float S = grad_scale, invS = 1.0f / grad_scale;
+    const f32x16 z = {};
+    // persistent weight-gradient accumulators, 16x16 tiles [m-tile][n-tile] (160 registers)
+    f32x4 dw1[4][2], dw2[4], dwr1[4][2], dwr2[4][4], dwr3[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        dw2[a] = f32x4{}; dwr3[a] = f32x4{};
+#pragma unroll
+        for (int b = 0; b < 2; ++b) { dw1[a][b] = f32x4{}; dwr1[a][b] = f32x4{}; }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) dwr2[a][b] = f32x4{};
+    }
+
+    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
+    const int64_t tiles = div_up<int64_t>(nn, 32);
+    for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile < tiles; tile += (int64_t)gridDim.x * 4) {
+        const int64_t s = tile * 32 + r;
+        const bool valid = s < nn;
+        FwdTile T;
+        forward_tile<false>(lds, lane, feat, dirs, s, valid, T);
+        float gs = 0.0f, g0 = 0.0f, g1 = 0.0f, g2 = 0.0f;
+        if (valid && h == 0) {
+            gs = dL_dsigma[s];
+            g0 = dL_drgb[3 * s]; g1 = dL_drgb[3 * s + 1]; g2 = dL_drgb[3 * s + 2];
+        }
+        // Layer by layer, each weight gradient right after its data gradient, so at most two dY
+        // tiles are live next to the 12 persistent dW accumulators.
+        // -- rgb layer 3: dO (rows 0..2 on lanes h==0) = dL/drgb * sigmoid'
+        f32x16 dO = z;
+        if (h == 0) {
+            dO[0] = g0 * S * T.rgb[0] * (1.0f - T.rgb[0]);
+            dO[1] = g1 * S * T.rgb[1] * (1.0f - T.rgb[1]);
+            dO[2] = g2 * S * T.rgb[2] * (1.0f - T.rgb[2]);
+        }
+        const half8 dOb = pack8<0, false>(dO);
+        //    dWr3 (16xW) += dO^T R2   (A rows 0..31 of dO: rows >= 3 are zero)
+        tp_store_acc<0, 16>(ta, dO, 0, r, h);
+        tp_store_op(tb, T.r2[0][0], 0, 1, r, h); tp_store_op(tb, T.r2[0][1], 16, 1, r, h);
+        tp_store_op(tb, T.r2[1][0], 32, 1, r, h); tp_store_op(tb, T.r2[1][1], 48, 1, r, h);
+        lds_sync_wave();
+        #pragma unroll
+        for (int b = 0; b < 4; ++b) DW16(dwr3[b], ta, 0, tb, b);
+        lds_sync_wave();
+        //    dR2 = Wr3^T dO, masked by R2 > 0
+        half8 dr2p[2][2];
+        {
+            f32x16 a0 = mfma(lds_frag(lds, B5 + 0, lane), dOb, z);
+            f32x16 a1 = mfma(lds_frag(lds, B5 + 1, lane), dOb, z);
+            relu_mask<0>(a0, T.r2[0][0]); relu_mask<8>(a0, T.r2[0][1]);
+            relu_mask<0>(a1, T.r2[1][0]); relu_mask<8>(a1, T.r2[1][1]);
+            dr2p[0][0] = pack8<0, false>(a0); dr2p[0][1] = pack8<8, false>(a0);
+            dr2p[1][0] = pack8<0, false>(a1); dr2p[1][1] = pack8<8, false>(a1);
+        }
+        // -- rgb layer 2: dWr2 (WxW) += dR2^T R1
+        tp_store_op(ta, dr2p[0][0], 0, 1, r, h); tp_store_op(ta, dr2p[0][1], 16, 1, r, h);
+        tp_store_op(ta, dr2p[1][0], 32, 1, r, h); tp_store_op(ta, dr2p[1][1], 48, 1, r, h);
+        tp_store_op(tb, T.r1[0][0], 0, 1, r, h); tp_store_op(tb, T.r1[0][1], 16, 1, r, h);
+        tp_store_op(tb, T.r1[1][0], 32, 1, r, h); tp_store_op(tb, T.r1[1][1], 48, 1, r, h);
+        lds_sync_wave();
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) DW16(dwr2[a][b], ta, a, tb, b);
+        lds_sync_wave();
+        //    dR1 = Wr2^T dR2, masked by R1 > 0
+        half8 dr1p[2][2];
+        {
+            f32x16 a0 = z, a1 = z;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    a0 = mfma(lds_frag(lds, B4 + 0 * 4 + t * 2 + q, lane), dr2p[t][q], a0);
+                    a1 = mfma(lds_frag(lds, B4 + 1 * 4 + t * 2 + q, lane), dr2p[t][q], a1);
+                }
+            relu_mask<0>(a0, T.r1[0][0]); relu_mask<8>(a0, T.r1[0][1]);
+            relu_mask<0>(a1, T.r1[1][0]); relu_mask<8>(a1, T.r1[1][1]);
+            dr1p[0][0] = pack8<0, false>(a0); dr1p[0][1] = pack8<8, false>(a0);
+            dr1p[1][0] = pack8<0, false>(a1); dr1p[1][1] = pack8<8, false>(a1);
+        }
+        // -- rgb layer 1: dWr1 (Wx32) += dR1^T [SH;h]
+        tp_store_op(ta, dr1p[0][0], 0, 1, r, h); tp_store_op(ta, dr1p[0][1], 16, 1, r, h);
+        tp_store_op(ta, dr1p[1][0], 32, 1, r, h); tp_store_op(ta, dr1p[1][1], 48, 1, r, h);
+        tp_store_op(tb, T.sh, 0, 0, r, h); tp_store_op(tb, T.hb, 16, 1, r, h);
+        lds_sync_wave();
+        #pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) DW16(dwr1[a][b], ta, a, tb, b);
+        lds_sync_wave();
+        //    d[SH;h] = Wr1^T dR1 (rows 16..31 = dh) + TruncExp backward into h[0]
+        half8 dhb;
+        {
+            f32x16 dsh = z;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) dsh = mfma(lds_frag(lds, B3 + t * 2 + q, lane), dr1p[t][q], dsh);
+            // row 16 = reg 8 on lanes h==0: g * exp(clamp(h0,-15,15)) (custom_functions.py:170-173)
+            if (h == 0) dsh[8] += gs * S * __expf(fminf(fmaxf(T.h0, -15.0f), 15.0f));
+            dhb = pack8<8, false>(dsh);
+        }
+        // -- xyz layer 2: dW2 (16x64) += dh^T Y1 (A rows 0..15 = dh, rows 16..31 = 0)
+        tp_store_op(ta, dhb, 0, 1, r, h);
+        tp_store_op(ta, half8{}, 16, 1, r, h);
+        tp_store_op(tb, T.y1[0][0], 0, 1, r, h); tp_store_op(tb, T.y1[0][1], 16, 1, r, h);
+        tp_store_op(tb, T.y1[1][0], 32, 1, r, h); tp_store_op(tb, T.y1[1][1], 48, 1, r, h);
+        lds_sync_wave();
+        #pragma unroll
+        for (int b = 0; b < 4; ++b) DW16(dw2[b], ta, 0, tb, b);
+        lds_sync_wave();
+        //    dY1 = W2^T dh, masked by Y1 > 0
+        half8 dy1p[2][2];
+        {
+            f32x16 a0 = mfma(lds_frag(lds, B2 + 0, lane), dhb, z);
+            f32x16 a1 = mfma(lds_frag(lds, B2 + 1, lane), dhb, z);
+            relu_mask<0>(a0, T.y1[0][0]); relu_mask<8>(a0, T.y1[0][1]);
+            relu_mask<0>(a1, T.y1[1][0]); relu_mask<8>(a1, T.y1[1][1]);
+            dy1p[0][0] = pack8<0, false>(a0); dy1p[0][1] = pack8<8, false>(a0);
+            dy1p[1][0] = pack8<0, false>(a1); dy1p[1][1] = pack8<8, false>(a1);
+        }
+        // -- xyz layer 1: dW1 (64x32) += dY1^T X
+        tp_store_op(ta, dy1p[0][0], 0, 1, r, h); tp_store_op(ta, dy1p[0][1], 16, 1, r, h);
+        tp_store_op(ta, dy1p[1][0], 32, 1, r, h); tp_store_op(ta, dy1p[1][1], 48, 1, r, h);
+        tp_store_op(tb, T.x[0], 0, 0, r, h); tp_store_op(tb, T.x[1], 16, 0, r, h);
+        lds_sync_wave();
+        #pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) DW16(dw1[a][b], ta, a, tb, b);
+        lds_sync_wave();
+        //    dX = W1^T dY1 -> global fp32 (features (i&3)+8(i>>2)+4h)
+        {
+            f32x16 dx = z;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) dx = mfma(lds_frag(lds, B1 + t * 2 + q, lane), dy1p[t][q], dx);
+            if (valid) {
+                float4* dst = reinterpret_cast<float4*>(dL_dfeat + s * 32);
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    dst[2 * g + h] = make_float4(dx[4 * g] * invS, dx[4 * g + 1] * invS, dx[4 * g + 2] * invS,
+                                                 dx[4 * g + 3] * invS);
+            }
+        }
+    }
+
+    // ---- block reduction of the per-wave dW partials into an fp32 LDS image, then one slab row
+    __syncthreads();
+    float* img = reinterpret_cast<float*>(smem);  // reuses the fragment area (N_DW*4 <= frags+buffers)
+    for (int i = threadIdx.x; i < N_DW; i += blockDim.x) img[i] = 0.0f;
+    __syncthreads();
+    float* ix = img;
+    float* ir = img + N_XYZ_PARAMS;
+    float* ir2 = ir + RGB_W * 32;
+    float* ir3 = ir2 + RGB_W * RGB_W;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        dw_add16(ix + 64 * 32, dw2[a], 0, a, 16, 64, lane);
+        dw_add16(ir3, dwr3[a], 0, a, 16, RGB_W, lane);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            dw_add16(ix, dw1[a][b], a, b, 64, 32, lane);
+            dw_add16(ir, dwr1[a][b], a, b, RGB_W, 32, lane);
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) dw_add16(ir2, dwr2[a][b], a, b, RGB_W, RGB_W, lane);
+    }
+    __syncthreads();
+    float* row = slab + (int64_t)blockIdx.x * N_DW;
+    for (int i = threadIdx.x; i < N_DW; i += blockDim.x) row[i] = img[i] * invS;
+}
+
+// grad[p] += sum over slab rows (fixed order: deterministic)
+__global__ void slab_reduce_kernel(const float* __restrict__ slab, int rows, float* __restrict__ gx,
+                                   float* __restrict__ gr) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N_DW) return;
+    float acc = 0.0f;
+    for (int b = 0; b < rows; ++b) acc += slab[(int64_t)b * N_DW + p];
+    if (p < N_XYZ_PARAMS) gx[p] += acc;
+    else gr[p - N_XYZ_PARAMS] += acc;
+}
+
+constexpr int BW_BLOCKS = 256;
+constexpr size_t BW_LDS = (size_t)N_FRAGS * FRAG_HALFS * 2 + 4 * 2 * 64 * TP_STRIDE * 2;
+static_assert((size_t)N_DW * 4 <= BW_LDS, "reduction image must fit the bw LDS");
+
+// debug: one MFMA with A (32x16) and B (16x32) f16 row-major -> D (32x32) f32, to pin the lane maps
+__global__ void mfma_probe_kernel(const _Float16* A, const _Float16* B, float* D) {
+    const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+    half8 a, b;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { a[j] = A[r * 16 + 8 * h + j]; b[j] = B[(8 * h + j) * 32 + r]; }
+    f32x16 c = {};
+    c = mfma(a, b, c);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) D[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = c[i];
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t mfnerf_field_packed_bytes(int rgb_width) {
+    if (rgb_width != RGB_W) return -1;
+    return (int64_t)N_FRAGS * FRAG_HALFS * 2;
+}
+
+int mfnerf_field_pack_weights(const float* params_xyz, const float* params_rgb, int rgb_width, void* packed,
+                              mfnerf_stream_t stream) {
+    if (rgb_width != RGB_W) { mfn_set_error("field: rgb_width=%d unsupported (this build: %d)", rgb_width, RGB_W); return MFN_ERR_INVALID; }
+    if (!params_xyz || !params_rgb || !packed) { mfn_set_error("field_pack_weights: null pointer"); return MFN_ERR_INVALID; }
+    const int total = N_FRAGS * FRAG_HALFS;
+    hipLaunchKernelGGL(pack_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, params_xyz, params_rgb,
+                       (_Float16*)packed);
+    return mfn_check_launch("field_pack_weights");
+}
+
+int mfnerf_field_fw(const void* feat_f16, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
+                    int rgb_width, int density_only, float* sigma, float* rgb, mfnerf_stream_t stream) {
+    if (rgb_width != RGB_W) { mfn_set_error("field: rgb_width=%d unsupported (this build: %d)", rgb_width, RGB_W); return MFN_ERR_INVALID; }
+    if (n < 0) { mfn_set_error("field_fw: bad size"); return MFN_ERR_INVALID; }
+    if (n == 0) return MFN_OK;
+    if (!feat_f16 || !packed || !sigma || (!density_only && (!dirs || !rgb))) {
+        mfn_set_error("field_fw: null pointer"); return MFN_ERR_INVALID;
+    }
+    const int64_t tiles = div_up<int64_t>(n, 32);
+    const int64_t want = div_up<int64_t>(tiles, 4);
+    const unsigned blocks = (unsigned)(want < 2048 ? want : 2048);
+    if (density_only)
+        hipLaunchKernelGGL(field_fw_kernel<true>, dim3(blocks), dim3(FIELD_BLOCK), 8 * FRAG_HALFS * 2, stream,
+                           (const _Float16*)feat_f16, dirs, n, n_dev, (const _Float16*)packed, sigma, rgb);
+    else
+        hipLaunchKernelGGL(field_fw_kernel<false>, dim3(blocks), dim3(FIELD_BLOCK), 24 * FRAG_HALFS * 2, stream,
+                           (const _Float16*)feat_f16, dirs, n, n_dev, (const _Float16*)packed, sigma, rgb);
+    return mfn_check_launch("field_fw");
+}
+
+int64_t mfnerf_field_bw_workspace(int64_t n, int rgb_width) {
+    (void)n;
+    if (rgb_width != RGB_W) return -1;
+    return (int64_t)BW_BLOCKS * N_DW * 4;
+}
+
+int mfnerf_field_bw(const void* feat_f16, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
+                    int rgb_width, const float* dL_dsigma, const float* dL_drgb, float grad_scale, float* dL_dfeat,
+                    float* grad_xyz, float* grad_rgb, void* workspace, mfnerf_stream_t stream) {
+    if (rgb_width != RGB_W) { mfn_set_error("field: rgb_width=%d unsupported (this build: %d)", rgb_width, RGB_W); return MFN_ERR_INVALID; }
+    if (n < 0 || !(grad_scale > 0.0f)) { mfn_set_error("field_bw: bad size or grad_scale"); return MFN_ERR_INVALID; }
+    if (n == 0) return MFN_OK;
+    if (!feat_f16 || !dirs || !packed || !dL_dsigma || !dL_drgb || !dL_dfeat || !grad_xyz || !grad_rgb || !workspace) {
+        mfn_set_error("field_bw: null pointer"); return MFN_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(field_bw_kernel, dim3(BW_BLOCKS), dim3(FIELD_BLOCK), BW_LDS, stream, (const _Float16*)feat_f16,
+                       dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb, grad_scale, dL_dfeat,
+                       (float*)workspace);
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((N_DW + 255) / 256), dim3(256), 0, stream, (const float*)workspace,
+                       BW_BLOCKS, grad_xyz, grad_rgb);
+    return mfn_check_launch("field_bw");
+}
+
+int mfnerf_debug_mfma_probe(const void* A, const void* B, float* D, mfnerf_stream_t stream) {
+    hipLaunchKernelGGL(mfma_probe_kernel, dim3(1), dim3(64), 0, stream, (const _Float16*)A, (const _Float16*)B, D);
+    return mfn_check_launch("mfma_probe");
+}
+
+}  // extern "C"

@@ -1,0 +1,187 @@
+// grid.hip -- multiresolution grid encoding (tiny-cuda-nn HashGrid semantics, plus this repo's
+// MixedFeature shared-table variant) forward and backward on gfx950.
+//
+// Forward: 4 lanes per point, each lane owns 4 consecutive levels (8 f16 features = one 16-B
+// store), so the 4 lanes of a point write its 64-B output row with one coalesced 64-B burst and
+// every lane keeps 32 independent 4-B corner gathers in flight.  Accumulation is fp32 (tcnn
+// accumulates in half; the difference is inside the fp16 output rounding).
+// Backward: 16 lanes per point (one level each), fp32 dL/dy read as one 128-B row per point,
+// two no-return global_atomic_add_f32 per corner (features f0,f1 of the same entry share a
+// 64-B line).
+#include "common.hpp"
+#include "../../include/mfnerf.h"
+
+using namespace mfn;
+
+namespace {
+
+constexpr uint32_t PRIME1 = 2654435761u, PRIME2 = 805459861u;
+
+struct LevelGeo {
+    uint32_t g[3];  // floor(pos)
+    float w[3];     // pos - floor(pos)
+};
+
+// tcnn pos_fract (grid.h): pos = fmaf(scale, x, 0.5f); g = floor(pos); w = pos - g  (Linear)
+__device__ __forceinline__ LevelGeo level_geo(float scale, float x, float y, float z) {
+    LevelGeo L;
+    const float px = fmaf(scale, x, 0.5f), py = fmaf(scale, y, 0.5f), pz = fmaf(scale, z, 0.5f);
+    const float fx = floorf(px), fy = floorf(py), fz = floorf(pz);
+    L.g[0] = (uint32_t)(int)fx; L.g[1] = (uint32_t)(int)fy; L.g[2] = (uint32_t)(int)fz;
+    L.w[0] = px - fx; L.w[1] = py - fy; L.w[2] = pz - fz;
+    return L;
+}
+
+// tcnn grid_index: dense strides while res^3 <= size, else the coherent prime hash; `% size`.
+// MixedFeature shared tables hash the point's coordinates on the canonical grid.
+__device__ __forceinline__ uint32_t corner_index(const mfnerf_grid_desc& D, int l, uint32_t x, uint32_t y,
+                                                 uint32_t z) {
+    const uint32_t res = D.res[l], size = D.size[l];
+    uint32_t idx;
+    if (D.table_kind[l] == 1) {
+        const uint32_t rc = (uint32_t)D.canon_res;
+        x = (uint32_t)(((uint64_t)x * rc) / res);
+        y = (uint32_t)(((uint64_t)y * rc) / res);
+        z = (uint32_t)(((uint64_t)z * rc) / res);
+        idx = (x * 1u) ^ (y * PRIME1) ^ (z * PRIME2);
+    } else if ((uint64_t)res * res * res <= size) {
+        idx = x + y * res + z * res * res;
+    } else {
+        idx = (x * 1u) ^ (y * PRIME1) ^ (z * PRIME2);
+    }
+    if ((size & (size - 1)) == 0) return idx & (size - 1);
+    return idx < size ? idx : idx % size;
+}
+
+__device__ __forceinline__ float corner_weight(const LevelGeo& L, int c) {
+    float w = 1.0f;
+    w *= (c & 1) ? L.w[0] : (1.0f - L.w[0]);
+    w *= (c & 2) ? L.w[1] : (1.0f - L.w[1]);
+    w *= (c & 4) ? L.w[2] : (1.0f - L.w[2]);
+    return w;
+}
+
+constexpr int ENC_BLOCK = 256;
+constexpr int LEVELS_PER_LANE = 4;
+
+// out row = 32 halfs (L=16, F=2); requires n_levels % 4 == 0 and F == 2.
+__global__ __launch_bounds__(ENC_BLOCK) void grid_fw_kernel(const float* __restrict__ X, int64_t n,
+                                                             const int32_t* __restrict__ n_dev, float x_min,
+                                                             float x_range, const mfnerf_grid_desc D,
+                                                             const __half2* __restrict__ table,
+                                                             __half* __restrict__ out) {
+    const int groups = D.n_levels / LEVELS_PER_LANE;
+    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
+    const int64_t total = nn * groups;
+    for (int64_t t = (int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x; t < total; t += (int64_t)gridDim.x * ENC_BLOCK) {
+    const int64_t i = t / groups;
+    const int grp = (int)(t - i * groups);
+    const float x = (X[3 * i] - x_min) / x_range;
+    const float y = (X[3 * i + 1] - x_min) / x_range;
+    const float z = (X[3 * i + 2] - x_min) / x_range;
+    float acc[2 * LEVELS_PER_LANE];
+#pragma unroll
+    for (int k = 0; k < LEVELS_PER_LANE; ++k) {
+        const int l = grp * LEVELS_PER_LANE + k;
+        const LevelGeo L = level_geo(D.scale[l], x, y, z);
+        const __half2* tab = table + D.offset[l];
+        __half2 v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+            v[c] = tab[corner_index(D, l, L.g[0] + (c & 1), L.g[1] + ((c >> 1) & 1), L.g[2] + ((c >> 2) & 1))];
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const float w = corner_weight(L, c);
+            const float2 f = __half22float2(v[c]);
+            a0 = fmaf(w, f.x, a0);
+            a1 = fmaf(w, f.y, a1);
+        }
+        acc[2 * k] = a0; acc[2 * k + 1] = a1;
+    }
+    __half2 h[LEVELS_PER_LANE];
+#pragma unroll
+    for (int k = 0; k < LEVELS_PER_LANE; ++k) h[k] = __floats2half2_rn(acc[2 * k], acc[2 * k + 1]);
+    uint4 pk;
+    pk.x = *reinterpret_cast<uint32_t*>(&h[0]); pk.y = *reinterpret_cast<uint32_t*>(&h[1]);
+    pk.z = *reinterpret_cast<uint32_t*>(&h[2]); pk.w = *reinterpret_cast<uint32_t*>(&h[3]);
+    reinterpret_cast<uint4*>(out + i * (2 * D.n_levels))[grp] = pk;
+    }
+}
+
+__global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restrict__ X, int64_t n,
+                                                             const int32_t* __restrict__ n_dev, float x_min,
+                                                             float x_range, const mfnerf_grid_desc D,
+                                                             const float* __restrict__ dy, float* __restrict__ grad) {
+    const int L_ = D.n_levels;
+    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
+    const int64_t total = nn * L_;
+    for (int64_t t = (int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x; t < total; t += (int64_t)gridDim.x * ENC_BLOCK) {
+    const int64_t i = t / L_;
+    const int l = (int)(t - i * L_);
+    const float2 g = reinterpret_cast<const float2*>(dy + i * (2 * L_))[l];
+    if (g.x == 0.0f && g.y == 0.0f) continue;
+    const float x = (X[3 * i] - x_min) / x_range;
+    const float y = (X[3 * i + 1] - x_min) / x_range;
+    const float z = (X[3 * i + 2] - x_min) / x_range;
+    const LevelGeo Lg = level_geo(D.scale[l], x, y, z);
+    float* gt = grad + 2 * (int64_t)D.offset[l];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const uint32_t idx = corner_index(D, l, Lg.g[0] + (c & 1), Lg.g[1] + ((c >> 1) & 1), Lg.g[2] + ((c >> 2) & 1));
+        const float w = corner_weight(Lg, c);
+        __hip_atomic_fetch_add(gt + 2 * idx, w * g.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(gt + 2 * idx + 1, w * g.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    }
+}
+
+int check_desc(const mfnerf_grid_desc* d, const char* what) {
+    if (!d) { mfn_set_error("%s: null grid desc", what); return MFN_ERR_INVALID; }
+    if (d->n_features != 2 || d->n_levels <= 0 || d->n_levels > MFN_MAX_LEVELS || d->n_levels % 4 != 0) {
+        mfn_set_error("%s: unsupported grid (n_features=%d must be 2, n_levels=%d must be a multiple of 4 <= %d)",
+                      what, d->n_features, d->n_levels, MFN_MAX_LEVELS);
+        return MFN_ERR_INVALID;
+    }
+    for (int l = 0; l < d->n_levels; ++l)
+        if (d->size[l] == 0 || d->res[l] == 0 || d->table_kind[l] < 0 || d->table_kind[l] > 1) {
+            mfn_set_error("%s: bad level %d", what, l); return MFN_ERR_INVALID;
+        }
+    return MFN_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mfnerf_grid_encode_fw(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                          const mfnerf_grid_desc* desc, const void* table_f16, void* out_f16,
+                          mfnerf_stream_t stream) {
+    int st = check_desc(desc, "grid_encode_fw");
+    if (st) return st;
+    if (n < 0) { mfn_set_error("grid_encode_fw: bad size"); return MFN_ERR_INVALID; }
+    if (n == 0) return MFN_OK;
+    if (!x || !table_f16 || !out_f16) { mfn_set_error("grid_encode_fw: null pointer"); return MFN_ERR_INVALID; }
+    const int64_t want = div_up<int64_t>(n * (desc->n_levels / LEVELS_PER_LANE), ENC_BLOCK);
+    const int64_t blocks = want < 8192 ? want : 8192;
+    hipLaunchKernelGGL(grid_fw_kernel, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0,
+                       stream, x, n, n_dev, x_min, x_range, *desc, (const __half2*)table_f16, (__half*)out_f16);
+    return mfn_check_launch("grid_encode_fw");
+}
+
+int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                          const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
+                          mfnerf_stream_t stream) {
+    int st = check_desc(desc, "grid_encode_bw");
+    if (st) return st;
+    if (n < 0) { mfn_set_error("grid_encode_bw: bad size"); return MFN_ERR_INVALID; }
+    if (n == 0) return MFN_OK;
+    if (!x || !dL_dout || !grad_table) { mfn_set_error("grid_encode_bw: null pointer"); return MFN_ERR_INVALID; }
+    const int64_t want = div_up<int64_t>(n * desc->n_levels, ENC_BLOCK);
+    const int64_t blocks = want < 16384 ? want : 16384;
+    hipLaunchKernelGGL(grid_bw_kernel, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0,
+                       stream, x, n, n_dev, x_min, x_range, *desc, dL_dout, grad_table);
+    return mfn_check_launch("grid_encode_bw");
+}
+
+}  // extern "C"

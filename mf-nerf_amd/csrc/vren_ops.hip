@@ -1,0 +1,552 @@
+// vren_ops.hip -- gfx950 kernels for the reference's `vren` op set (models/csrc/*.cu) and their
+// C-ABI entry points (include/mfnerf.h).  Kernel arithmetic follows the reference statement by
+// statement (see common.hpp for the fp contract); launch geometry and data flow are MI355X-first:
+//   * ray-level kernels use 64-thread workgroups (one wave) so a 8192-ray batch spreads over 128
+//     CUs instead of 32 workgroups of 256;
+//   * raymarching_train is count -> one-workgroup prefix scan -> write, with the sample count kept
+//     on the device (no host sync, graph-capturable) and rays_a in canonical ray order;
+//   * compositing writes every sample of every ray exactly once (zeros after termination), so no
+//     n_samples-sized memsets are needed; the backward's per-ray scan runs in registers.
+#include "common.hpp"
+#include "../../include/mfnerf.h"
+
+using namespace mfn;
+
+namespace {
+
+constexpr int RAY_BLOCK = 64;
+
+// ------------------------------------------------------------------ ray / AABB (intersection.cu:5-56)
+__global__ void ray_aabb_kernel(const float* __restrict__ o, const float* __restrict__ d,
+                                const float* __restrict__ centers, const float* __restrict__ half_sizes,
+                                int64_t n_rays, int64_t n_vox, int max_hits, int32_t* __restrict__ hit_cnt,
+                                float* __restrict__ hits_t, int64_t* __restrict__ hits_idx) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rays) return;
+    const float ox = o[3 * r], oy = o[3 * r + 1], oz = o[3 * r + 2];
+    const float ix = 1.0f / d[3 * r], iy = 1.0f / d[3 * r + 1], iz = 1.0f / d[3 * r + 2];
+    float* ht = hits_t + r * max_hits * 2;
+    int64_t* hi = hits_idx + r * max_hits;
+    for (int k = 0; k < max_hits; ++k) { ht[2 * k] = -1.0f; ht[2 * k + 1] = -1.0f; hi[k] = -1; }
+    int cnt = 0;
+    for (int64_t v = 0; v < n_vox; ++v) {
+        const float cx = centers[3 * v], cy = centers[3 * v + 1], cz = centers[3 * v + 2];
+        const float hx = half_sizes[3 * v], hy = half_sizes[3 * v + 1], hz = half_sizes[3 * v + 2];
+        const float tminx = (cx - hx - ox) * ix, tminy = (cy - hy - oy) * iy, tminz = (cz - hz - oz) * iz;
+        const float tmaxx = (cx + hx - ox) * ix, tmaxy = (cy + hy - oy) * iy, tmaxz = (cz + hz - oz) * iz;
+        float t1 = fmaxf(fmaxf(fminf(tminx, tmaxx), fminf(tminy, tmaxy)), fminf(tminz, tmaxz));
+        float t2 = fminf(fminf(fmaxf(tminx, tmaxx), fmaxf(tminy, tmaxy)), fmaxf(tminz, tmaxz));
+        if (t1 > t2) { t1 = -1.0f; t2 = -1.0f; }
+        if (t2 > 0) {
+            if (cnt < max_hits) { ht[2 * cnt] = fmaxf(t1, 0.0f); ht[2 * cnt + 1] = t2; hi[cnt] = v; }
+            cnt++;
+        }
+    }
+    hit_cnt[r] = cnt;
+    // the reference sorts all max_hits slots by t1 (intersection.cu:95-97): unfilled slots (t1=-1)
+    // come first, then the real hits ascending.  Insertion sort of the k real hits, then shift right.
+    const int k = min(cnt, max_hits);
+    for (int i = 1; i < k; ++i) {
+        const float a = ht[2 * i], b = ht[2 * i + 1]; const int64_t c = hi[i];
+        int j = i - 1;
+        while (j >= 0 && ht[2 * j] > a) { ht[2 * j + 2] = ht[2 * j]; ht[2 * j + 3] = ht[2 * j + 1]; hi[j + 1] = hi[j]; --j; }
+        ht[2 * j + 2] = a; ht[2 * j + 3] = b; hi[j + 1] = c;
+    }
+    const int sh = max_hits - k;
+    if (sh > 0 && k > 0) {
+        for (int i = k - 1; i >= 0; --i) {
+            ht[2 * (i + sh)] = ht[2 * i]; ht[2 * (i + sh) + 1] = ht[2 * i + 1]; hi[i + sh] = hi[i];
+        }
+        for (int i = 0; i < sh; ++i) { ht[2 * i] = -1.0f; ht[2 * i + 1] = -1.0f; hi[i] = -1; }
+    }
+}
+
+// ------------------------------------------------------------------ morton / packbits (raymarching.cu:62-161)
+__global__ void morton_kernel(const int32_t* __restrict__ c, int64_t n, int32_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = (int32_t)morton3((uint32_t)c[3 * i], (uint32_t)c[3 * i + 1], (uint32_t)c[3 * i + 2]);
+}
+
+__global__ void morton_invert_kernel(const int32_t* __restrict__ idx, int64_t n, int32_t* __restrict__ c) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t v = (uint32_t)idx[i];
+    c[3 * i] = (int32_t)morton3_invert(v);
+    c[3 * i + 1] = (int32_t)morton3_invert(v >> 1);
+    c[3 * i + 2] = (int32_t)morton3_invert(v >> 2);
+}
+
+// one thread per output byte: two 16-B loads of the 8 floats, one byte store
+__global__ void packbits_kernel(const float* __restrict__ grid, int64_t n_bytes, float thr,
+                                const float* __restrict__ thr_dev, uint8_t* __restrict__ bits) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_bytes) return;
+    const float t = thr_dev ? *thr_dev : thr;
+    const float4 a = reinterpret_cast<const float4*>(grid)[2 * n];
+    const float4 b = reinterpret_cast<const float4*>(grid)[2 * n + 1];
+    uint32_t v = (a.x > t) | ((a.y > t) << 1) | ((a.z > t) << 2) | ((a.w > t) << 3) |
+                 ((b.x > t) << 4) | ((b.y > t) << 5) | ((b.z > t) << 6) | ((b.w > t) << 7);
+    bits[n] = (uint8_t)v;
+}
+
+// ------------------------------------------------------------------ ray marching (raymarching.cu:166-454)
+struct MarchParams {
+    const float* o; const float* d; const float* hits_t; int64_t hits_stride;
+    const uint8_t* bitfield; int cascades; float scale; float exp_step; const float* noise;
+    int grid_size; int max_samples;
+};
+
+// Marches ray r (raymarching.cu:190-234 / :243-279).  WRITE=false counts (up to max_samples);
+// WRITE=true re-marches and stores the first `limit` samples at `base`.
+template <bool WRITE>
+__device__ __forceinline__ int march_ray(const MarchParams& p, int64_t r, int limit, int64_t base,
+                                         float* __restrict__ xyzs, float* __restrict__ dirs,
+                                         float* __restrict__ deltas, float* __restrict__ ts) {
+    const float gsi = 1.0f / (float)p.grid_size;
+    const float ox = p.o[3 * r], oy = p.o[3 * r + 1], oz = p.o[3 * r + 2];
+    const float dx = p.d[3 * r], dy = p.d[3 * r + 1], dz = p.d[3 * r + 2];
+    const float dxi = 1.0f / dx, dyi = 1.0f / dy, dzi = 1.0f / dz;
+    float t1 = p.hits_t[r * p.hits_stride], t2 = p.hits_t[r * p.hits_stride + 1];
+    if (t1 >= 0) {
+        const float dt = calc_dt(t1, p.exp_step, p.max_samples, p.grid_size, p.scale);
+        t1 = fmaf(dt, p.noise[r], t1);
+    }
+    float t = t1; int n = 0;
+    while (0 <= t && t < t2 && n < limit) {
+        const float x = fmaf(t, dx, ox), y = fmaf(t, dy, oy), z = fmaf(t, dz, oz);
+        const float dt = calc_dt(t, p.exp_step, p.max_samples, p.grid_size, p.scale);
+        const Cell c = lookup_cell(x, y, z, dt, p.cascades, p.grid_size, p.scale, p.bitfield);
+        if (c.occ) {
+            if (WRITE) {
+                const int64_t s = base + n;
+                xyzs[3 * s] = x; xyzs[3 * s + 1] = y; xyzs[3 * s + 2] = z;
+                dirs[3 * s] = dx; dirs[3 * s + 1] = dy; dirs[3 * s + 2] = dz;
+                ts[s] = t; deltas[s] = dt;
+            }
+            t += dt; n++;
+        } else {
+            const float tt = skip_target(t, c, x, y, z, dx, dy, dz, dxi, dyi, dzi, gsi);
+            do { t += calc_dt(t, p.exp_step, p.max_samples, p.grid_size, p.scale); } while (t < tt);
+        }
+    }
+    return n;
+}
+
+__global__ void march_count_kernel(MarchParams p, int64_t n_rays, int32_t* __restrict__ counts) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rays) return;
+    counts[r] = march_ray<false>(p, r, p.max_samples, 0, nullptr, nullptr, nullptr, nullptr);
+}
+
+// One-workgroup exclusive scan of the per-ray counts -> rays_a rows and counter (device resident).
+constexpr int SCAN_THREADS = 1024;
+__global__ __launch_bounds__(SCAN_THREADS) void march_scan_kernel(const int32_t* __restrict__ counts, int64_t n_rays,
+                                                                 int64_t capacity, int64_t* __restrict__ rays_a,
+                                                                 int32_t* __restrict__ counter) {
+    __shared__ int64_t wave_tot[SCAN_THREADS / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int64_t chunk = div_up<int64_t>(n_rays, SCAN_THREADS);
+    const int64_t b = tid * chunk, e = min(n_rays, b + chunk);
+    int64_t local = 0;
+    for (int64_t i = b; i < e; ++i) local += counts[i];
+    // inclusive wave scan
+    int64_t v = local;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t u = __shfl_up(v, off, 64);
+        if (lane >= off) v += u;
+    }
+    if (lane == 63) wave_tot[wid] = v;
+    __syncthreads();
+    if (wid == 0) {
+        int64_t w = lane < SCAN_THREADS / 64 ? wave_tot[lane] : 0;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t u = __shfl_up(w, off, 64);
+            if (lane >= off) w += u;
+        }
+        if (lane < SCAN_THREADS / 64) wave_tot[lane] = w;  // inclusive per-wave totals
+    }
+    __syncthreads();
+    int64_t run = (v - local) + (wid > 0 ? wave_tot[wid - 1] : 0);  // exclusive start of this chunk
+    for (int64_t i = b; i < e; ++i) {
+        const int64_t c = counts[i];
+        const int64_t s = min(run, capacity);
+        const int64_t cc = max<int64_t>(0, min(c, capacity - run));
+        rays_a[3 * i] = i; rays_a[3 * i + 1] = s; rays_a[3 * i + 2] = cc;
+        run += c;
+    }
+    if (tid == SCAN_THREADS - 1) {
+        counter[0] = (int32_t)min(run, capacity);
+        counter[1] = (int32_t)n_rays;
+    }
+}
+
+__global__ void march_write_kernel(MarchParams p, int64_t n_rays, const int64_t* __restrict__ rays_a,
+                                   float* __restrict__ xyzs, float* __restrict__ dirs, float* __restrict__ deltas,
+                                   float* __restrict__ ts) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rays) return;
+    const int limit = (int)rays_a[3 * r + 2];
+    if (limit == 0) return;
+    march_ray<true>(p, r, limit, rays_a[3 * r + 1], xyzs, dirs, deltas, ts);
+}
+
+// raymarching_test_kernel (raymarching.cu:335-404) with the calc_dt(..., cascades) quirk.
+__global__ void march_test_kernel(MarchParams p, float* __restrict__ hits_t, const int64_t* __restrict__ alive,
+                                  int64_t n_alive, int N_samples, float* __restrict__ xyzs, float* __restrict__ dirs,
+                                  float* __restrict__ deltas, float* __restrict__ ts, int32_t* __restrict__ n_eff) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_alive) return;
+    const int64_t r = alive[n];
+    const float gsi = 1.0f / (float)p.grid_size;
+    const float qscale = (float)p.cascades;  // the reference's quirk: cascades passed as `scale`
+    const float ox = p.o[3 * r], oy = p.o[3 * r + 1], oz = p.o[3 * r + 2];
+    const float dx = p.d[3 * r], dy = p.d[3 * r + 1], dz = p.d[3 * r + 2];
+    const float dxi = 1.0f / dx, dyi = 1.0f / dy, dzi = 1.0f / dz;
+    float t = hits_t[r * p.hits_stride], t2 = hits_t[r * p.hits_stride + 1];
+    const int64_t row = n * N_samples;
+    int s = 0;
+    while (t < t2 && s < N_samples) {
+        const float x = fmaf(t, dx, ox), y = fmaf(t, dy, oy), z = fmaf(t, dz, oz);
+        const float dt = calc_dt(t, p.exp_step, p.max_samples, p.grid_size, qscale);
+        const Cell c = lookup_cell(x, y, z, dt, p.cascades, p.grid_size, p.scale, p.bitfield);
+        if (c.occ) {
+            const int64_t k = row + s;
+            xyzs[3 * k] = x; xyzs[3 * k + 1] = y; xyzs[3 * k + 2] = z;
+            dirs[3 * k] = dx; dirs[3 * k + 1] = dy; dirs[3 * k + 2] = dz;
+            ts[k] = t; deltas[k] = dt;
+            t += dt;
+            hits_t[r * p.hits_stride] = t;
+            s++;
+        } else {
+            const float tt = skip_target(t, c, x, y, z, dx, dy, dz, dxi, dyi, dzi, gsi);
+            do { t += calc_dt(t, p.exp_step, p.max_samples, p.grid_size, qscale); } while (t < tt);
+        }
+    }
+    for (int k = s; k < N_samples; ++k) {  // zero the unused tail of this row (the reference zero-fills)
+        const int64_t q = row + k;
+        xyzs[3 * q] = 0.f; xyzs[3 * q + 1] = 0.f; xyzs[3 * q + 2] = 0.f;
+        dirs[3 * q] = 0.f; dirs[3 * q + 1] = 0.f; dirs[3 * q + 2] = 0.f;
+        ts[q] = 0.f; deltas[q] = 0.f;
+    }
+    n_eff[n] = s;
+}
+
+// ------------------------------------------------------------------ compositing (volumerendering.cu)
+__global__ void composite_fw_kernel(const float* __restrict__ sigmas, const float* __restrict__ rgbs,
+                                    const float* __restrict__ deltas, const float* __restrict__ ts,
+                                    const int64_t* __restrict__ rays_a, int64_t n_rays, float T_thr,
+                                    int64_t* __restrict__ total_samples, float* __restrict__ opacity,
+                                    float* __restrict__ depth, float* __restrict__ rgb, float* __restrict__ ws) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_rays) return;
+    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
+    const int N = (int)rays_a[3 * n + 2];
+    float T = 1.0f, R = 0.f, G = 0.f, B = 0.f, D = 0.f, O = 0.f;
+    int samples = 0;
+    while (samples < N) {
+        const int64_t s = start + samples;
+        const float a = 1.0f - fast_exp(-sigmas[s] * deltas[s]);
+        const float w = a * T;
+        R = fmaf(w, rgbs[3 * s], R); G = fmaf(w, rgbs[3 * s + 1], G); B = fmaf(w, rgbs[3 * s + 2], B);
+        D = fmaf(w, ts[s], D);
+        O += w;
+        ws[s] = w;
+        T *= 1.0f - a;
+        if (T <= T_thr) break;
+        samples++;
+    }
+    for (int k = samples + 1; k < N; ++k) ws[start + k] = 0.0f;
+    opacity[ray] = O; depth[ray] = D;
+    rgb[3 * ray] = R; rgb[3 * ray + 1] = G; rgb[3 * ray + 2] = B;
+    total_samples[ray] = samples;
+}
+
+__global__ void composite_bw_kernel(const float* __restrict__ dL_dopacity, const float* __restrict__ dL_ddepth,
+                                    const float* __restrict__ dL_drgb, const float* __restrict__ dL_dws,
+                                    const float* __restrict__ sigmas, const float* __restrict__ rgbs,
+                                    const float* __restrict__ ws, const float* __restrict__ deltas,
+                                    const float* __restrict__ ts, const int64_t* __restrict__ rays_a,
+                                    const float* __restrict__ opacity, const float* __restrict__ depth,
+                                    const float* __restrict__ rgb, int64_t n_rays, float T_thr,
+                                    float* __restrict__ dL_dsigmas, float* __restrict__ dL_drgbs) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_rays) return;
+    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
+    const int N = (int)rays_a[3 * n + 2];
+    if (N <= 0) return;
+    // inclusive scan of dL_dws*ws (volumerendering.cu:119-123, host product :175): total first ...
+    float wsum = 0.0f;
+    for (int k = 0; k < N; ++k) wsum += dL_dws[start + k] * ws[start + k];
+    const float R = rgb[3 * ray], G = rgb[3 * ray + 1], B = rgb[3 * ray + 2];
+    const float O = opacity[ray], Dp = depth[ray];
+    const float gr = dL_drgb[3 * ray], gg = dL_drgb[3 * ray + 1], gb = dL_drgb[3 * ray + 2];
+    const float go = dL_dopacity[ray], gd = dL_ddepth[ray];
+    float T = 1.0f, r = 0.f, g = 0.f, b = 0.f, dd = 0.f, scan = 0.0f;
+    int samples = 0;
+    while (samples < N) {
+        const int64_t s = start + samples;
+        scan += dL_dws[s] * ws[s];  // ... then the running prefix, same sequential sums as thrust's scan
+        const float a = 1.0f - fast_exp(-sigmas[s] * deltas[s]);
+        const float w = a * T;
+        r = fmaf(w, rgbs[3 * s], r); g = fmaf(w, rgbs[3 * s + 1], g); b = fmaf(w, rgbs[3 * s + 2], b);
+        dd = fmaf(w, ts[s], dd);
+        T *= 1.0f - a;
+        dL_drgbs[3 * s] = gr * w; dL_drgbs[3 * s + 1] = gg * w; dL_drgbs[3 * s + 2] = gb * w;
+        float acc = gr * fmaf(rgbs[3 * s], T, -(R - r));
+        acc = fmaf(gg, fmaf(rgbs[3 * s + 1], T, -(G - g)), acc);
+        acc = fmaf(gb, fmaf(rgbs[3 * s + 2], T, -(B - b)), acc);
+        acc = fmaf(go, 1 - O, acc);
+        acc = fmaf(gd, fmaf(ts[s], T, -(Dp - dd)), acc);
+        acc = fmaf(T, dL_dws[s], acc);
+        acc = acc - (wsum - scan);
+        dL_dsigmas[s] = deltas[s] * acc;
+        if (T <= T_thr) break;
+        samples++;
+    }
+    for (int k = samples + 1; k < N; ++k) {
+        const int64_t s = start + k;
+        dL_dsigmas[s] = 0.f; dL_drgbs[3 * s] = 0.f; dL_drgbs[3 * s + 1] = 0.f; dL_drgbs[3 * s + 2] = 0.f;
+    }
+}
+
+__global__ void composite_test_kernel(const float* __restrict__ sigmas, const float* __restrict__ rgbs,
+                                      const float* __restrict__ deltas, const float* __restrict__ ts,
+                                      int64_t* __restrict__ alive, int64_t n_alive, int N_samples, float T_thr,
+                                      const int32_t* __restrict__ n_eff, float* __restrict__ opacity,
+                                      float* __restrict__ depth, float* __restrict__ rgb) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_alive) return;
+    const int ne = n_eff[n];
+    if (ne == 0) { alive[n] = -1; return; }
+    const int64_t r = alive[n];
+    float O = opacity[r], D = depth[r], R = rgb[3 * r], G = rgb[3 * r + 1], B = rgb[3 * r + 2];
+    float T = 1 - O;
+    for (int s = 0; s < ne; ++s) {
+        const int64_t k = n * N_samples + s;
+        const float a = 1.0f - fast_exp(-sigmas[k] * deltas[k]);
+        const float w = a * T;
+        R = fmaf(w, rgbs[3 * k], R); G = fmaf(w, rgbs[3 * k + 1], G); B = fmaf(w, rgbs[3 * k + 2], B);
+        D = fmaf(w, ts[k], D);
+        O += w;
+        T *= 1.0f - a;
+        if (T <= T_thr) { alive[n] = -1; break; }
+    }
+    opacity[r] = O; depth[r] = D; rgb[3 * r] = R; rgb[3 * r + 1] = G; rgb[3 * r + 2] = B;
+}
+
+// ------------------------------------------------------------------ distortion loss (losses.cu)
+__global__ void distortion_fw_kernel(const float* __restrict__ ws, const float* __restrict__ deltas,
+                                     const float* __restrict__ ts, const int64_t* __restrict__ rays_a,
+                                     int64_t n_rays, float* __restrict__ loss, float* __restrict__ ws_incl,
+                                     float* __restrict__ wts_incl) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_rays) return;
+    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
+    const int N = (int)rays_a[3 * n + 2];
+    const float third = 1.0f / 3;
+    float a = 0.f, b = 0.f, sum = 0.f;
+    for (int k = 0; k < N; ++k) {
+        const int64_t s = start + k;
+        const float wx = a, wtx = b;
+        a += ws[s]; b += ws[s] * ts[s];
+        ws_incl[s] = a; wts_incl[s] = b;
+        sum += 2 * (b * wx - a * wtx) + third * ws[s] * ws[s] * deltas[s];
+    }
+    loss[ray] = sum;
+}
+
+__global__ void distortion_bw_kernel(const float* __restrict__ dL_dloss, const float* __restrict__ ws_incl,
+                                     const float* __restrict__ wts_incl, const float* __restrict__ ws,
+                                     const float* __restrict__ deltas, const float* __restrict__ ts,
+                                     const int64_t* __restrict__ rays_a, int64_t n_rays, float* __restrict__ dL_dws) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_rays) return;
+    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
+    const int N = (int)rays_a[3 * n + 2];
+    if (N <= 0) return;
+    const int64_t end = start + N - 1;
+    const float ws_sum = ws_incl[end], wts_sum = wts_incl[end], g = dL_dloss[ray];
+    for (int64_t s = start; s <= end; ++s) {
+        const float first = (s == start) ? 0.0f : fmaf(ts[s], ws_incl[s - 1], -wts_incl[s - 1]);
+        const float second = fmaf(-ts[s], ws_sum - ws_incl[s], wts_sum - wts_incl[s]);
+        float v = g * 2 * (first + second);
+        dL_dws[s] = fmaf(g * (float)2 / 3 * ws[s], deltas[s], v);
+    }
+}
+
+inline unsigned blocks_for(int64_t n, int b) { return (unsigned)div_up<int64_t>(n, b); }
+
+}  // namespace
+
+// ================================================================== C ABI
+extern "C" {
+
+int mfnerf_ray_aabb_intersect(const float* rays_o, const float* rays_d, const float* centers,
+                              const float* half_sizes, int64_t n_rays, int64_t n_voxels, int max_hits,
+                              int32_t* hit_cnt, float* hits_t, int64_t* hits_voxel_idx, mfnerf_stream_t stream) {
+    if (n_rays < 0 || n_voxels < 0 || max_hits <= 0) { mfn_set_error("ray_aabb_intersect: bad sizes"); return MFN_ERR_INVALID; }
+    if (n_rays == 0) return MFN_OK;
+    if (!rays_o || !rays_d || !centers || !half_sizes || !hit_cnt || !hits_t || !hits_voxel_idx) {
+        mfn_set_error("ray_aabb_intersect: null pointer"); return MFN_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(ray_aabb_kernel, dim3(blocks_for(n_rays, RAY_BLOCK)), dim3(RAY_BLOCK), 0, stream,
+                       rays_o, rays_d, centers, half_sizes, n_rays, n_voxels, max_hits, hit_cnt, hits_t,
+                       hits_voxel_idx);
+    return mfn_check_launch("ray_aabb_intersect");
+}
+
+int mfnerf_morton3d(const int32_t* coords, int64_t n, int32_t* out, mfnerf_stream_t stream) {
+    if (n < 0) { mfn_set_error("morton3D: bad size"); return MFN_ERR_INVALID; }
+    if (n == 0) return MFN_OK;
+    if (!coords || !out) { mfn_set_error("morton3D: null pointer"); return MFN_ERR_INVALID; }
+    hipLaunchKernelGGL(morton_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, stream, coords, n, out);
+    return mfn_check_launch("morton3D");
+}
+
+int mfnerf_morton3d_invert(const int32_t* idx, int64_t n, int32_t* coords, mfnerf_stream_t stream) {
+    if (n < 0) { mfn_set_error("morton3D_invert: bad size"); return MFN_ERR_INVALID; }
+    if (n == 0) return MFN_OK;
+    if (!idx || !coords) { mfn_set_error("morton3D_invert: null pointer"); return MFN_ERR_INVALID; }
+    hipLaunchKernelGGL(morton_invert_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, stream, idx, n, coords);
+    return mfn_check_launch("morton3D_invert");
+}
+
+int mfnerf_packbits(const float* grid, int64_t n_bytes, float thr, const float* thr_dev, uint8_t* bitfield,
+                    mfnerf_stream_t stream) {
+    if (n_bytes < 0) { mfn_set_error("packbits: bad size"); return MFN_ERR_INVALID; }
+    if (n_bytes == 0) return MFN_OK;
+    if (!grid || !bitfield) { mfn_set_error("packbits: null pointer"); return MFN_ERR_INVALID; }
+    if (((uintptr_t)grid) & 15) { mfn_set_error("packbits: density grid must be 16-byte aligned"); return MFN_ERR_INVALID; }
+    hipLaunchKernelGGL(packbits_kernel, dim3(blocks_for(n_bytes, 256)), dim3(256), 0, stream, grid, n_bytes, thr,
+                       thr_dev, bitfield);
+    return mfn_check_launch("packbits");
+}
+
+int64_t mfnerf_raymarching_train_workspace(int64_t n_rays) { return ((n_rays * 4 + 255) / 256) * 256; }
+
+int mfnerf_raymarching_train(const float* rays_o, const float* rays_d, const float* hits_t, int64_t hits_stride,
+                             const uint8_t* bitfield, int cascades, float scale, float exp_step_factor,
+                             const float* noise, int grid_size, int max_samples, int64_t n_rays, int64_t capacity,
+                             int64_t* rays_a, float* xyzs, float* dirs, float* deltas, float* ts, int32_t* counter,
+                             void* workspace, mfnerf_stream_t stream) {
+    if (n_rays < 0 || capacity < 0 || cascades < 1 || grid_size < 1 || grid_size > 1024 || max_samples < 1 ||
+        hits_stride < 2) {
+        mfn_set_error("raymarching_train: bad arguments"); return MFN_ERR_INVALID;
+    }
+    if (!counter) { mfn_set_error("raymarching_train: null counter"); return MFN_ERR_INVALID; }
+    if (n_rays == 0) { (void)hipMemsetAsync(counter, 0, 8, stream); return mfn_check_launch("raymarching_train"); }
+    if (!rays_o || !rays_d || !hits_t || !bitfield || !noise || !rays_a || !workspace ||
+        (capacity > 0 && (!xyzs || !dirs || !deltas || !ts))) {
+        mfn_set_error("raymarching_train: null pointer"); return MFN_ERR_INVALID;
+    }
+    MarchParams p{rays_o, rays_d, hits_t, hits_stride, bitfield, cascades, scale, exp_step_factor, noise,
+                  grid_size, max_samples};
+    int32_t* counts = (int32_t*)workspace;
+    const unsigned nb = blocks_for(n_rays, RAY_BLOCK);
+    hipLaunchKernelGGL(march_count_kernel, dim3(nb), dim3(RAY_BLOCK), 0, stream, p, n_rays, counts);
+    hipLaunchKernelGGL(march_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, counts, n_rays, capacity, rays_a,
+                       counter);
+    hipLaunchKernelGGL(march_write_kernel, dim3(nb), dim3(RAY_BLOCK), 0, stream, p, n_rays, rays_a, xyzs, dirs,
+                       deltas, ts);
+    return mfn_check_launch("raymarching_train");
+}
+
+int mfnerf_raymarching_test(const float* rays_o, const float* rays_d, float* hits_t, int64_t hits_stride,
+                            const int64_t* alive_indices, int64_t n_alive, const uint8_t* bitfield, int cascades,
+                            float scale, float exp_step_factor, int grid_size, int max_samples, int N_samples,
+                            float* xyzs, float* dirs, float* deltas, float* ts, int32_t* n_eff,
+                            mfnerf_stream_t stream) {
+    if (n_alive < 0 || N_samples < 0 || cascades < 1 || grid_size < 1 || grid_size > 1024 || max_samples < 1 ||
+        hits_stride < 2) {
+        mfn_set_error("raymarching_test: bad arguments"); return MFN_ERR_INVALID;
+    }
+    if (n_alive == 0) return MFN_OK;
+    if (!rays_o || !rays_d || !hits_t || !alive_indices || !bitfield || !n_eff ||
+        (N_samples > 0 && (!xyzs || !dirs || !deltas || !ts))) {
+        mfn_set_error("raymarching_test: null pointer"); return MFN_ERR_INVALID;
+    }
+    MarchParams p{rays_o, rays_d, hits_t, hits_stride, bitfield, cascades, scale, exp_step_factor, nullptr,
+                  grid_size, max_samples};
+    hipLaunchKernelGGL(march_test_kernel, dim3(blocks_for(n_alive, RAY_BLOCK)), dim3(RAY_BLOCK), 0, stream, p,
+                       hits_t, alive_indices, n_alive, N_samples, xyzs, dirs, deltas, ts, n_eff);
+    return mfn_check_launch("raymarching_test");
+}
+
+int mfnerf_composite_train_fw(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
+                              const int64_t* rays_a, int64_t n_rays, int64_t n_samples, float T_threshold,
+                              int64_t* total_samples, float* opacity, float* depth, float* rgb, float* ws,
+                              mfnerf_stream_t stream) {
+    if (n_rays < 0 || n_samples < 0) { mfn_set_error("composite_train_fw: bad sizes"); return MFN_ERR_INVALID; }
+    if (n_rays == 0) return MFN_OK;
+    if (!rays_a || !total_samples || !opacity || !depth || !rgb ||
+        (n_samples > 0 && (!sigmas || !rgbs || !deltas || !ts || !ws))) {
+        mfn_set_error("composite_train_fw: null pointer"); return MFN_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(composite_fw_kernel, dim3(blocks_for(n_rays, RAY_BLOCK)), dim3(RAY_BLOCK), 0, stream, sigmas,
+                       rgbs, deltas, ts, rays_a, n_rays, T_threshold, total_samples, opacity, depth, rgb, ws);
+    return mfn_check_launch("composite_train_fw");
+}
+
+int mfnerf_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, const float* dL_drgb,
+                              const float* dL_dws, const float* sigmas, const float* rgbs, const float* ws,
+                              const float* deltas, const float* ts, const int64_t* rays_a, const float* opacity,
+                              const float* depth, const float* rgb, int64_t n_rays, int64_t n_samples,
+                              float T_threshold, float* dL_dsigmas, float* dL_drgbs, mfnerf_stream_t stream) {
+    if (n_rays < 0 || n_samples < 0) { mfn_set_error("composite_train_bw: bad sizes"); return MFN_ERR_INVALID; }
+    if (n_rays == 0) return MFN_OK;
+    if (!dL_dopacity || !dL_ddepth || !dL_drgb || !rays_a || !opacity || !depth || !rgb ||
+        (n_samples > 0 && (!dL_dws || !sigmas || !rgbs || !ws || !deltas || !ts || !dL_dsigmas || !dL_drgbs))) {
+        mfn_set_error("composite_train_bw: null pointer"); return MFN_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(composite_bw_kernel, dim3(blocks_for(n_rays, RAY_BLOCK)), dim3(RAY_BLOCK), 0, stream,
+                       dL_dopacity, dL_ddepth, dL_drgb, dL_dws, sigmas, rgbs, ws, deltas, ts, rays_a, opacity,
+                       depth, rgb, n_rays, T_threshold, dL_dsigmas, dL_drgbs);
+    return mfn_check_launch("composite_train_bw");
+}
+
+int mfnerf_composite_test_fw(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
+                             int64_t* alive_indices, int64_t n_alive, int N_samples, float T_threshold,
+                             const int32_t* n_eff, float* opacity, float* depth, float* rgb,
+                             mfnerf_stream_t stream) {
+    if (n_alive < 0 || N_samples < 0) { mfn_set_error("composite_test_fw: bad sizes"); return MFN_ERR_INVALID; }
+    if (n_alive == 0) return MFN_OK;
+    if (!alive_indices || !n_eff || !opacity || !depth || !rgb ||
+        (N_samples > 0 && (!sigmas || !rgbs || !deltas || !ts))) {
+        mfn_set_error("composite_test_fw: null pointer"); return MFN_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(composite_test_kernel, dim3(blocks_for(n_alive, RAY_BLOCK)), dim3(RAY_BLOCK), 0, stream,
+                       sigmas, rgbs, deltas, ts, alive_indices, n_alive, N_samples, T_threshold, n_eff, opacity,
+                       depth, rgb);
+    return mfn_check_launch("composite_test_fw");
+}
+
+int mfnerf_distortion_loss_fw(const float* ws, const float* deltas, const float* ts, const int64_t* rays_a,
+                              int64_t n_rays, int64_t n_samples, float* loss, float* ws_incl, float* wts_incl,
+                              mfnerf_stream_t stream) {
+    if (n_rays < 0 || n_samples < 0) { mfn_set_error("distortion_loss_fw: bad sizes"); return MFN_ERR_INVALID; }
+    if (n_rays == 0) return MFN_OK;
+    if (!rays_a || !loss || (n_samples > 0 && (!ws || !deltas || !ts || !ws_incl || !wts_incl))) {
+        mfn_set_error("distortion_loss_fw: null pointer"); return MFN_ERR_INVALID;
+    }
+    (void)hipMemsetAsync(loss, 0, n_rays * sizeof(float), stream);
+    hipLaunchKernelGGL(distortion_fw_kernel, dim3(blocks_for(n_rays, RAY_BLOCK)), dim3(RAY_BLOCK), 0, stream, ws,
+                       deltas, ts, rays_a, n_rays, loss, ws_incl, wts_incl);
+    return mfn_check_launch("distortion_loss_fw");
+}
+
+int mfnerf_distortion_loss_bw(const float* dL_dloss, const float* ws_incl, const float* wts_incl,
+                              const float* ws, const float* deltas, const float* ts, const int64_t* rays_a,
+                              int64_t n_rays, int64_t n_samples, float* dL_dws, mfnerf_stream_t stream) {
+    if (n_rays < 0 || n_samples < 0) { mfn_set_error("distortion_loss_bw: bad sizes"); return MFN_ERR_INVALID; }
+    if (n_rays == 0) return MFN_OK;
+    if (!dL_dloss || !rays_a || (n_samples > 0 && (!ws_incl || !wts_incl || !ws || !deltas || !ts || !dL_dws))) {
+        mfn_set_error("distortion_loss_bw: null pointer"); return MFN_ERR_INVALID;
+    }
+    if (n_samples > 0) (void)hipMemsetAsync(dL_dws, 0, n_samples * sizeof(float), stream);
+    hipLaunchKernelGGL(distortion_bw_kernel, dim3(blocks_for(n_rays, RAY_BLOCK)), dim3(RAY_BLOCK), 0, stream,
+                       dL_dloss, ws_incl, wts_incl, ws, deltas, ts, rays_a, n_rays, dL_dws);
+    return mfn_check_launch("distortion_loss_bw");
+}
+
+}  // extern "C"

@@ -1,0 +1,126 @@
+"""tinycudann-compatible modules (the subset MF-NeRF configures, models/networks.py:36-79).
+
+Each module owns one flat fp32 `params` Parameter in tcnn's layout (state-dict keys
+`xyz_encoder.params`, `rgb_net.params` as in the reference), initialised like tcnn (grid
+U(-1e-4, 1e-4), MLP Xavier-uniform).  NGP (mfnerf.networks) does not call these forwards: it
+runs the fused gfx950 field kernels on the same parameters.  The standalone forwards exist for
+users who build tcnn modules directly: grids run the HIP grid kernels; the MLP standalone path
+is a plain fp16 GEMM chain (library GEMMs, not on the hot path).
+"""
+import math
+
+import torch
+
+from .field import GridEncodeFunction
+from .grid import GridLayout
+
+
+def _pad16(n):
+    return (n + 15) // 16 * 16
+
+
+def mlp_shapes(n_in, n_out, n_neurons, n_hidden_layers):
+    """FullyFusedMLP weights, bias-free, output width padded to 16: [(out, in), ...]."""
+    shapes = [(n_neurons, n_in)] + [(n_neurons, n_neurons)] * (n_hidden_layers - 1)
+    return shapes + [(_pad16(n_out), n_neurons)]
+
+
+def _xavier(shapes, gen):
+    parts = []
+    for o, k in shapes:
+        s = math.sqrt(6.0 / (o + k))
+        parts.append(torch.empty(o * k).uniform_(-s, s, generator=gen))
+    return torch.cat(parts)
+
+
+def _act(x, name):
+    return {"None": lambda v: v, "ReLU": torch.relu, "Sigmoid": torch.sigmoid, "Exponential": torch.exp}[name](x)
+
+
+def mlp_forward_fp16(x, params, shapes, n_out, activation, output_activation):
+    h = x.half()
+    off = 0
+    for i, (o, k) in enumerate(shapes):
+        W = params[off:off + o * k].view(o, k).half()
+        off += o * k
+        h = _act(h @ W.t(), activation if i < len(shapes) - 1 else output_activation)
+    return h[:, :n_out]
+
+
+class Encoding(torch.nn.Module):
+    """tcnn.Encoding for {Hash,MixedFeature}Grid and SphericalHarmonics (degree 4)."""
+
+    def __init__(self, n_input_dims, encoding_config, seed=1337, dtype=None):
+        super().__init__()
+        self.n_input_dims = n_input_dims
+        self.encoding_config = dict(encoding_config)
+        otype = self.encoding_config.get("otype", "")
+        if "SphericalHarmonics" in otype:
+            self.kind = "sh"
+            self.n_output_dims = self.encoding_config.get("degree", 4) ** 2
+            self.params = torch.nn.Parameter(torch.zeros(0))
+        elif otype.endswith("Grid"):
+            self.kind = "grid"
+            self.layout = GridLayout.from_config(self.encoding_config)
+            self.desc = self.layout.desc()
+            self.n_output_dims = self.layout.L * self.layout.F
+            g = torch.Generator().manual_seed(seed)
+            self.params = torch.nn.Parameter(torch.empty(self.layout.n_params).uniform_(-1e-4, 1e-4, generator=g))
+        else:
+            raise NotImplementedError(f"encoding {otype} is outside MF-NeRF's configuration")
+
+    def forward(self, x):
+        if self.kind == "grid":
+            return GridEncodeFunction.apply(x, self.params, self.layout, self.desc)
+        return sh4_torch(x.float()).half()
+
+
+def sh4_torch(d01):
+    x, y, z = (d01 * 2 - 1).unbind(-1)
+    xy, xz, yz, x2, y2, z2 = x * y, x * z, y * z, x * x, y * y, z * z
+    return torch.stack([
+        torch.full_like(x, 0.28209479177387814), -0.48860251190291987 * y, 0.48860251190291987 * z,
+        -0.48860251190291987 * x, 1.0925484305920792 * xy, -1.0925484305920792 * yz,
+        0.94617469575755997 * z2 - 0.31539156525251999, -1.0925484305920792 * xz,
+        0.54627421529603959 * x2 - 0.54627421529603959 * y2, 0.59004358992664352 * y * (-3.0 * x2 + y2),
+        2.8906114426405538 * xy * z, 0.45704579946446572 * y * (1.0 - 5.0 * z2),
+        0.3731763325901154 * z * (5.0 * z2 - 3.0), 0.45704579946446572 * x * (1.0 - 5.0 * z2),
+        1.4453057213202769 * z * (x2 - y2), 0.59004358992664352 * x * (-x2 + 3.0 * y2)], -1)
+
+
+class Network(torch.nn.Module):
+    """tcnn.Network with a FullyFusedMLP config."""
+
+    def __init__(self, n_input_dims, n_output_dims, network_config, seed=1337):
+        super().__init__()
+        c = network_config
+        self.n_input_dims, self.n_output_dims = n_input_dims, n_output_dims
+        self.width, self.depth = c["n_neurons"], c["n_hidden_layers"]
+        self.activation, self.output_activation = c.get("activation", "ReLU"), c.get("output_activation", "None")
+        self.shapes = mlp_shapes(n_input_dims, n_output_dims, self.width, self.depth)
+        g = torch.Generator().manual_seed(seed)
+        self.params = torch.nn.Parameter(_xavier(self.shapes, g))
+
+    def forward(self, x):
+        return mlp_forward_fp16(x, self.params, self.shapes, self.n_output_dims, self.activation,
+                                self.output_activation)
+
+
+class NetworkWithInputEncoding(torch.nn.Module):
+    """tcnn.NetworkWithInputEncoding: params = [network (MLP) | encoding (grid)]."""
+
+    def __init__(self, n_input_dims, n_output_dims, encoding_config, network_config, seed=1337):
+        super().__init__()
+        enc = Encoding(n_input_dims, encoding_config, seed=seed)
+        net = Network(enc.n_output_dims, n_output_dims, network_config, seed=seed)
+        self.layout, self.desc = enc.layout, enc.desc
+        self.n_output_dims = n_output_dims
+        self.shapes, self.n_net = net.shapes, net.params.numel()
+        self.activation, self.output_activation = net.activation, net.output_activation
+        self.width, self.depth = net.width, net.depth
+        self.params = torch.nn.Parameter(torch.cat([net.params.data, enc.params.data]))
+
+    def forward(self, x):
+        feat = GridEncodeFunction.apply(x, self.params[self.n_net:], self.layout, self.desc)
+        return mlp_forward_fp16(feat, self.params[:self.n_net], self.shapes, self.n_output_dims, self.activation,
+                                self.output_activation)

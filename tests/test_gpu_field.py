@@ -1,0 +1,153 @@
+"""GPU parity of the grid encoding and the MFMA field head against the fp32 torch oracle
+(oracle/field_oracle.py).  tcnn computes in fp16, so the oracle here rounds every MLP operand to
+fp16 exactly where the kernels do and the tolerances are fp16-sized (stated per assert)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from mfnerf import field as FLD
+from mfnerf._lib import call, ptr
+from mfnerf.grid import GridLayout
+from oracle import field_oracle as FO
+
+pytestmark = pytest.mark.gpu
+
+LEGO_B = math.exp(math.log(2048 * 0.5 / 16) / 15)
+
+
+def test_mfma_f16_lane_maps(gpu):
+    g = torch.Generator().manual_seed(0)
+    A = torch.randint(-4, 5, (32, 16), generator=g).half()
+    B = torch.randint(-4, 5, (16, 32), generator=g).half()
+    B[3, 7] = 3  # asymmetric
+    D = torch.empty(32, 32, device=gpu)
+    Ag, Bg = A.to(gpu), B.to(gpu)
+    call("mfnerf_debug_mfma_probe", ptr(Ag), ptr(Bg), ptr(D), torch.cuda.current_stream().cuda_stream)
+    assert torch.equal(D.cpu(), A.float() @ B.float())
+
+
+def _layouts():
+    return [("lego_hash", (16, 2, 19, 16, LEGO_B, "Hash", 1)),
+            ("small_T_hash", (8, 2, 10, 4, 8 ** (1 / 7), "Hash", 1)),
+            ("mixed_feature", (16, 2, 16, 16, LEGO_B, "MixedFeature", 4))]
+
+
+@pytest.mark.parametrize("name,args", _layouts())
+def test_grid_encode_fw_bw(gpu, name, args):
+    lay = GridLayout(*args)
+    olay = FO.GridLayout(*args)
+    assert lay.n_params == olay.n_params and lay.offsets == olay.offsets
+    g = torch.Generator().manual_seed(2)
+    N = 6000
+    x = torch.rand(N, 3, generator=g)
+    x[:8] = torch.tensor([0.0, 1.0]).repeat(12)[:24].view(8, 3)  # faces/corners of the unit cube
+    table = ((torch.rand(lay.n_params, generator=g) - 0.5)).half().float()
+    ref = FO.grid_encode(x, table, olay)
+    desc = lay.desc()
+    out = FLD.grid_encode_fw(x.to(gpu), N, table.half().to(gpu), lay, desc)
+    # fp32 accumulation of fp16 corners, one fp16 rounding of the output: <= 1 fp16 ulp (|y| < 1)
+    assert torch.allclose(out.float().cpu(), ref, atol=1e-3, rtol=0)
+    # backward: index_add (oracle autograd) vs fp32 atomics
+    dy = torch.randn(N, lay.L * lay.F, generator=g)
+    tp = table.clone().requires_grad_(True)
+    (FO.grid_encode(x, tp, olay) * dy).sum().backward()
+    gref = tp.grad
+    gt = torch.zeros(lay.n_params, device=gpu)
+    FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc)
+    assert torch.allclose(gt.cpu(), gref, rtol=1e-4, atol=1e-4 * float(gref.abs().max()))
+
+
+def test_grid_encode_world_coords_normalisation(gpu):
+    lay = GridLayout(16, 2, 19, 16, LEGO_B)
+    olay = FO.GridLayout(16, 2, 19, 16, LEGO_B)
+    g = torch.Generator().manual_seed(3)
+    xw = torch.rand(4096, 3, generator=g) - 0.5
+    table = ((torch.rand(lay.n_params, generator=g) - 0.5)).half().float()
+    xmin, xmax = -torch.ones(1, 3) * 0.5, torch.ones(1, 3) * 0.5
+    ref = FO.grid_encode((xw - xmin) / (xmax - xmin), table, olay)  # networks.py:105
+    out = FLD.grid_encode_fw(xw.to(gpu), 4096, table.half().to(gpu), lay, lay.desc(), -0.5, 1.0)
+    assert torch.allclose(out.float().cpu(), ref, atol=1e-3, rtol=0)
+
+
+def _h(t):
+    return t.half().float()
+
+
+def oracle_field(feat16, dirs, px, pr, width=64):
+    """fp32 restatement of the two FullyFusedMLPs + TruncExp + SH4 with operands rounded to fp16
+    where tcnn (and the kernels) hold them in fp16."""
+    W1 = _h(px[:2048].view(64, 32)); W2 = _h(px[2048:3072].view(16, 64))
+    R1 = _h(pr[:width * 32].view(width, 32)); R2 = _h(pr[width * 32:width * 32 + width * width].view(width, width))
+    R3 = _h(pr[width * 32 + width * width:].view(16, width))
+    y1 = _h(torch.relu(feat16 @ W1.t()))
+    h = _h(y1 @ W2.t())
+    sigma = torch.exp(h[:, 0])
+    dn = dirs / torch.norm(dirs, dim=1, keepdim=True)
+    sh = _h(FO.sh4((dn + 1) / 2))
+    r1 = _h(torch.relu(torch.cat([sh, h], 1) @ R1.t()))
+    r2 = _h(torch.relu(r1 @ R2.t()))
+    rgb = torch.sigmoid(r2 @ R3.t())[:, :3]
+    return sigma, rgb
+
+
+def _field_inputs(N, seed=4):
+    g = torch.Generator().manual_seed(seed)
+    feat = (torch.rand(N, 32, generator=g) - 0.5).half()
+    dirs = torch.randn(N, 3, generator=g)
+    px = FO.xavier_uniform_(torch.empty(3072), FO.mlp_shapes(32, 16, 64, 1), g) * 3
+    pr = FO.xavier_uniform_(torch.empty(7168), FO.mlp_shapes(32, 3, 64, 2), g) * 3
+    return feat, dirs, px, pr
+
+
+@pytest.mark.parametrize("N", [1, 31, 33, 5000])
+def test_field_fw(gpu, N):
+    feat, dirs, px, pr = _field_inputs(N)
+    s_ref, c_ref = oracle_field(feat.float(), dirs, px, pr)
+    packed = FLD.pack_field_weights(px.to(gpu), pr.to(gpu))
+    s, c = FLD.field_fw(feat.to(gpu), dirs.to(gpu), N, packed)
+    # h0 is one fp16 value on both sides; sigma = exp(h0): fp16-accumulation-order noise only
+    assert torch.allclose(s.cpu(), s_ref, rtol=4e-3, atol=1e-6)
+    assert torch.allclose(c.cpu(), c_ref, atol=2e-3, rtol=0)
+    sd, _ = FLD.field_fw(feat.to(gpu), None, N, packed, density_only=True)
+    assert torch.equal(sd.cpu(), s.cpu())
+
+
+def test_field_bw(gpu):
+    N = 3000
+    feat, dirs, px, pr = _field_inputs(N, seed=5)
+    g = torch.Generator().manual_seed(6)
+    dsig = torch.randn(N, generator=g) * 1e-6
+    drgb = torch.randn(N, 3, generator=g) * 1e-5
+    # oracle: fp32 autograd through the same fp16-rounded forward
+    f32 = feat.float().requires_grad_(True)
+    pxr = px.clone().requires_grad_(True)
+    prr = pr.clone().requires_grad_(True)
+
+    def fwd(f, a, b):
+        W1 = a[:2048].view(64, 32); W2 = a[2048:3072].view(16, 64)
+        R1 = b[:2048].view(64, 32); R2 = b[2048:6144].view(64, 64); R3 = b[6144:].view(16, 64)
+        y1 = torch.relu(f @ W1.t()); h = y1 @ W2.t()
+        sigma = torch.exp(h[:, 0])
+        dn = dirs / torch.norm(dirs, dim=1, keepdim=True)
+        sh = FO.sh4((dn + 1) / 2)
+        r1 = torch.relu(torch.cat([sh, h], 1) @ R1.t()); r2 = torch.relu(r1 @ R2.t())
+        return sigma, torch.sigmoid(r2 @ R3.t())[:, :3]
+
+    s, c = fwd(f32, pxr, prr)
+    ((s * dsig).sum() + (c * drgb).sum()).backward()
+    packed = FLD.pack_field_weights(px.to(gpu), pr.to(gpu))
+    dfeat = torch.empty(N, 32, device=gpu)
+    gx = torch.zeros(3072, device=gpu)
+    gr = torch.zeros(7168, device=gpu)
+    ws = FLD.field_bw_workspace(N, 64, gpu)
+    smax = float(torch.maximum(drgb.abs().max(), (dsig * s.detach()).abs().max()))
+    S = FLD.pow2_grad_scale(smax)
+    FLD.field_bw(feat.to(gpu), dirs.to(gpu), N, packed, dsig.to(gpu), drgb.to(gpu), S, dfeat, gx, gr, ws)
+    # fp16 operands in every backward product: compare relative to each tensor's scale
+    for got, ref in ((dfeat.cpu(), f32.grad), (gx.cpu(), pxr.grad), (gr.cpu(), prr.grad)):
+        err = (got - ref).abs().max() / ref.abs().max()
+        assert err < 2e-2, float(err)
+        cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0)
+        assert cos > 0.999, float(cos)
