@@ -1,0 +1,252 @@
+"""Training-throughput benchmark of the MF-NeRF hot path on MI355X.
+
+One step = one NeRF training iteration on a synthetic Lego-like batch (BASELINE config 2:
+8192 rays/batch per GPU, Hash grid L=16 F=2 T=2^19, rgb 64x2): AABB -> ray march -> grid encode
+-> MFMA field head -> composite -> loss -> composite bw -> field bw -> grid bw -> [all-reduce] ->
+Adam.  The occupancy-grid refresh (every 16 steps in the reference) is excluded from the timed
+step as SURVEY.md 8d prescribes and reported separately (density_update_ms).
+
+python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run (one rank per
+GPU, rank-distinct rays, one flat fp32 gradient all-reduce per step over RCCL).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mf-nerf_amd")]
+
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+# algorithmic bytes per live sample of each per-sample kernel (DESIGN.md "Kernels and rooflines")
+L, F = 16, 2
+BYTES_PER_SAMPLE = {
+    "grid_fw": 12 + L * 8 * F * 2 + L * F * 2,          # xyz + fp16 corner gathers + fp16 features = 588
+    "grid_bw": 12 + L * F * 4 + L * 8 * F * 4,          # xyz + fp32 dL/dfeat + fp32 atomic adds = 1164
+    "field_fw": L * F * 2 + 12 + 4 + 12,                 # feat + dir + sigma + rgb = 92
+    "field_bw": L * F * 2 + 12 + 16 + L * F * 4,         # feat + dir + dsigma,drgb + dfeat = 220
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--n-rays", type=int, default=8192)
+    ap.add_argument("--log2-T", type=int, default=19)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+STAGES = ["prep", "march", "grid_fw", "field_fw", "composite_fw", "composite_bw", "field_bw", "grid_bw", "allreduce",
+          "adam"]
+
+
+def run_step(step, batch, world, ev=None):
+    """One training step; if ev is given, records a CUDA event after every stage."""
+    from mfnerf._lib import call, ptr, stream
+    st, c = step.state, step.cfg
+    N, cap = c.n_rays, step.cap
+    s = stream()
+
+    def mark(name):
+        if ev is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            ev.append((name, e))
+
+    mark("start")
+    call("mfnerf_ray_aabb_intersect", ptr(batch.rays_o), ptr(batch.rays_d), ptr(step.center), ptr(step.half_size),
+         N, 1, 1, ptr(st.hit_cnt), ptr(st.hits), ptr(st.hits_idx), s)
+    t1 = st.hits[:, 0, 0]
+    t1.masked_fill_((t1 >= 0) & (t1 < 0.01), 0.01)
+    torch.rand(N, generator=step.gen, device=step.dev, out=st.noise)
+    mark("prep")
+    call("mfnerf_raymarching_train", ptr(batch.rays_o), ptr(batch.rays_d), ptr(st.hits_t), 2, ptr(step.bitfield),
+         step.cascades, float(c.scale), 0.0, ptr(st.noise), step.G, c.max_samples, N, cap, ptr(st.rays_a),
+         ptr(st.xyzs), ptr(st.dirs), ptr(st.deltas), ptr(st.ts), ptr(st.counter), ptr(st.march_ws), s)
+    mark("march")
+    call("mfnerf_grid_encode_fw", ptr(st.xyzs), cap, ptr(st.counter), step.x_min, step.x_range, step.desc,
+         ptr(step.p16[step.off_table:]), ptr(st.feat), s)
+    mark("grid_fw")
+    call("mfnerf_field_fw", ptr(st.feat), ptr(st.dirs), cap, ptr(st.counter), ptr(step.packed), c.rgb_width, 0,
+         ptr(st.sigma), ptr(st.rgb_s), s)
+    mark("field_fw")
+    call("mfnerf_composite_train_fw", ptr(st.sigma), ptr(st.rgb_s), ptr(st.deltas), ptr(st.ts), ptr(st.rays_a), N,
+         cap, c.T_threshold, ptr(st.total), ptr(st.opacity), ptr(st.depth), ptr(st.rgb), ptr(st.ws), s)
+    st.loss_sum.zero_()
+    call("mfnerf_nerf_loss", ptr(st.rgb), ptr(st.opacity), ptr(batch.rgb), N, c.lambda_opacity, 1.0, 1.0, 1.0,
+         ptr(st.dL_drgb), ptr(st.dL_dop), ptr(st.loss_sum), s)
+    mark("composite_fw")
+    call("mfnerf_composite_train_bw", ptr(st.dL_dop), ptr(st.zeros_ray), ptr(st.dL_drgb), ptr(st.zeros_samp),
+         ptr(st.sigma), ptr(st.rgb_s), ptr(st.ws), ptr(st.deltas), ptr(st.ts), ptr(st.rays_a), ptr(st.opacity),
+         ptr(st.depth), ptr(st.rgb), N, cap, c.T_threshold, ptr(st.dsig), ptr(st.drgb_s), s)
+    mark("composite_bw")
+    step.grads.zero_()
+    call("mfnerf_field_bw", ptr(st.feat), ptr(st.dirs), cap, ptr(st.counter), ptr(step.packed), c.rgb_width,
+         ptr(st.dsig), ptr(st.drgb_s), step.grad_scale, ptr(st.dfeat), ptr(step.grads),
+         ptr(step.grads[step.off_rgb:]), ptr(st.field_ws), s)
+    mark("field_bw")
+    call("mfnerf_grid_encode_bw", ptr(st.xyzs), cap, ptr(st.counter), step.x_min, step.x_range, step.desc,
+         ptr(st.dfeat), ptr(step.grads[step.off_table:]), s)
+    mark("grid_bw")
+    if world > 1:
+        torch.distributed.all_reduce(step.grads, op=torch.distributed.ReduceOp.AVG)
+    mark("allreduce")
+    step.optimizer()
+    mark("adam")
+
+
+# ---------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(n_rays, log2_T, seconds):
+    """The reference's hot path restated on the host (oracle/): C march + compositing, fp32 torch
+    grid encoding + MLPs with autograd, fused loss, Adam.  Timed on a bounded sample."""
+    from mfnerf import synthetic
+    from oracle import field_oracle as FO
+    from oracle import vren_oracle as O
+
+    # the box's CPU share (OMP_NUM_THREADS is set to it there); os.cpu_count() is the whole host
+    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+    b = math.exp(math.log(2048 * 0.5 / 16) / 15)
+    lay = FO.GridLayout(16, 2, log2_T, 16, b)
+    g = torch.Generator().manual_seed(0)
+    table = torch.empty(lay.n_params).uniform_(-1e-4, 1e-4, generator=g).requires_grad_(True)
+    px = FO.xavier_uniform_(torch.empty(3072), FO.mlp_shapes(32, 16, 64, 1), g).requires_grad_(True)
+    pr = FO.xavier_uniform_(torch.empty(7168), FO.mlp_shapes(32, 3, 64, 2), g).requires_grad_(True)
+    opt = torch.optim.Adam([px, pr, table], lr=1e-2, eps=1e-15)
+    bf = synthetic.packbits_np(synthetic.ball_density_grid(), 0.01 * 1024 / math.sqrt(3))
+    poses = synthetic.camera_poses()
+    steps, t0 = 0, None
+    while True:
+        o, d = synthetic.random_rays(n_rays, poses, seed=steps)
+        gt = torch.rand(n_rays, 3, generator=g)
+        if steps == 1:
+            t0 = time.time()  # first step warms the allocator/threads
+        _, ht, _ = O.ray_aabb_intersect(o, d, torch.zeros(1, 3), torch.full((1, 3), 0.5), 1)
+        ht[(ht[:, 0, 0] >= 0) & (ht[:, 0, 0] < 0.01), 0, 0] = 0.01
+        ra, x, dd, de, ts, cnt = O.raymarching_train(o, d, ht[:, 0].contiguous(), bf, 1, 0.5, 0.0,
+                                                     torch.rand(n_rays, generator=g), 128, 1024)
+        n = int(cnt[0])
+        x, dd, de, ts = x[:n], dd[:n], de[:n].contiguous(), ts[:n].contiguous()
+        feat = FO.grid_encode(x + 0.5, table, lay)
+        h = FO.mlp_forward(feat, px, 32, 16, 64, 1)
+        sigma = torch.exp(h[:, 0])
+        dn = dd / dd.norm(dim=1, keepdim=True)
+        rgbs = FO.mlp_forward(torch.cat([FO.sh4((dn + 1) / 2), h], 1), pr, 32, 3, 64, 2, "ReLU", "Sigmoid")
+        s_d, c_d = sigma.detach().contiguous(), rgbs.detach().contiguous()
+        tot, op, dep, rgb, ws = O.composite_train_fw(s_d, c_d, de, ts, ra, 1e-4)
+        pred = rgb + (1 - op)[:, None]
+        e = pred - gt
+        dL_drgb = 2 * e / (3 * n_rays)
+        o_ = op + 1e-10
+        dL_dop = -(dL_drgb.sum(1)) + 1e-3 * (-(torch.log(o_) + 1)) / n_rays
+        dsig, drgb = O.composite_train_bw(dL_dop.contiguous(), torch.zeros(n_rays), dL_drgb.contiguous(),
+                                          torch.zeros(n), s_d, c_d, ws, de, ts, ra, op, dep, rgb, 1e-4)
+        opt.zero_grad()
+        torch.autograd.backward([sigma, rgbs], [dsig, drgb])
+        opt.step()
+        steps += 1
+        if t0 is not None and time.time() - t0 >= seconds and steps >= 3:
+            break
+    el = time.time() - t0
+    return {"value": round(n_rays * (steps - 1) / el, 2), "unit": "rays/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{steps - 1} timed training steps x {n_rays} rays, Lego-like synthetic batch, Hash L16 T2^{log2_T},"
+                      f" fp32 torch-CPU field + C oracle march/compositing ({el:.1f} s)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from mfnerf import engine, synthetic
+
+    cfg = engine.StepConfig(n_rays=args.n_rays, log2_T=args.log2_T)
+    step = engine.TrainStep(cfg, device=dev, seed=0)  # identical init on every rank
+    step.set_occupancy(synthetic.ball_density_grid())
+    batches = step.make_batches(8, seed=100 + rank)  # rank-distinct rays
+
+    for i in range(args.warmup):
+        run_step(step, batches[i % len(batches)], world)
+    # occupancy refresh cost (amortised every 16 steps in the reference), measured separately
+    torch.cuda.synchronize()
+    td = time.time()
+    for _ in range(3):
+        step.update_density_grid(warmup=False)
+    torch.cuda.synchronize()
+    density_ms = (time.time() - td) / 3 * 1e3
+    step.set_occupancy(synthetic.ball_density_grid())  # keep the calibrated workload for the timed steps
+
+    events = []
+    n_samples = torch.zeros((), dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for i in range(args.steps):
+        ev = []
+        run_step(step, batches[i % len(batches)], world, ev)
+        n_samples += step.state.counter[0]
+        events.append(ev)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.time() - t0
+    t = torch.tensor([elapsed], device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(t)
+
+    stage_ms = {k: 0.0 for k in STAGES}
+    for ev in events:
+        for (a, ea), (b, eb) in zip(ev[:-1], ev[1:]):
+            stage_ms[b] += ea.elapsed_time(eb)
+    stage_ms = {k: v / args.steps for k, v in stage_ms.items()}
+    mean_samples = float(n_samples) / args.steps
+    rays_total = args.n_rays * args.steps * world
+    value = rays_total / elapsed
+
+    dom = max(BYTES_PER_SAMPLE, key=lambda k: stage_ms[k])
+    dom_bytes = BYTES_PER_SAMPLE[dom] * mean_samples
+    achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(256, args.log2_T, args.cpu_seconds)
+        out = {
+            "metric": "training rays/sec + test PSNR, Synthetic-NeRF Lego 30k steps",
+            "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f16-mfma/f32",
+            "data": "synthetic (seeded Lego-like rays + ball-union occupancy; no dataset in the image)",
+            "config": {"workload": "Lego 800x800 training step, 8192 rays/batch/GPU, Hash L16 F2 T2^%d, rgb 64x2"
+                       % args.log2_T, "global_batch": args.n_rays * world, "rm_s": round(mean_samples / args.n_rays, 2),
+                       "parallelism": f"dp{world}", "psnr": None},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "bytes_per_launch": round(dom_bytes)},
+            "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+            "density_update_ms": round(density_ms, 3),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

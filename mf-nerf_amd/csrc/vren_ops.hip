@@ -375,6 +375,38 @@ __global__ void distortion_bw_kernel(const float* __restrict__ dL_dloss, const f
     }
 }
 
+
+// ------------------------------------------------------------------ NeRF loss (losses.py:47-60, train.py:178)
+// pred = rgb + bg*(1-opacity) (rendering.py:153-161); loss = mean((pred-gt)^2) + lambda*mean(-o ln o),
+// o = opacity + 1e-10.  Writes dL/drgb, dL/dopacity of that scalar and accumulates it into loss_sum.
+__global__ void nerf_loss_kernel(const float* __restrict__ rgb, const float* __restrict__ opacity,
+                                 const float* __restrict__ gt, int64_t n_rays, float lambda_o, float bg0, float bg1,
+                                 float bg2, float* __restrict__ dL_drgb, float* __restrict__ dL_dop,
+                                 float* __restrict__ loss_sum) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float l = 0.0f;
+    if (r < n_rays) {
+        const float op = opacity[r];
+        const float inv3n = 1.0f / (3.0f * (float)n_rays), invn = 1.0f / (float)n_rays;
+        const float bg[3] = {bg0, bg1, bg2};
+        float dop = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float e = rgb[3 * r + c] + bg[c] * (1.0f - op) - gt[3 * r + c];
+            l += e * e * inv3n;
+            const float g = 2.0f * e * inv3n;
+            dL_drgb[3 * r + c] = g;
+            dop -= bg[c] * g;
+        }
+        const float o = op + 1e-10f;
+        l += lambda_o * (-o * logf(o)) * invn;
+        dL_dop[r] = dop + lambda_o * (-(logf(o) + 1.0f)) * invn;
+    }
+    // wave reduction, one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) l += __shfl_down(l, off, 64);
+    if ((threadIdx.x & 63) == 0 && loss_sum) atomicAdd(loss_sum, l);
+}
+
 inline unsigned blocks_for(int64_t n, int b) { return (unsigned)div_up<int64_t>(n, b); }
 
 }  // namespace
@@ -547,6 +579,17 @@ int mfnerf_distortion_loss_bw(const float* dL_dloss, const float* ws_incl, const
     hipLaunchKernelGGL(distortion_bw_kernel, dim3(blocks_for(n_rays, RAY_BLOCK)), dim3(RAY_BLOCK), 0, stream,
                        dL_dloss, ws_incl, wts_incl, ws, deltas, ts, rays_a, n_rays, dL_dws);
     return mfn_check_launch("distortion_loss_bw");
+}
+
+int mfnerf_nerf_loss(const float* rgb, const float* opacity, const float* target, int64_t n_rays, float lambda_opacity,
+                     float bg_r, float bg_g, float bg_b, float* dL_drgb, float* dL_dopacity, float* loss_sum,
+                     mfnerf_stream_t stream) {
+    if (n_rays < 0) { mfn_set_error("nerf_loss: bad size"); return MFN_ERR_INVALID; }
+    if (n_rays == 0) return MFN_OK;
+    if (!rgb || !opacity || !target || !dL_drgb || !dL_dopacity) { mfn_set_error("nerf_loss: null pointer"); return MFN_ERR_INVALID; }
+    hipLaunchKernelGGL(nerf_loss_kernel, dim3(blocks_for(n_rays, 256)), dim3(256), 0, stream, rgb, opacity, target,
+                       n_rays, lambda_opacity, bg_r, bg_g, bg_b, dL_drgb, dL_dopacity, loss_sum);
+    return mfn_check_launch("nerf_loss");
 }
 
 }  // extern "C"

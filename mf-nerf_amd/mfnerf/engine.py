@@ -1,0 +1,258 @@
+"""The fused MI355X training step: one NeRF training iteration of the reference's hot path
+(train.py:164-190 -> rendering.py:121-163 -> losses.py:47-60 -> backward -> FusedAdam) as a
+fixed sequence of gfx950 kernels on one stream, with every intermediate resident in HBM and the
+sample count kept on the device (no host synchronisation, so a step is capturable in a HIP graph).
+
+Buffers are sized once for the worst case (n_rays * MAX_SAMPLES samples, as the reference's
+raymarching_train does); kernels that run per sample read the live count from `counter[0]` and
+grid-stride over it.  Parameters live in one flat fp32 vector
+    params = [xyz MLP (3072) | rgb MLP (7168) | grid table (L*F*entries)]
+so Adam is one launch and the gradient zeroing one memset; an fp16 mirror of the whole vector is
+refreshed by the same Adam pass and is what the grid kernels gather from.
+Multi-GPU: the caller all-reduces `grads` between backward() and optimizer() (bench.py).
+"""
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import synthetic
+from ._lib import call, load, ptr, stream
+from .field import XYZ_NET_PARAMS, rgb_net_params
+from .grid import GridLayout
+
+MAX_SAMPLES = 1024
+NEAR_DISTANCE = 0.01
+SQRT3 = 3 ** 0.5
+
+
+@dataclass
+class StepConfig:
+    n_rays: int = 8192
+    scale: float = 0.5
+    L: int = 16
+    F: int = 2
+    log2_T: int = 19
+    N_min: int = 16
+    N_max: int = 2048
+    grid: str = "Hash"
+    N_tables: int = 1
+    rgb_width: int = 64
+    lr: float = 1e-2
+    eps: float = 1e-15
+    lambda_opacity: float = 1e-3
+    T_threshold: float = 1e-4
+    max_samples: int = MAX_SAMPLES
+
+
+@dataclass
+class Batch:
+    rays_o: torch.Tensor
+    rays_d: torch.Tensor
+    rgb: torch.Tensor
+
+
+class _State:
+    pass
+
+
+class TrainStep:
+    def __init__(self, cfg: StepConfig, device="cuda", seed=0):
+        self.cfg = cfg
+        self.dev = torch.device(device)
+        load()
+        c = cfg
+        self.cascades = max(1 + int(np.ceil(np.log2(2 * c.scale))), 1)
+        self.G = 128
+        b = float(np.exp(np.log(c.N_max * c.scale / c.N_min) / (c.L - 1)))
+        self.layout = GridLayout(c.L, c.F, c.log2_T, c.N_min, b, c.grid, c.N_tables)
+        self.desc = self.layout.desc()
+        self.n_rgb = rgb_net_params(c.rgb_width)
+        self.off_rgb = XYZ_NET_PARAMS
+        self.off_table = XYZ_NET_PARAMS + self.n_rgb
+        self.n_params = self.off_table + self.layout.n_params
+        s32 = np.float32(c.scale)
+        self.x_min, self.x_range = float(-s32), float(np.float32(s32) - np.float32(-s32))
+
+        dev = self.dev
+        g = torch.Generator().manual_seed(seed)
+        p = torch.empty(self.n_params)
+        off = 0
+        for o, k in [(64, 32), (16, 64), (c.rgb_width, 32), (c.rgb_width, c.rgb_width), (16, c.rgb_width)]:
+            s = math.sqrt(6.0 / (o + k))  # tcnn Xavier-uniform per matrix
+            p[off:off + o * k].uniform_(-s, s, generator=g)
+            off += o * k
+        p[self.off_table:].uniform_(-1e-4, 1e-4, generator=g)  # tcnn grid init
+        self.params = p.to(dev)
+        self.grads = torch.zeros(self.n_params, device=dev)
+        self.m = torch.zeros(self.n_params, device=dev)
+        self.v = torch.zeros(self.n_params, device=dev)
+        self.p16 = self.params.half()
+        self.packed = torch.empty(load().mfnerf_field_packed_bytes(c.rgb_width) // 2, dtype=torch.float16,
+                                  device=dev)
+        self._pack()
+        self.adam_step = 0
+
+        # scene bounding box (networks.py:18-23) and occupancy
+        self.center = torch.zeros(1, 3, device=dev)
+        self.half_size = torch.full((1, 3), c.scale, device=dev)
+        self.density_grid = torch.zeros(self.cascades, self.G ** 3, device=dev)
+        self.bitfield = torch.zeros(self.cascades * self.G ** 3 // 8, dtype=torch.uint8, device=dev)
+
+        N, cap = c.n_rays, c.n_rays * c.max_samples
+        self.cap = cap
+        st = _State()
+        f32 = dict(dtype=torch.float32, device=dev)
+        st.hit_cnt = torch.empty(N, dtype=torch.int32, device=dev)
+        st.hits = torch.empty(N, 1, 2, **f32)
+        st.hits_t = st.hits[:, 0]
+        st.hits_idx = torch.empty(N, 1, dtype=torch.int64, device=dev)
+        st.noise = torch.empty(N, **f32)
+        st.rays_a = torch.empty(N, 3, dtype=torch.int64, device=dev)
+        st.xyzs = torch.empty(cap, 3, **f32)
+        st.dirs = torch.empty(cap, 3, **f32)
+        st.deltas = torch.empty(cap, **f32)
+        st.ts = torch.empty(cap, **f32)
+        st.counter = torch.zeros(2, dtype=torch.int32, device=dev)
+        st.march_ws = torch.empty(max(16, load().mfnerf_raymarching_train_workspace(N)), dtype=torch.uint8,
+                                  device=dev)
+        st.feat = torch.empty(cap, c.L * c.F, dtype=torch.float16, device=dev)
+        st.sigma = torch.empty(cap, **f32)
+        st.rgb_s = torch.empty(cap, 3, **f32)
+        st.total = torch.empty(N, dtype=torch.int64, device=dev)
+        st.opacity = torch.empty(N, **f32)
+        st.depth = torch.empty(N, **f32)
+        st.rgb = torch.empty(N, 3, **f32)
+        st.ws = torch.empty(cap, **f32)
+        st.dL_drgb = torch.empty(N, 3, **f32)
+        st.dL_dop = torch.empty(N, **f32)
+        st.zeros_ray = torch.zeros(N, **f32)       # dL/ddepth (unused by the loss)
+        st.zeros_samp = torch.zeros(cap, **f32)    # dL/dws (no distortion loss by default)
+        st.dsig = torch.empty(cap, **f32)
+        st.drgb_s = torch.empty(cap, 3, **f32)
+        st.dfeat = torch.empty(cap, c.L * c.F, **f32)
+        st.field_ws = torch.empty(load().mfnerf_field_bw_workspace(cap, c.rgb_width) // 4, **f32)
+        st.loss_sum = torch.zeros(1, **f32)
+        self.state = st
+        self.gen = torch.Generator(device=dev)
+        self.gen.manual_seed(seed + 1)
+        # fp16 backward scale: per-sample grads are O(1/n_rays); 2^(floor(log2 N)-2) keeps them normal
+        self.grad_scale = float(2.0 ** max(0, int(math.floor(math.log2(N))) - 2))
+
+    # ---------------------------------------------------------------- data
+    def make_batches(self, k, seed=0):
+        """k synthetic Lego-like ray batches (mfnerf.synthetic), resident on the device."""
+        poses = synthetic.camera_poses(seed=seed)
+        out = []
+        for i in range(k):
+            o, d = synthetic.random_rays(self.cfg.n_rays, poses, seed=seed * 1000 + i)
+            dn = d / d.norm(dim=1, keepdim=True)
+            gt = 0.5 + 0.5 * torch.sin(3 * dn + torch.tensor([0.0, 1.0, 2.0]))  # smooth view-dependent target
+            out.append(Batch(o.to(self.dev), d.to(self.dev), gt.float().to(self.dev)))
+        return out
+
+    def set_occupancy(self, density_grid):
+        """Install a (C, G^3) density grid and pack it with the reference's threshold."""
+        self.density_grid.copy_(density_grid.to(self.dev))
+        thr = 0.01 * MAX_SAMPLES / SQRT3
+        call("mfnerf_packbits", ptr(self.density_grid), self.bitfield.numel(), thr, None, ptr(self.bitfield), stream())
+
+    def _pack(self):
+        call("mfnerf_field_pack_weights", ptr(self.params), ptr(self.params[self.off_rgb:]), self.cfg.rgb_width,
+             ptr(self.packed), stream())
+
+    # ---------------------------------------------------------------- the step
+    def forward(self, batch: Batch):
+        c, st, s = self.cfg, self.state, stream()
+        N, cap = c.n_rays, self.cap
+        call("mfnerf_ray_aabb_intersect", ptr(batch.rays_o), ptr(batch.rays_d), ptr(self.center),
+             ptr(self.half_size), N, 1, 1, ptr(st.hit_cnt), ptr(st.hits), ptr(st.hits_idx), s)
+        t1 = st.hits[:, 0, 0]
+        t1.masked_fill_((t1 >= 0) & (t1 < NEAR_DISTANCE), NEAR_DISTANCE)  # rendering.py:29
+        torch.rand(N, generator=self.gen, device=self.dev, out=st.noise)  # custom_functions.py:83
+        call("mfnerf_raymarching_train", ptr(batch.rays_o), ptr(batch.rays_d), ptr(st.hits_t), 2, ptr(self.bitfield),
+             self.cascades, float(c.scale), 0.0 if c.scale <= 0.5 else 1 / 256, ptr(st.noise), self.G,
+             c.max_samples, N, cap, ptr(st.rays_a), ptr(st.xyzs), ptr(st.dirs), ptr(st.deltas), ptr(st.ts),
+             ptr(st.counter), ptr(st.march_ws), s)
+        call("mfnerf_grid_encode_fw", ptr(st.xyzs), cap, ptr(st.counter), self.x_min, self.x_range, self.desc,
+             ptr(self.p16[self.off_table:]), ptr(st.feat), s)
+        call("mfnerf_field_fw", ptr(st.feat), ptr(st.dirs), cap, ptr(st.counter), ptr(self.packed), c.rgb_width, 0,
+             ptr(st.sigma), ptr(st.rgb_s), s)
+        call("mfnerf_composite_train_fw", ptr(st.sigma), ptr(st.rgb_s), ptr(st.deltas), ptr(st.ts), ptr(st.rays_a),
+             N, cap, c.T_threshold, ptr(st.total), ptr(st.opacity), ptr(st.depth), ptr(st.rgb), ptr(st.ws), s)
+        bg = 1.0 if c.scale <= 0.5 else 0.0
+        st.loss_sum.zero_()
+        call("mfnerf_nerf_loss", ptr(st.rgb), ptr(st.opacity), ptr(batch.rgb), N, c.lambda_opacity, bg, bg, bg,
+             ptr(st.dL_drgb), ptr(st.dL_dop), ptr(st.loss_sum), s)
+
+    def backward(self):
+        c, st, s = self.cfg, self.state, stream()
+        N, cap = c.n_rays, self.cap
+        call("mfnerf_composite_train_bw", ptr(st.dL_dop), ptr(st.zeros_ray), ptr(st.dL_drgb), ptr(st.zeros_samp),
+             ptr(st.sigma), ptr(st.rgb_s), ptr(st.ws), ptr(st.deltas), ptr(st.ts), ptr(st.rays_a), ptr(st.opacity),
+             ptr(st.depth), ptr(st.rgb), N, cap, c.T_threshold, ptr(st.dsig), ptr(st.drgb_s), s)
+        self.grads.zero_()
+        call("mfnerf_field_bw", ptr(st.feat), ptr(st.dirs), cap, ptr(st.counter), ptr(self.packed), c.rgb_width,
+             ptr(st.dsig), ptr(st.drgb_s), self.grad_scale, ptr(st.dfeat), ptr(self.grads),
+             ptr(self.grads[self.off_rgb:]), ptr(st.field_ws), s)
+        call("mfnerf_grid_encode_bw", ptr(st.xyzs), cap, ptr(st.counter), self.x_min, self.x_range, self.desc,
+             ptr(st.dfeat), ptr(self.grads[self.off_table:]), s)
+
+    def optimizer(self, lr=None):
+        c = self.cfg
+        self.adam_step += 1
+        call("mfnerf_adam_step", ptr(self.params), ptr(self.grads), ptr(self.m), ptr(self.v), ptr(self.p16),
+             self.n_params, float(c.lr if lr is None else lr), 0.9, 0.999, c.eps, 1.0, self.adam_step, None, stream())
+        self._pack()
+
+    def step(self, batch: Batch):
+        self.forward(batch)
+        self.backward()
+        self.optimizer()
+
+    # ---------------------------------------------------------------- occupancy (networks.py:242-271)
+    @torch.no_grad()
+    def update_density_grid(self, warmup=False, decay=0.95):
+        """Device-only version of NGP.update_density_grid: no .item(), the packbits threshold is
+        read from device memory."""
+        c = self.cfg
+        G, dev = self.G, self.dev
+        thr = 0.01 * MAX_SAMPLES / SQRT3
+        tmp = torch.zeros_like(self.density_grid)
+        for ci in range(self.cascades):
+            if warmup:
+                r = torch.arange(G, dtype=torch.int32, device=dev)
+                coords = torch.stack(torch.meshgrid(r, r, r, indexing="ij"), -1).reshape(-1, 3).contiguous()
+            else:
+                M = G ** 3 // 4
+                coords1 = torch.randint(G, (M, 3), dtype=torch.int32, device=dev, generator=self.gen)
+                occ = self.density_grid[ci] > thr
+                # M samples among occupied cells (uniform over the occupied set) without a host sync
+                w = occ.float() + 1e-30
+                idx2 = torch.multinomial(w, M, replacement=True, generator=self.gen).int().contiguous()
+                coords2 = torch.empty(M, 3, dtype=torch.int32, device=dev)
+                call("mfnerf_morton3d_invert", ptr(idx2), M, ptr(coords2), stream())
+                coords = torch.cat([coords1, coords2]).contiguous()
+            idx = torch.empty(coords.shape[0], dtype=torch.int32, device=dev)
+            call("mfnerf_morton3d", ptr(coords), coords.shape[0], ptr(idx), stream())
+            s = min(2 ** (ci - 1), c.scale)
+            hgs = s / G
+            xyz = (coords / (G - 1) * 2 - 1) * (s - hgs)
+            xyz += (torch.rand(xyz.shape, generator=self.gen, device=dev) * 2 - 1) * hgs
+            xyz = xyz.contiguous()
+            n = xyz.shape[0]
+            feat = torch.empty(n, c.L * c.F, dtype=torch.float16, device=dev)
+            sig = torch.empty(n, device=dev)
+            call("mfnerf_grid_encode_fw", ptr(xyz), n, None, self.x_min, self.x_range, self.desc,
+                 ptr(self.p16[self.off_table:]), ptr(feat), stream())
+            call("mfnerf_field_fw", ptr(feat), None, n, None, ptr(self.packed), c.rgb_width, 1, ptr(sig), None,
+                 stream())
+            tmp[ci, idx.long()] = sig
+        self.density_grid.copy_(torch.where(self.density_grid < 0, self.density_grid,
+                                            torch.maximum(self.density_grid * decay, tmp)))
+        pos = self.density_grid > 0
+        mean = (self.density_grid * pos).sum() / pos.sum().clamp(min=1)
+        thr_dev = torch.minimum(mean, torch.tensor(thr, device=dev)).reshape(1)
+        call("mfnerf_packbits", ptr(self.density_grid), self.bitfield.numel(), 0.0, ptr(thr_dev), ptr(self.bitfield),
+             stream())

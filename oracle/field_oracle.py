@@ -292,3 +292,57 @@ class NetworkWithInputEncoding(torch.nn.Module):
         feat = grid_encode(x.float(), self.params[self.n_net:], self.enc.layout)
         c = self.net
         return mlp_forward(feat, self.params[:self.n_net], c.n_in, c.n_out, c.width, c.depth, c.act, c.out_act)
+
+
+# ---- fp16-point emulation of the NGP field head (the arithmetic tcnn and the HIP kernels share)
+
+
+def _h(t):
+    return t.half().float()
+
+
+def ngp_field_fw16(feat16, dirs, px, pr, width=64):
+    """NGP.forward's MLP part (networks.py:106,144-147) with every operand rounded to fp16 where
+    tcnn holds it in fp16: feat, weights, ReLU outputs, h (the xyz net's half output) and SH.
+    Returns sigma (N), rgb (N,3) fp32 and the rounded activations for the backward."""
+    f = feat16.float()
+    W1 = _h(px[:2048].view(64, 32)); W2 = _h(px[2048:3072].view(16, 64))
+    R1 = _h(pr[:width * 32].view(width, 32))
+    R2 = _h(pr[width * 32:width * 32 + width * width].view(width, width))
+    R3 = _h(pr[width * 32 + width * width:].view(16, width))
+    y1 = _h(torch.relu(f @ W1.t()))
+    h = _h(y1 @ W2.t())
+    dn = dirs / torch.norm(dirs, dim=1, keepdim=True)
+    sh = _h(sh4((dn + 1) / 2))
+    inp = torch.cat([sh, h], 1)
+    r1 = _h(torch.relu(inp @ R1.t()))
+    r2 = _h(torch.relu(r1 @ R2.t()))
+    rgb = torch.sigmoid((r2 @ R3.t())[:, :3])
+    acts = dict(f=f, W1=W1, W2=W2, R1=R1, R2=R2, R3=R3, y1=y1, h=h, inp=inp, r1=r1, r2=r2, rgb=rgb)
+    return torch.exp(h[:, 0]), rgb, acts
+
+
+def ngp_field_bw16(acts, dL_dsigma, dL_drgb, S):
+    """Manual backward of ngp_field_fw16 with the incoming grads scaled by S and every data
+    gradient rounded to fp16 after its ReLU mask (the fp16 backward products).  Returns
+    dL/dfeat (N,32), d xyz-MLP params (3072), d rgb-MLP params, all unscaled fp32."""
+    a = acts
+    N = a["f"].shape[0]
+    rgb = a["rgb"]
+    dO = torch.zeros(N, 16)
+    dO[:, :3] = dL_drgb * S * rgb * (1 - rgb)
+    dO = _h(dO)
+    dWr3 = dO.t() @ a["r2"]
+    dr2 = _h((dO @ a["R3"]) * (a["r2"] > 0))
+    dWr2 = dr2.t() @ a["r1"]
+    dr1 = _h((dr2 @ a["R2"]) * (a["r1"] > 0))
+    dWr1 = dr1.t() @ a["inp"]
+    dh = (dr1 @ a["R1"])[:, 16:].clone()
+    dh[:, 0] += dL_dsigma * S * torch.exp(a["h"][:, 0].clamp(-15, 15))  # TruncExp bw
+    dh = _h(dh)
+    dW2 = dh.t() @ a["y1"]
+    dy1 = _h((dh @ a["W2"]) * (a["y1"] > 0))
+    dW1 = dy1.t() @ a["f"]
+    dX = dy1 @ a["W1"]
+    return (dX / S, torch.cat([dW1.flatten(), dW2.flatten()]) / S,
+            torch.cat([dWr1.flatten(), dWr2.flatten(), dWr3.flatten()]) / S)

@@ -71,40 +71,19 @@ def test_grid_encode_world_coords_normalisation(gpu):
     assert torch.allclose(out.float().cpu(), ref, atol=1e-3, rtol=0)
 
 
-def _h(t):
-    return t.half().float()
-
-
-def oracle_field(feat16, dirs, px, pr, width=64):
-    """fp32 restatement of the two FullyFusedMLPs + TruncExp + SH4 with operands rounded to fp16
-    where tcnn (and the kernels) hold them in fp16."""
-    W1 = _h(px[:2048].view(64, 32)); W2 = _h(px[2048:3072].view(16, 64))
-    R1 = _h(pr[:width * 32].view(width, 32)); R2 = _h(pr[width * 32:width * 32 + width * width].view(width, width))
-    R3 = _h(pr[width * 32 + width * width:].view(16, width))
-    y1 = _h(torch.relu(feat16 @ W1.t()))
-    h = _h(y1 @ W2.t())
-    sigma = torch.exp(h[:, 0])
-    dn = dirs / torch.norm(dirs, dim=1, keepdim=True)
-    sh = _h(FO.sh4((dn + 1) / 2))
-    r1 = _h(torch.relu(torch.cat([sh, h], 1) @ R1.t()))
-    r2 = _h(torch.relu(r1 @ R2.t()))
-    rgb = torch.sigmoid(r2 @ R3.t())[:, :3]
-    return sigma, rgb
-
-
-def _field_inputs(N, seed=4):
+def _field_inputs(N, seed=4, wscale=3.0):
     g = torch.Generator().manual_seed(seed)
     feat = (torch.rand(N, 32, generator=g) - 0.5).half()
     dirs = torch.randn(N, 3, generator=g)
-    px = FO.xavier_uniform_(torch.empty(3072), FO.mlp_shapes(32, 16, 64, 1), g) * 3
-    pr = FO.xavier_uniform_(torch.empty(7168), FO.mlp_shapes(32, 3, 64, 2), g) * 3
+    px = FO.xavier_uniform_(torch.empty(3072), FO.mlp_shapes(32, 16, 64, 1), g) * wscale
+    pr = FO.xavier_uniform_(torch.empty(7168), FO.mlp_shapes(32, 3, 64, 2), g) * wscale
     return feat, dirs, px, pr
 
 
 @pytest.mark.parametrize("N", [1, 31, 33, 5000])
 def test_field_fw(gpu, N):
     feat, dirs, px, pr = _field_inputs(N)
-    s_ref, c_ref = oracle_field(feat.float(), dirs, px, pr)
+    s_ref, c_ref, _ = FO.ngp_field_fw16(feat, dirs, px, pr)
     packed = FLD.pack_field_weights(px.to(gpu), pr.to(gpu))
     s, c = FLD.field_fw(feat.to(gpu), dirs.to(gpu), N, packed)
     # h0 is one fp16 value on both sides; sigma = exp(h0): fp16-accumulation-order noise only
@@ -114,40 +93,42 @@ def test_field_fw(gpu, N):
     assert torch.equal(sd.cpu(), s.cpu())
 
 
-def test_field_bw(gpu):
-    N = 3000
-    feat, dirs, px, pr = _field_inputs(N, seed=5)
-    g = torch.Generator().manual_seed(6)
-    dsig = torch.randn(N, generator=g) * 1e-6
-    drgb = torch.randn(N, 3, generator=g) * 1e-5
-    # oracle: fp32 autograd through the same fp16-rounded forward
+def _fp32_autograd(feat, dirs, px, pr, dsig, drgb):
     f32 = feat.float().requires_grad_(True)
-    pxr = px.clone().requires_grad_(True)
-    prr = pr.clone().requires_grad_(True)
+    a = px.half().float().requires_grad_(True)
+    b = pr.half().float().requires_grad_(True)
+    W1 = a[:2048].view(64, 32); W2 = a[2048:3072].view(16, 64)
+    R1 = b[:2048].view(64, 32); R2 = b[2048:6144].view(64, 64); R3 = b[6144:].view(16, 64)
+    y1 = torch.relu(f32 @ W1.t()); h = y1 @ W2.t()
+    sigma = torch.exp(h[:, 0])
+    dn = dirs / torch.norm(dirs, dim=1, keepdim=True)
+    r1 = torch.relu(torch.cat([FO.sh4((dn + 1) / 2), h], 1) @ R1.t()); r2 = torch.relu(r1 @ R2.t())
+    c = torch.sigmoid(r2 @ R3.t())[:, :3]
+    ((sigma * dsig).sum() + (c * drgb).sum()).backward()
+    return f32.grad, a.grad, b.grad
 
-    def fwd(f, a, b):
-        W1 = a[:2048].view(64, 32); W2 = a[2048:3072].view(16, 64)
-        R1 = b[:2048].view(64, 32); R2 = b[2048:6144].view(64, 64); R3 = b[6144:].view(16, 64)
-        y1 = torch.relu(f @ W1.t()); h = y1 @ W2.t()
-        sigma = torch.exp(h[:, 0])
-        dn = dirs / torch.norm(dirs, dim=1, keepdim=True)
-        sh = FO.sh4((dn + 1) / 2)
-        r1 = torch.relu(torch.cat([sh, h], 1) @ R1.t()); r2 = torch.relu(r1 @ R2.t())
-        return sigma, torch.sigmoid(r2 @ R3.t())[:, :3]
 
-    s, c = fwd(f32, pxr, prr)
-    ((s * dsig).sum() + (c * drgb).sum()).backward()
+@pytest.mark.parametrize("wscale,sig_on", [(1.0, 0.0), (1.0, 1.0), (3.0, 1.0)])
+def test_field_bw(gpu, wscale, sig_on):
+    N = 3000
+    feat, dirs, px, pr = _field_inputs(N, seed=5, wscale=wscale)
+    g = torch.Generator().manual_seed(6)
+    dsig = torch.randn(N, generator=g) * 1e-6 * sig_on
+    drgb = torch.randn(N, 3, generator=g) * 1e-5
+    S = 16384.0
+    sig, _, acts = FO.ngp_field_fw16(feat, dirs, px, pr)
+    ref16 = FO.ngp_field_bw16(acts, dsig, drgb, S)
+    ref32 = _fp32_autograd(feat, dirs, px, pr, dsig, drgb)
     packed = FLD.pack_field_weights(px.to(gpu), pr.to(gpu))
     dfeat = torch.empty(N, 32, device=gpu)
     gx = torch.zeros(3072, device=gpu)
     gr = torch.zeros(7168, device=gpu)
     ws = FLD.field_bw_workspace(N, 64, gpu)
-    smax = float(torch.maximum(drgb.abs().max(), (dsig * s.detach()).abs().max()))
-    S = FLD.pow2_grad_scale(smax)
     FLD.field_bw(feat.to(gpu), dirs.to(gpu), N, packed, dsig.to(gpu), drgb.to(gpu), S, dfeat, gx, gr, ws)
-    # fp16 operands in every backward product: compare relative to each tensor's scale
-    for got, ref in ((dfeat.cpu(), f32.grad), (gx.cpu(), pxr.grad), (gr.cpu(), prr.grad)):
-        err = (got - ref).abs().max() / ref.abs().max()
-        assert err < 2e-2, float(err)
-        cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0)
-        assert cos > 0.999, float(cos)
+    for got, r16, r32 in zip((dfeat.cpu(), gx.cpu(), gr.cpu()), ref16, ref32):
+        # vs the fp16-point emulation: only fp32 summation-order differences remain
+        err = float((got - r16).abs().max() / r16.abs().max())
+        assert err < 2e-3, err
+        # vs pure fp32 autograd: the fp16 quantisation tcnn's backward has too (~1% rms)
+        cos = float(torch.nn.functional.cosine_similarity(got.flatten(), r32.flatten(), dim=0))
+        assert cos > 0.9995, cos

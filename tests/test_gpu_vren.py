@@ -20,7 +20,8 @@ def _to(d, *ts):
 
 
 def lego_inputs(n_rays, seed=0, scale=0.5, cascades=1, exp_step=0.0):
-    poses = synthetic.camera_poses(seed=seed, radius=1.5 if scale <= 0.5 else 3.0 * scale)
+    # real (unbounded) scenes: cameras inside the box, near the content (mip-NeRF 360 style)
+    poses = synthetic.camera_poses(seed=seed, radius=1.5 if scale <= 0.5 else 2.0)
     o, d = synthetic.random_rays(n_rays, poses, seed=seed)
     grid = synthetic.ball_density_grid(cascades=cascades, scale=scale, seed=seed)
     bf = synthetic.packbits_np(grid, 0.01 * 1024 / SQRT3)
