@@ -51,6 +51,7 @@ STAGES = ["prep", "march", "grid_fw", "field_fw", "composite_fw", "composite_bw"
 
 def run_step(step, batch, world, ev=None):
     """One training step; if ev is given, records a CUDA event after every stage."""
+    from mfnerf import dp
     from mfnerf._lib import call, ptr, stream
     st, c = step.state, step.cfg
     N, cap = c.n_rays, step.cap
@@ -98,7 +99,7 @@ def run_step(step, batch, world, ev=None):
          ptr(st.dfeat), ptr(step.grads[step.off_table:]), s)
     mark("grid_bw")
     if world > 1:
-        torch.distributed.all_reduce(step.grads, op=torch.distributed.ReduceOp.AVG)
+        dp.allreduce_mean_(step.grads)  # the one exchange per step (mfnerf/dp.py)
     mark("allreduce")
     step.optimizer()
     mark("adam")
@@ -173,12 +174,12 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from mfnerf import engine, synthetic
+    from mfnerf import dp, engine, synthetic
 
     cfg = engine.StepConfig(n_rays=args.n_rays, log2_T=args.log2_T)
     step = engine.TrainStep(cfg, device=dev, seed=0)  # identical init on every rank
     step.set_occupancy(synthetic.ball_density_grid())
-    batches = step.make_batches(8, seed=100 + rank)  # rank-distinct rays
+    batches = step.make_batches(8, seed=dp.rank_seed(100, rank))  # rank-distinct rays
 
     for i in range(args.warmup):
         run_step(step, batches[i % len(batches)], world)
@@ -206,10 +207,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.time() - t0
-    t = torch.tensor([elapsed], device=dev)
-    if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    elapsed = float(t)
+    elapsed = dp.max_over_ranks(elapsed, dev)  # the slowest rank's clock
 
     stage_ms = {k: 0.0 for k in STAGES}
     for ev in events:

@@ -5,9 +5,7 @@
 // store), so the 4 lanes of a point write its 64-B output row with one coalesced 64-B burst and
 // every lane keeps 32 independent 4-B corner gathers in flight.  Accumulation is fp32 (tcnn
 // accumulates in half; the difference is inside the fp16 output rounding).
-// Backward: 16 lanes per point (one level each), fp32 dL/dy read as one 128-B row per point,
-// two no-return global_atomic_add_f32 per corner (features f0,f1 of the same entry share a
-// 64-B line).
+// Backward: see grid_bw_kernel (request-shaped float atomics with in-wave run merging).
 #include "common.hpp"
 #include "../../include/mfnerf.h"
 
@@ -109,30 +107,58 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_fw_kernel(const float* __restr
     }
 }
 
+// Backward.  The table gradient is a scatter-add; on MI355X a float atomic executes at the memory
+// side and costs one 64-B request per distinct line of a wave-instruction (MI355X_MICROARCH.md,
+// "Global float atomics"), so the kernel is shaped to minimise requests, not bytes:
+//   * one wave = 16 consecutive samples of ONE level; lane = (sample s = lane>>2, x-corner bit
+//     xb, feature f): per (y,z) corner pair the 4 lanes of a sample add to table entries idx(x),
+//     idx(x+1) x features f0,f1 -- one 16-B span (one line) for dense levels and, for hashed
+//     levels, whenever x->x+1 leaves the low bits of the hash alone (7/8 of the time);
+//   * samples are consecutive along a ray, so at coarse levels many neighbours hit the same
+//     corner: a 4-step segmented suffix scan over each lane's stride-4 stream merges such runs
+//     and only run heads issue the atomic (level 0 of the Lego config merges ~37 samples).
 __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restrict__ X, int64_t n,
                                                              const int32_t* __restrict__ n_dev, float x_min,
                                                              float x_range, const mfnerf_grid_desc D,
                                                              const float* __restrict__ dy, float* __restrict__ grad) {
     const int L_ = D.n_levels;
+    const int lane = threadIdx.x & 63, s = lane >> 2, xb = (lane >> 1) & 1, f = lane & 1;
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
-    const int64_t total = nn * L_;
-    for (int64_t t = (int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x; t < total; t += (int64_t)gridDim.x * ENC_BLOCK) {
-    const int64_t i = t / L_;
-    const int l = (int)(t - i * L_);
-    const float2 g = reinterpret_cast<const float2*>(dy + i * (2 * L_))[l];
-    if (g.x == 0.0f && g.y == 0.0f) continue;
-    const float x = (X[3 * i] - x_min) / x_range;
-    const float y = (X[3 * i + 1] - x_min) / x_range;
-    const float z = (X[3 * i + 2] - x_min) / x_range;
-    const LevelGeo Lg = level_geo(D.scale[l], x, y, z);
-    float* gt = grad + 2 * (int64_t)D.offset[l];
+    const int64_t items = div_up<int64_t>(nn, 16) * L_;
+    const int64_t wave0 = ((int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * ENC_BLOCK) >> 6;
+    for (int64_t item = wave0; item < items; item += n_waves) {
+        const int l = (int)(item % L_);
+        const int64_t i = (item / L_) * 16 + s;
+        const bool valid = i < nn;
+        float g = 0.0f, x = 0.0f, y = 0.0f, z = 0.0f;
+        if (valid) {
+            g = dy[i * (2 * L_) + 2 * l + f];
+            x = (X[3 * i] - x_min) / x_range;
+            y = (X[3 * i + 1] - x_min) / x_range;
+            z = (X[3 * i + 2] - x_min) / x_range;
+        }
+        const LevelGeo Lg = level_geo(D.scale[l], x, y, z);
+        float* gt = grad + 2 * (int64_t)D.offset[l];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const uint32_t idx = corner_index(D, l, Lg.g[0] + (c & 1), Lg.g[1] + ((c >> 1) & 1), Lg.g[2] + ((c >> 2) & 1));
-        const float w = corner_weight(Lg, c);
-        __hip_atomic_fetch_add(gt + 2 * idx, w * g.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(gt + 2 * idx + 1, w * g.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+        for (int yz = 0; yz < 4; ++yz) {
+            const int c = xb | (yz << 1);
+            const uint32_t idx =
+                corner_index(D, l, Lg.g[0] + (c & 1), Lg.g[1] + ((c >> 1) & 1), Lg.g[2] + ((c >> 2) & 1));
+            const uint32_t key = valid ? idx : 0xFFFFFFFFu;
+            float v = corner_weight(Lg, c) * g;
+            const uint32_t kp = __shfl(key, lane - 4, 64), kn = __shfl(key, lane + 4, 64);
+            const bool head = (s == 0) || kp != key;
+            bool stop = (s == 15) || kn != key;  // this lane ends its run
+#pragma unroll
+            for (int d = 1; d < 16; d <<= 1) {  // segmented suffix sum (run head ends up with the total)
+                const float vp = __shfl(v, lane + 4 * d, 64);
+                const bool sp = __shfl((int)stop, lane + 4 * d, 64);
+                if (!stop) { v += vp; stop = sp; }
+            }
+            if (head && valid && v != 0.0f)
+                __hip_atomic_fetch_add(gt + 2 * idx + f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -177,8 +203,8 @@ int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float
     if (n < 0) { mfn_set_error("grid_encode_bw: bad size"); return MFN_ERR_INVALID; }
     if (n == 0) return MFN_OK;
     if (!x || !dL_dout || !grad_table) { mfn_set_error("grid_encode_bw: null pointer"); return MFN_ERR_INVALID; }
-    const int64_t want = div_up<int64_t>(n * desc->n_levels, ENC_BLOCK);
-    const int64_t blocks = want < 16384 ? want : 16384;
+    const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16) * desc->n_levels, ENC_BLOCK / 64);
+    const int64_t blocks = want < 8192 ? want : 8192;
     hipLaunchKernelGGL(grid_bw_kernel, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0,
                        stream, x, n, n_dev, x_min, x_range, *desc, dL_dout, grad_table);
     return mfn_check_launch("grid_encode_bw");

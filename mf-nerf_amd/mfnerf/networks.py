@@ -49,6 +49,8 @@ class NGP(nn.Module):
         N_tables = getattr(hparams, "N_tables", 1)
         b = np.exp(np.log(hparams.N_max * scale / N_min) / (L - 1))
         self.rgb_width = hparams.rgb_channels
+        if L * F != 32:
+            raise NotImplementedError("the fused field head takes L*F = 32 grid features (the reference's L=16, F=2)")
         if hparams.rgb_layers != 2:
             raise NotImplementedError("the fused field head implements rgb_layers=2 (the reference default)")
         self.xyz_encoder = tcnn.NetworkWithInputEncoding(

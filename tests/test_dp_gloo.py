@@ -1,0 +1,57 @@
+"""world_size=2 data-parallel step semantics on CPU over gloo: rank-distinct batches, one mean
+all-reduce of the flat gradient, identical Adam updates -> bitwise-identical replicas."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG, ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def adam_ref(p, g, m, v, t, lr=1e-2, b1=0.9, b2=0.999, eps=1e-15):
+    """The update of mfnerf_adam_step (apex FusedAdam, decay 0)."""
+    m.mul_(b1).add_((1 - b1) * g)
+    v.mul_(b2).add_((1 - b2) * g * g)
+    p.sub_(lr * ((m / (1 - b1 ** t)) / (torch.sqrt(v / (1 - b2 ** t)) + eps)))
+
+
+def _worker(rank, world, port, out):
+    import sys
+    sys.path[:0] = [ROOT, PKG]
+    from mfnerf import dp
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)  # identical init on every rank
+    p = torch.randn(1000)
+    m, v = torch.zeros(1000), torch.zeros(1000)
+    for t in range(1, 4):
+        g = torch.Generator().manual_seed(dp.rank_seed(t, rank))  # rank-distinct "batch"
+        grad = torch.randn(1000, generator=g)
+        local = grad.clone()
+        dp.allreduce_mean_(grad)
+        gathered = [torch.zeros(1000) for _ in range(world)]
+        dist.all_gather(gathered, local)
+        assert torch.allclose(grad, torch.stack(gathered).mean(0), atol=1e-6)
+        assert not torch.equal(gathered[0], gathered[1])
+        adam_ref(p, grad, m, v, t)
+    out[rank] = p
+    assert dp.max_over_ranks(float(rank)) == world - 1
+    dist.destroy_process_group()
+
+
+def test_two_rank_step_keeps_replicas_identical():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    assert torch.equal(out[0], out[1])
