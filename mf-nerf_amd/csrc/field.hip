@@ -489,15 +489,22 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
     for (int i = threadIdx.x; i < N_DW; i += blockDim.x) row[i] = img[i] * invS;
 }
 
-// grad[p] += sum over slab rows (fixed order: deterministic)
-__global__ void slab_reduce_kernel(const float* __restrict__ slab, int rows, float* __restrict__ gx,
-                                   float* __restrict__ gr) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= N_DW) return;
+// grad[p] += sum over slab rows (fixed order: deterministic).  64 columns x 4 row groups per block.
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int rows,
+                                                          float* __restrict__ gx, float* __restrict__ gr) {
+    __shared__ float part[4][64];
+    const int l = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    const int p = blockIdx.x * 64 + l;
     float acc = 0.0f;
-    for (int b = 0; b < rows; ++b) acc += slab[(int64_t)b * N_DW + p];
-    if (p < N_XYZ_PARAMS) gx[p] += acc;
-    else gr[p - N_XYZ_PARAMS] += acc;
+    if (p < N_DW)
+        for (int b = rg; b < rows; b += 4) acc += slab[(int64_t)b * N_DW + p];
+    part[rg][l] = acc;
+    __syncthreads();
+    if (rg == 0 && p < N_DW) {
+        const float v = (part[0][l] + part[1][l]) + (part[2][l] + part[3][l]);
+        if (p < N_XYZ_PARAMS) gx[p] += v;
+        else gr[p - N_XYZ_PARAMS] += v;
+    }
 }
 
 constexpr int BW_BLOCKS = 256;
@@ -573,7 +580,7 @@ int mfnerf_field_bw(const void* feat_f16, const float* dirs, int64_t n, const in
     hipLaunchKernelGGL(field_bw_kernel, dim3(BW_BLOCKS), dim3(FIELD_BLOCK), BW_LDS, stream, (const _Float16*)feat_f16,
                        dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb, grad_scale, dL_dfeat,
                        (float*)workspace);
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3((N_DW + 255) / 256), dim3(256), 0, stream, (const float*)workspace,
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((N_DW + 63) / 64), dim3(256), 0, stream, (const float*)workspace,
                        BW_BLOCKS, grad_xyz, grad_rgb);
     return mfn_check_launch("field_bw");
 }

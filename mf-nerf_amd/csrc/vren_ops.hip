@@ -191,6 +191,101 @@ __global__ void march_write_kernel(MarchParams p, int64_t n_rays, const int64_t*
     march_ray<true>(p, r, limit, rays_a[3 * r + 1], xyzs, dirs, deltas, ts);
 }
 
+// ---- wave-per-ray marching for constant dt (exp_step_factor == 0: every synthetic scene).
+// One wave marches one ray 64 chain points at a time.  The chain t_{k+1} = fl(t_k + dt) that both
+// reference branches walk (raymarching.cu:223,230-232) is laid on the lanes in closed form,
+// t_j = fmaf(j, delta, t_base) with delta = fl(t_base+dt) - t_base, and every lane checks
+// fl(t_j + dt) == t_{j+1}: the chunk is truncated at the first mismatch (binade crossing, tie), so
+// the lane values ARE the sequential chain.  Each live lane looks up its cell; a scalar walk over
+// the lanes then replays the reference's control flow exactly (occupied: emit and step; empty:
+// jump to the first chain point >= the DDA target), and the emitted lanes are compacted with a
+// ballot prefix count.  Bit-identical to march_ray<> (and the oracle), ~64x more parallel.
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ int ffs64(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
+
+template <bool WRITE>
+__global__ __launch_bounds__(256) void march_wave_kernel(MarchParams p, int64_t n_rays, int32_t* __restrict__ counts,
+                                                         const int64_t* __restrict__ rays_a, float* __restrict__ xyzs,
+                                                         float* __restrict__ dirs, float* __restrict__ deltas,
+                                                         float* __restrict__ ts) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (r >= n_rays) return;  // wave-uniform
+    int limit = p.max_samples;
+    int64_t base = 0;
+    if (WRITE) {
+        limit = (int)rays_a[3 * r + 2];
+        base = rays_a[3 * r + 1];
+        if (limit == 0) return;
+    }
+    const float gsi = 1.0f / (float)p.grid_size;
+    const float ox = p.o[3 * r], oy = p.o[3 * r + 1], oz = p.o[3 * r + 2];
+    const float dx = p.d[3 * r], dy = p.d[3 * r + 1], dz = p.d[3 * r + 2];
+    const float dxi = 1.0f / dx, dyi = 1.0f / dy, dzi = 1.0f / dz;
+    float t1 = p.hits_t[r * p.hits_stride];
+    const float t2 = p.hits_t[r * p.hits_stride + 1];
+    int n = 0;
+    if (t1 >= 0) {
+        const float dt = calc_dt(t1, p.exp_step, p.max_samples, p.grid_size, p.scale);  // constant
+        t1 = fmaf(dt, p.noise[r], t1);
+        float t_base = t1, pending = 0.0f;
+        bool skip = false, done = false;
+        while (!done) {
+            if (!(t_base < t2) || n >= limit) break;  // every later visited point fails the loop test
+            const float delta = (t_base + dt) - t_base;
+            const float tl = fmaf((float)lane, delta, t_base);
+            const float succ = tl + dt;
+            const float tl_next = __shfl_down(tl, 1, 64);
+            const uint64_t bad = __ballot(lane < 63 && succ != tl_next);
+            const int chain_end = bad ? ffs64(bad) + 1 : 64;
+            const float next_base = readlane_f(succ, chain_end - 1);
+            const bool live = lane < chain_end && tl < t2;
+            bool occ = false;
+            float tt = 0.0f, x = 0.0f, y = 0.0f, z = 0.0f;
+            if (live) {
+                x = fmaf(tl, dx, ox); y = fmaf(tl, dy, oy); z = fmaf(tl, dz, oz);
+                const Cell c = lookup_cell(x, y, z, dt, p.cascades, p.grid_size, p.scale, p.bitfield);
+                occ = c.occ;
+                if (!occ) tt = skip_target(tl, c, x, y, z, dx, dy, dz, dxi, dyi, dzi, gsi);
+            }
+            const uint64_t live_m = __ballot(live), occ_m = __ballot(occ);
+            const uint64_t chain_m = chain_end == 64 ? ~0ull : ((1ull << chain_end) - 1);
+            uint64_t emit_m = 0;
+            const int n0 = n;
+            int c = 0;
+            if (skip) {
+                const uint64_t ge = __ballot(tl >= pending) & chain_m;
+                if (ge) { c = ffs64(ge); skip = false; } else c = chain_end;
+            }
+            while (c < chain_end) {
+                if (!((live_m >> c) & 1) || n >= limit) { done = true; break; }
+                if ((occ_m >> c) & 1) {
+                    const uint64_t rest = ~(occ_m >> c);
+                    int len = rest ? ffs64(rest) : 64 - c;
+                    len = min(len, limit - n);
+                    emit_m |= (len >= 64 ? ~0ull : ((1ull << len) - 1)) << c;
+                    n += len; c += len;
+                } else {
+                    const float target = readlane_f(tt, c);
+                    const uint64_t ge = __ballot(tl >= target) & chain_m & ~((2ull << c) - 1);
+                    if (ge) c = ffs64(ge);
+                    else { skip = true; pending = target; c = chain_end; }
+                }
+            }
+            if (WRITE && ((emit_m >> lane) & 1)) {
+                const int64_t s = base + n0 + __popcll(emit_m & ((1ull << lane) - 1));
+                xyzs[3 * s] = x; xyzs[3 * s + 1] = y; xyzs[3 * s + 2] = z;
+                dirs[3 * s] = dx; dirs[3 * s + 1] = dy; dirs[3 * s + 2] = dz;
+                ts[s] = tl; deltas[s] = dt;
+            }
+            t_base = next_base;
+        }
+    }
+    if (!WRITE && lane == 0) counts[r] = n;
+}
+
 // raymarching_test_kernel (raymarching.cu:335-404) with the calc_dt(..., cascades) quirk.
 __global__ void march_test_kernel(MarchParams p, float* __restrict__ hits_t, const int64_t* __restrict__ alive,
                                   int64_t n_alive, int N_samples, float* __restrict__ xyzs, float* __restrict__ dirs,
@@ -233,80 +328,143 @@ __global__ void march_test_kernel(MarchParams p, float* __restrict__ hits_t, con
 }
 
 // ------------------------------------------------------------------ compositing (volumerendering.cu)
-__global__ void composite_fw_kernel(const float* __restrict__ sigmas, const float* __restrict__ rgbs,
-                                    const float* __restrict__ deltas, const float* __restrict__ ts,
-                                    const int64_t* __restrict__ rays_a, int64_t n_rays, float T_thr,
-                                    int64_t* __restrict__ total_samples, float* __restrict__ opacity,
-                                    float* __restrict__ depth, float* __restrict__ rgb, float* __restrict__ ws) {
-    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// ---- wave-per-ray compositing (volumerendering.cu:6-45 / :87-151).  One wave per ray, lanes =
+// samples (coalesced loads/stores, 64 samples per chunk).  The transmittance chain T *= 1-a is
+// evaluated in the reference's sequential order by a uniform loop over the lanes (bit-identical
+// T, hence identical termination and total_samples); the rgb/depth/opacity sums and the backward's
+// prefix sums are wave reductions/scans (fp32 reassociation only, ~1e-7 relative).
+__device__ __forceinline__ float wave_sum(float v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_incl_scan(float v, int lane) {
+    for (int off = 1; off < 64; off <<= 1) {
+        const float u = __shfl_up(v, off, 64);
+        if (lane >= off) v += u;
+    }
+    return v;
+}
+
+// Sequential T over the chunk: returns this lane's T before its sample; T_run is advanced; *stop is
+// the first lane whose post-update T <= thr (64 if none).
+__device__ __forceinline__ float t_chain(float a, float& T_run, float thr, int lane, int n_valid, int* stop) {
+    float myT = T_run;
+    int st = 64;
+    for (int j = 0; j < n_valid; ++j) {
+        const float aj = readlane_f(a, j);
+        if (lane == j) myT = T_run;
+        T_run *= 1.0f - aj;
+        if (T_run <= thr) { st = j; break; }
+    }
+    *stop = st;
+    return myT;
+}
+
+__global__ __launch_bounds__(256) void composite_fw_wave_kernel(
+    const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
+    const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t n_rays, float T_thr,
+    int64_t* __restrict__ total_samples, float* __restrict__ opacity, float* __restrict__ depth,
+    float* __restrict__ rgb, float* __restrict__ ws) {
+    const int lane = threadIdx.x & 63;
+    const int64_t n = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (n >= n_rays) return;
     const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
     const int N = (int)rays_a[3 * n + 2];
     float T = 1.0f, R = 0.f, G = 0.f, B = 0.f, D = 0.f, O = 0.f;
-    int samples = 0;
-    while (samples < N) {
-        const int64_t s = start + samples;
-        const float a = 1.0f - fast_exp(-sigmas[s] * deltas[s]);
-        const float w = a * T;
-        R = fmaf(w, rgbs[3 * s], R); G = fmaf(w, rgbs[3 * s + 1], G); B = fmaf(w, rgbs[3 * s + 2], B);
-        D = fmaf(w, ts[s], D);
-        O += w;
-        ws[s] = w;
-        T *= 1.0f - a;
-        if (T <= T_thr) break;
-        samples++;
+    int total = N;
+    bool ended = false;
+    for (int k0 = 0; k0 < N; k0 += 64) {
+        const int nv = min(64, N - k0);
+        const int64_t s = start + k0 + lane;
+        const bool valid = lane < nv;
+        float w = 0.0f;
+        if (!ended) {
+            const float a = valid ? 1.0f - fast_exp(-sigmas[s] * deltas[s]) : 0.0f;
+            int stop;
+            const float myT = t_chain(a, T, T_thr, lane, nv, &stop);
+            if (valid && lane <= stop) {
+                w = a * myT;
+                R = fmaf(w, rgbs[3 * s], R); G = fmaf(w, rgbs[3 * s + 1], G); B = fmaf(w, rgbs[3 * s + 2], B);
+                D = fmaf(w, ts[s], D);
+                O += w;
+            }
+            if (stop < 64) { ended = true; total = k0 + stop; }
+        }
+        if (valid) ws[s] = w;
     }
-    for (int k = samples + 1; k < N; ++k) ws[start + k] = 0.0f;
-    opacity[ray] = O; depth[ray] = D;
-    rgb[3 * ray] = R; rgb[3 * ray + 1] = G; rgb[3 * ray + 2] = B;
-    total_samples[ray] = samples;
+    R = wave_sum(R); G = wave_sum(G); B = wave_sum(B); D = wave_sum(D); O = wave_sum(O);
+    if (lane == 0) {
+        opacity[ray] = O; depth[ray] = D;
+        rgb[3 * ray] = R; rgb[3 * ray + 1] = G; rgb[3 * ray + 2] = B;
+        total_samples[ray] = total;
+    }
 }
 
-__global__ void composite_bw_kernel(const float* __restrict__ dL_dopacity, const float* __restrict__ dL_ddepth,
-                                    const float* __restrict__ dL_drgb, const float* __restrict__ dL_dws,
-                                    const float* __restrict__ sigmas, const float* __restrict__ rgbs,
-                                    const float* __restrict__ ws, const float* __restrict__ deltas,
-                                    const float* __restrict__ ts, const int64_t* __restrict__ rays_a,
-                                    const float* __restrict__ opacity, const float* __restrict__ depth,
-                                    const float* __restrict__ rgb, int64_t n_rays, float T_thr,
-                                    float* __restrict__ dL_dsigmas, float* __restrict__ dL_drgbs) {
-    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void composite_bw_wave_kernel(
+    const float* __restrict__ dL_dopacity, const float* __restrict__ dL_ddepth, const float* __restrict__ dL_drgb,
+    const float* __restrict__ dL_dws, const float* __restrict__ sigmas, const float* __restrict__ rgbs,
+    const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
+    const int64_t* __restrict__ rays_a, const float* __restrict__ opacity, const float* __restrict__ depth,
+    const float* __restrict__ rgb, int64_t n_rays, float T_thr, float* __restrict__ dL_dsigmas,
+    float* __restrict__ dL_drgbs) {
+    const int lane = threadIdx.x & 63;
+    const int64_t n = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (n >= n_rays) return;
     const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
     const int N = (int)rays_a[3 * n + 2];
     if (N <= 0) return;
-    // inclusive scan of dL_dws*ws (volumerendering.cu:119-123, host product :175): total first ...
+    // total of dL_dws*ws over the whole ray (the inclusive scan's last element)
     float wsum = 0.0f;
-    for (int k = 0; k < N; ++k) wsum += dL_dws[start + k] * ws[start + k];
-    const float R = rgb[3 * ray], G = rgb[3 * ray + 1], B = rgb[3 * ray + 2];
-    const float O = opacity[ray], Dp = depth[ray];
+    for (int k0 = 0; k0 < N; k0 += 64) {
+        const int64_t s = start + k0 + lane;
+        if (k0 + lane < N) wsum += dL_dws[s] * ws[s];
+    }
+    wsum = wave_sum(wsum);
+    const float Rt = rgb[3 * ray], Gt = rgb[3 * ray + 1], Bt = rgb[3 * ray + 2];
+    const float O = opacity[ray], Dt = depth[ray];
     const float gr = dL_drgb[3 * ray], gg = dL_drgb[3 * ray + 1], gb = dL_drgb[3 * ray + 2];
     const float go = dL_dopacity[ray], gd = dL_ddepth[ray];
-    float T = 1.0f, r = 0.f, g = 0.f, b = 0.f, dd = 0.f, scan = 0.0f;
-    int samples = 0;
-    while (samples < N) {
-        const int64_t s = start + samples;
-        scan += dL_dws[s] * ws[s];  // ... then the running prefix, same sequential sums as thrust's scan
-        const float a = 1.0f - fast_exp(-sigmas[s] * deltas[s]);
-        const float w = a * T;
-        r = fmaf(w, rgbs[3 * s], r); g = fmaf(w, rgbs[3 * s + 1], g); b = fmaf(w, rgbs[3 * s + 2], b);
-        dd = fmaf(w, ts[s], dd);
-        T *= 1.0f - a;
-        dL_drgbs[3 * s] = gr * w; dL_drgbs[3 * s + 1] = gg * w; dL_drgbs[3 * s + 2] = gb * w;
-        float acc = gr * fmaf(rgbs[3 * s], T, -(R - r));
-        acc = fmaf(gg, fmaf(rgbs[3 * s + 1], T, -(G - g)), acc);
-        acc = fmaf(gb, fmaf(rgbs[3 * s + 2], T, -(B - b)), acc);
-        acc = fmaf(go, 1 - O, acc);
-        acc = fmaf(gd, fmaf(ts[s], T, -(Dp - dd)), acc);
-        acc = fmaf(T, dL_dws[s], acc);
-        acc = acc - (wsum - scan);
-        dL_dsigmas[s] = deltas[s] * acc;
-        if (T <= T_thr) break;
-        samples++;
-    }
-    for (int k = samples + 1; k < N; ++k) {
-        const int64_t s = start + k;
-        dL_dsigmas[s] = 0.f; dL_drgbs[3 * s] = 0.f; dL_drgbs[3 * s + 1] = 0.f; dL_drgbs[3 * s + 2] = 0.f;
+    float T = 1.0f, cr = 0.f, cg = 0.f, cb = 0.f, cd = 0.f, cs = 0.f;  // carries of the prefix sums
+    bool ended = false;
+    for (int k0 = 0; k0 < N; k0 += 64) {
+        const int nv = min(64, N - k0);
+        const int64_t s = start + k0 + lane;
+        const bool valid = lane < nv;
+        float dsig = 0.0f, d0 = 0.0f, d1 = 0.0f, d2 = 0.0f;
+        if (!ended) {
+            float sg = 0.f, dl = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f, tv = 0.f, dw = 0.f, wv = 0.f;
+            if (valid) {
+                sg = sigmas[s]; dl = deltas[s]; tv = ts[s]; dw = dL_dws[s]; wv = ws[s];
+                c0 = rgbs[3 * s]; c1 = rgbs[3 * s + 1]; c2 = rgbs[3 * s + 2];
+            }
+            const float a = valid ? 1.0f - fast_exp(-sg * dl) : 0.0f;
+            int stop;
+            const float myT = t_chain(a, T, T_thr, lane, nv, &stop);
+            const bool act = valid && lane <= stop;
+            const float w = act ? a * myT : 0.0f;
+            const float Tn = myT * (1.0f - a);  // T after this sample (the reference's updated T)
+            const float pr = wave_incl_scan(w * c0, lane) + cr, pg = wave_incl_scan(w * c1, lane) + cg;
+            const float pb = wave_incl_scan(w * c2, lane) + cb, pd = wave_incl_scan(w * tv, lane) + cd;
+            const float ps = wave_incl_scan(act ? dw * wv : 0.0f, lane) + cs;
+            cr = readlane_f(pr, 63); cg = readlane_f(pg, 63); cb = readlane_f(pb, 63); cd = readlane_f(pd, 63);
+            cs = readlane_f(ps, 63);
+            if (act) {
+                d0 = gr * w; d1 = gg * w; d2 = gb * w;
+                float acc = gr * fmaf(c0, Tn, -(Rt - pr));
+                acc = fmaf(gg, fmaf(c1, Tn, -(Gt - pg)), acc);
+                acc = fmaf(gb, fmaf(c2, Tn, -(Bt - pb)), acc);
+                acc = fmaf(go, 1 - O, acc);
+                acc = fmaf(gd, fmaf(tv, Tn, -(Dt - pd)), acc);
+                acc = fmaf(Tn, dw, acc);
+                acc = acc - (wsum - ps);
+                dsig = dl * acc;
+            }
+            if (stop < 64) ended = true;
+        }
+        if (valid) {
+            dL_dsigmas[s] = dsig;
+            dL_drgbs[3 * s] = d0; dL_drgbs[3 * s + 1] = d1; dL_drgbs[3 * s + 2] = d2;
+        }
     }
 }
 
@@ -476,11 +634,21 @@ int mfnerf_raymarching_train(const float* rays_o, const float* rays_d, const flo
                   grid_size, max_samples};
     int32_t* counts = (int32_t*)workspace;
     const unsigned nb = blocks_for(n_rays, RAY_BLOCK);
-    hipLaunchKernelGGL(march_count_kernel, dim3(nb), dim3(RAY_BLOCK), 0, stream, p, n_rays, counts);
+    const bool wave = exp_step_factor == 0.0f;  // constant dt: the wave-per-ray marcher applies
+    const unsigned nbw = (unsigned)div_up<int64_t>(n_rays, 4);
+    if (wave)
+        hipLaunchKernelGGL(march_wave_kernel<false>, dim3(nbw), dim3(256), 0, stream, p, n_rays, counts, nullptr,
+                           nullptr, nullptr, nullptr, nullptr);
+    else
+        hipLaunchKernelGGL(march_count_kernel, dim3(nb), dim3(RAY_BLOCK), 0, stream, p, n_rays, counts);
     hipLaunchKernelGGL(march_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, counts, n_rays, capacity, rays_a,
                        counter);
-    hipLaunchKernelGGL(march_write_kernel, dim3(nb), dim3(RAY_BLOCK), 0, stream, p, n_rays, rays_a, xyzs, dirs,
-                       deltas, ts);
+    if (wave)
+        hipLaunchKernelGGL(march_wave_kernel<true>, dim3(nbw), dim3(256), 0, stream, p, n_rays, nullptr, rays_a, xyzs,
+                           dirs, deltas, ts);
+    else
+        hipLaunchKernelGGL(march_write_kernel, dim3(nb), dim3(RAY_BLOCK), 0, stream, p, n_rays, rays_a, xyzs, dirs,
+                           deltas, ts);
     return mfn_check_launch("raymarching_train");
 }
 
@@ -515,8 +683,8 @@ int mfnerf_composite_train_fw(const float* sigmas, const float* rgbs, const floa
         (n_samples > 0 && (!sigmas || !rgbs || !deltas || !ts || !ws))) {
         mfn_set_error("composite_train_fw: null pointer"); return MFN_ERR_INVALID;
     }
-    hipLaunchKernelGGL(composite_fw_kernel, dim3(blocks_for(n_rays, RAY_BLOCK)), dim3(RAY_BLOCK), 0, stream, sigmas,
-                       rgbs, deltas, ts, rays_a, n_rays, T_threshold, total_samples, opacity, depth, rgb, ws);
+    hipLaunchKernelGGL(composite_fw_wave_kernel, dim3(blocks_for(n_rays, 4)), dim3(256), 0, stream, sigmas, rgbs, deltas,
+                       ts, rays_a, n_rays, T_threshold, total_samples, opacity, depth, rgb, ws);
     return mfn_check_launch("composite_train_fw");
 }
 
@@ -531,7 +699,7 @@ int mfnerf_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, 
         (n_samples > 0 && (!dL_dws || !sigmas || !rgbs || !ws || !deltas || !ts || !dL_dsigmas || !dL_drgbs))) {
         mfn_set_error("composite_train_bw: null pointer"); return MFN_ERR_INVALID;
     }
-    hipLaunchKernelGGL(composite_bw_kernel, dim3(blocks_for(n_rays, RAY_BLOCK)), dim3(RAY_BLOCK), 0, stream,
+    hipLaunchKernelGGL(composite_bw_wave_kernel, dim3(blocks_for(n_rays, 4)), dim3(256), 0, stream,
                        dL_dopacity, dL_ddepth, dL_drgb, dL_dws, sigmas, rgbs, ws, deltas, ts, rays_a, opacity,
                        depth, rgb, n_rays, T_threshold, dL_dsigmas, dL_drgbs);
     return mfn_check_launch("composite_train_bw");
