@@ -50,12 +50,8 @@ STAGES = ["prep", "march", "grid_fw", "field_fw", "composite_fw", "composite_bw"
 
 
 def run_step(step, batch, world, ev=None):
-    """One training step; if ev is given, records a CUDA event after every stage."""
+    """One training step (mfnerf.engine.TrainStep.run); with ev, records a CUDA event after every stage."""
     from mfnerf import dp
-    from mfnerf._lib import call, ptr, stream
-    st, c = step.state, step.cfg
-    N, cap = c.n_rays, step.cap
-    s = stream()
 
     def mark(name):
         if ev is not None:
@@ -64,45 +60,7 @@ def run_step(step, batch, world, ev=None):
             ev.append((name, e))
 
     mark("start")
-    call("mfnerf_ray_aabb_intersect", ptr(batch.rays_o), ptr(batch.rays_d), ptr(step.center), ptr(step.half_size),
-         N, 1, 1, ptr(st.hit_cnt), ptr(st.hits), ptr(st.hits_idx), s)
-    t1 = st.hits[:, 0, 0]
-    t1.masked_fill_((t1 >= 0) & (t1 < 0.01), 0.01)
-    torch.rand(N, generator=step.gen, device=step.dev, out=st.noise)
-    mark("prep")
-    call("mfnerf_raymarching_train", ptr(batch.rays_o), ptr(batch.rays_d), ptr(st.hits_t), 2, ptr(step.bitfield),
-         step.cascades, float(c.scale), 0.0, ptr(st.noise), step.G, c.max_samples, N, cap, ptr(st.rays_a),
-         ptr(st.xyzs), ptr(st.dirs), ptr(st.deltas), ptr(st.ts), ptr(st.counter), ptr(st.march_ws), s)
-    mark("march")
-    call("mfnerf_grid_encode_fw", ptr(st.xyzs), cap, ptr(st.counter), step.x_min, step.x_range, step.desc,
-         ptr(step.p16[step.off_table:]), ptr(st.feat), s)
-    mark("grid_fw")
-    call("mfnerf_field_fw", ptr(st.feat), ptr(st.dirs), cap, ptr(st.counter), ptr(step.packed), c.rgb_width, 0,
-         ptr(st.sigma), ptr(st.rgb_s), s)
-    mark("field_fw")
-    call("mfnerf_composite_train_fw", ptr(st.sigma), ptr(st.rgb_s), ptr(st.deltas), ptr(st.ts), ptr(st.rays_a), N,
-         cap, c.T_threshold, ptr(st.total), ptr(st.opacity), ptr(st.depth), ptr(st.rgb), ptr(st.ws), s)
-    st.loss_sum.zero_()
-    call("mfnerf_nerf_loss", ptr(st.rgb), ptr(st.opacity), ptr(batch.rgb), N, c.lambda_opacity, 1.0, 1.0, 1.0,
-         ptr(st.dL_drgb), ptr(st.dL_dop), ptr(st.loss_sum), s)
-    mark("composite_fw")
-    call("mfnerf_composite_train_bw", ptr(st.dL_dop), ptr(st.zeros_ray), ptr(st.dL_drgb), ptr(st.zeros_samp),
-         ptr(st.sigma), ptr(st.rgb_s), ptr(st.ws), ptr(st.deltas), ptr(st.ts), ptr(st.rays_a), ptr(st.opacity),
-         ptr(st.depth), ptr(st.rgb), N, cap, c.T_threshold, ptr(st.dsig), ptr(st.drgb_s), s)
-    mark("composite_bw")
-    step.grads.zero_()
-    call("mfnerf_field_bw", ptr(st.feat), ptr(st.dirs), cap, ptr(st.counter), ptr(step.packed), c.rgb_width,
-         ptr(st.dsig), ptr(st.drgb_s), step.grad_scale, ptr(st.dfeat), ptr(step.grads),
-         ptr(step.grads[step.off_rgb:]), ptr(st.field_ws), s)
-    mark("field_bw")
-    call("mfnerf_grid_encode_bw", ptr(st.xyzs), cap, ptr(st.counter), step.x_min, step.x_range, step.desc,
-         ptr(st.dfeat), ptr(step.grads[step.off_table:]), s)
-    mark("grid_bw")
-    if world > 1:
-        dp.allreduce_mean_(step.grads)  # the one exchange per step (mfnerf/dp.py)
-    mark("allreduce")
-    step.optimizer()
-    mark("adam")
+    step.run(batch, mark=mark, exchange=dp.allreduce_mean_ if world > 1 else None)
 
 
 # ---------------------------------------------------------------------------- CPU baseline

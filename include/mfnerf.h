@@ -154,10 +154,19 @@ int mfnerf_grid_encode_fw(const float* x, int64_t n, const int32_t* n_dev, float
                           mfnerf_stream_t stream);
 
 /* Scatter dL/dout (n, n_levels*F) f32 into grad_table (n_entries*F) f32 by float atomics
- * (accumulates; caller zeroes). */
+ * (accumulates; caller zeroes).  workspace (optional, mfnerf_grid_encode_bw_workspace() bytes,
+ * ZERO on the first call; the call leaves it zero again): private copies of the dense coarse
+ * levels' gradient, which spread their hot-line atomics and are folded into grad_table. */
+int64_t mfnerf_grid_encode_bw_workspace(const mfnerf_grid_desc* desc);
 int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
-                          const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
+                          const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table, void* workspace,
                           mfnerf_stream_t stream);
+
+/* Debug: grid_encode_bw with an ablated body (1 plain stores, 2 levels 0-5 only, 3 levels 10-15 only;
+ * 0 = the product kernel).  Used by tools/ to attribute the kernel's time; not a training path. */
+int mfnerf_debug_grid_bw_ablate(int mode, const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                                const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
+                                mfnerf_stream_t stream);
 
 /* ---------------------------------------------------------------- NGP field head (MFMA) */
 

@@ -108,58 +108,109 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_fw_kernel(const float* __restr
 }
 
 // Backward.  The table gradient is a scatter-add; on MI355X a float atomic executes at the memory
-// side and costs one 64-B request per distinct line of a wave-instruction (MI355X_MICROARCH.md,
-// "Global float atomics"), so the kernel is shaped to minimise requests, not bytes:
-//   * one wave = 16 consecutive samples of ONE level; lane = (sample s = lane>>2, x-corner bit
-//     xb, feature f): per (y,z) corner pair the 4 lanes of a sample add to table entries idx(x),
-//     idx(x+1) x features f0,f1 -- one 16-B span (one line) for dense levels and, for hashed
-//     levels, whenever x->x+1 leaves the low bits of the hash alone (7/8 of the time);
-//   * samples are consecutive along a ray, so at coarse levels many neighbours hit the same
-//     corner: a 4-step segmented suffix scan over each lane's stride-4 stream merges such runs
-//     and only run heads issue the atomic (level 0 of the Lego config merges ~37 samples).
+// side and costs one request per distinct 64-B line of a wave-instruction -- lanes of one line are
+// free, lanes on the SAME address are not coalesced (tools/atomic_probe2.hip) -- so the kernel is
+// shaped to minimise requests, not bytes:
+//   * one wave = 16 consecutive samples, walking all levels; lane = (xb, f, s) with the sample s
+//     fastest: per (y,z) corner pair the 4 lanes of a sample add to entries idx(x), idx(x+1) x
+//     features f0,f1 -- one 16-B span, i.e. one line for dense levels and, for hashed levels,
+//     whenever x->x+1 leaves the hash's low bits alone (7/8 of the time);
+//   * consecutive samples lie along a ray, so coarse levels repeat a corner for many samples: a
+//     4-step segmented suffix scan (DPP row shifts inside each 16-lane row = one (xb,f) stream)
+//     merges such runs and only run heads issue the atomic;
+//   * the dense coarse levels (a few hundred to a few thousand hot lines) add into GRAD_COPIES
+//     private copies, picked per wave, folded back by fold_copies_kernel.
+constexpr int GRAD_COPIES = 8;
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
+}
+#define DPP_ROW_SHL(d) (0x100 | (d))
+#define DPP_ROW_SHR(d) (0x110 | (d))
+
+template <int ABLATE>  // 0 = product; debug builds: 1 plain stores, 2 levels 0-5 only, 3 levels 10-15 only
 __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restrict__ X, int64_t n,
                                                              const int32_t* __restrict__ n_dev, float x_min,
                                                              float x_range, const mfnerf_grid_desc D,
-                                                             const float* __restrict__ dy, float* __restrict__ grad) {
+                                                             const float* __restrict__ dy, float* __restrict__ grad,
+                                                             float* __restrict__ priv, int64_t dense_entries) {
     const int L_ = D.n_levels;
-    const int lane = threadIdx.x & 63, s = lane >> 2, xb = (lane >> 1) & 1, f = lane & 1;
+    const int lane = threadIdx.x & 63, s = lane & 15, f = (lane >> 4) & 1, xb = lane >> 5;
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
-    const int64_t items = div_up<int64_t>(nn, 16) * L_;
+    const int64_t chunks = div_up<int64_t>(nn, 16);
     const int64_t wave0 = ((int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x) >> 6;
     const int64_t n_waves = ((int64_t)gridDim.x * ENC_BLOCK) >> 6;
-    for (int64_t item = wave0; item < items; item += n_waves) {
-        const int l = (int)(item % L_);
-        const int64_t i = (item / L_) * 16 + s;
+    for (int64_t chunk = wave0; chunk < chunks; chunk += n_waves) {
+        const int64_t i = chunk * 16 + s;
         const bool valid = i < nn;
-        float g = 0.0f, x = 0.0f, y = 0.0f, z = 0.0f;
+        float x = 0.0f, y = 0.0f, z = 0.0f;
         if (valid) {
-            g = dy[i * (2 * L_) + 2 * l + f];
             x = (X[3 * i] - x_min) / x_range;
             y = (X[3 * i + 1] - x_min) / x_range;
             z = (X[3 * i + 2] - x_min) / x_range;
         }
-        const LevelGeo Lg = level_geo(D.scale[l], x, y, z);
-        float* gt = grad + 2 * (int64_t)D.offset[l];
+        const float* dyi = dy + i * (2 * L_) + f;
+        for (int l = 0; l < L_; ++l) {
+            if (ABLATE == 2 && l > 5) continue;
+            if (ABLATE == 3 && l < 10) continue;
+            const float g = valid ? dyi[2 * l] : 0.0f;
+            const LevelGeo Lg = level_geo(D.scale[l], x, y, z);
+            const bool spread = priv && (int64_t)D.offset[l] + D.size[l] <= dense_entries;
+            float* gt = spread ? priv + 2 * ((chunk & (GRAD_COPIES - 1)) * dense_entries + (int64_t)D.offset[l])
+                               : grad + 2 * (int64_t)D.offset[l];
 #pragma unroll
-        for (int yz = 0; yz < 4; ++yz) {
-            const int c = xb | (yz << 1);
-            const uint32_t idx =
-                corner_index(D, l, Lg.g[0] + (c & 1), Lg.g[1] + ((c >> 1) & 1), Lg.g[2] + ((c >> 2) & 1));
-            const uint32_t key = valid ? idx : 0xFFFFFFFFu;
-            float v = corner_weight(Lg, c) * g;
-            const uint32_t kp = __shfl(key, lane - 4, 64), kn = __shfl(key, lane + 4, 64);
-            const bool head = (s == 0) || kp != key;
-            bool stop = (s == 15) || kn != key;  // this lane ends its run
-#pragma unroll
-            for (int d = 1; d < 16; d <<= 1) {  // segmented suffix sum (run head ends up with the total)
-                const float vp = __shfl(v, lane + 4 * d, 64);
-                const bool sp = __shfl((int)stop, lane + 4 * d, 64);
-                if (!stop) { v += vp; stop = sp; }
+            for (int yz = 0; yz < 4; ++yz) {
+                const int c = xb | (yz << 1);
+                const uint32_t idx =
+                    corner_index(D, l, Lg.g[0] + (c & 1), Lg.g[1] + ((c >> 1) & 1), Lg.g[2] + ((c >> 2) & 1));
+                const int key = valid ? (int)idx : -1;
+                float v = corner_weight(Lg, c) * g;
+                const int kn = dpp_i<DPP_ROW_SHL(1)>(key), kp = dpp_i<DPP_ROW_SHR(1)>(key);
+                const bool head = (s == 0) || kp != key;
+                int stop = (s == 15) || kn != key;  // this lane ends its run
+                // segmented suffix sum within the 16-lane row: run heads end up with the run total
+                { const float vp = dpp_f<DPP_ROW_SHL(1)>(v); const int sp = dpp_i<DPP_ROW_SHL(1)>(stop); if (!stop) { v += vp; stop = sp; } }
+                { const float vp = dpp_f<DPP_ROW_SHL(2)>(v); const int sp = dpp_i<DPP_ROW_SHL(2)>(stop); if (!stop) { v += vp; stop = sp; } }
+                { const float vp = dpp_f<DPP_ROW_SHL(4)>(v); const int sp = dpp_i<DPP_ROW_SHL(4)>(stop); if (!stop) { v += vp; stop = sp; } }
+                { const float vp = dpp_f<DPP_ROW_SHL(8)>(v); const int sp = dpp_i<DPP_ROW_SHL(8)>(stop); if (!stop) { v += vp; stop = sp; } }
+                if (head && valid && v != 0.0f) {
+                    if (ABLATE == 1) gt[2 * idx + f] = v;
+                    else __hip_atomic_fetch_add(gt + 2 * idx + f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
-            if (head && valid && v != 0.0f)
-                __hip_atomic_fetch_add(gt + 2 * idx + f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+}
+
+// grad[p] += sum_k priv[k][p]; priv[k][p] = 0 (ready for the next backward)
+__global__ __launch_bounds__(256) void fold_copies_kernel(float* __restrict__ priv, int64_t n, float* __restrict__ grad) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 4; i += stride) {
+        float4 acc = reinterpret_cast<float4*>(grad)[i];
+#pragma unroll
+        for (int k = 0; k < GRAD_COPIES; ++k) {
+            float4* q = reinterpret_cast<float4*>(priv + k * n) + i;
+            const float4 v = *q;
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+            *q = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        reinterpret_cast<float4*>(grad)[i] = acc;
+    }
+}
+
+int64_t dense_entries_of(const mfnerf_grid_desc* d) {
+    int64_t e = 0;  // dense own-table levels are laid out first (res grows with the level)
+    for (int l = 0; l < d->n_levels; ++l) {
+        const uint64_t r = d->res[l];
+        if (d->table_kind[l] != 0 || r * r * r > d->size[l] || (int64_t)d->offset[l] != e) break;
+        e += d->size[l];
+    }
+    return e;
 }
 
 int check_desc(const mfnerf_grid_desc* d, const char* what) {
@@ -195,19 +246,44 @@ int mfnerf_grid_encode_fw(const float* x, int64_t n, const int32_t* n_dev, float
     return mfn_check_launch("grid_encode_fw");
 }
 
+int64_t mfnerf_grid_encode_bw_workspace(const mfnerf_grid_desc* desc) {
+    if (check_desc(desc, "grid_encode_bw_workspace")) return -1;
+    return (int64_t)GRAD_COPIES * dense_entries_of(desc) * 2 * (int64_t)sizeof(float);
+}
+
 int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
-                          const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
+                          const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table, void* workspace,
                           mfnerf_stream_t stream) {
     int st = check_desc(desc, "grid_encode_bw");
     if (st) return st;
     if (n < 0) { mfn_set_error("grid_encode_bw: bad size"); return MFN_ERR_INVALID; }
     if (n == 0) return MFN_OK;
     if (!x || !dL_dout || !grad_table) { mfn_set_error("grid_encode_bw: null pointer"); return MFN_ERR_INVALID; }
-    const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16) * desc->n_levels, ENC_BLOCK / 64);
-    const int64_t blocks = want < 8192 ? want : 8192;
-    hipLaunchKernelGGL(grid_bw_kernel, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0,
-                       stream, x, n, n_dev, x_min, x_range, *desc, dL_dout, grad_table);
+    const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16), ENC_BLOCK / 64);
+    const int64_t blocks = want < 4096 ? want : 4096;
+    const int64_t dense = workspace ? dense_entries_of(desc) : 0;
+    hipLaunchKernelGGL(grid_bw_kernel<0>, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0,
+                       stream, x, n, n_dev, x_min, x_range, *desc, dL_dout, grad_table, (float*)workspace, dense);
+    if (dense > 0) {
+        const int64_t nf = 2 * dense;  // multiple of 16 (level sizes are multiples of 8)
+        const int64_t fb = div_up<int64_t>(nf / 4, 256);
+        hipLaunchKernelGGL(fold_copies_kernel, dim3((unsigned)(fb < 2048 ? fb : 2048)), dim3(256), 0, stream,
+                           (float*)workspace, nf, grad_table);
+    }
     return mfn_check_launch("grid_encode_bw");
+}
+
+// Debug (not part of the training path): the same launch with an ablated kernel body.
+int mfnerf_debug_grid_bw_ablate(int mode, const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                                const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
+                                mfnerf_stream_t stream) {
+    const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16), ENC_BLOCK / 64);
+    const int64_t blocks = want < 4096 ? want : 4096;
+    auto k = mode == 1 ? grid_bw_kernel<1> : mode == 2 ? grid_bw_kernel<2> : mode == 3 ? grid_bw_kernel<3>
+                                                                                           : grid_bw_kernel<0>;
+    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc,
+                       dL_dout, grad_table, nullptr, (int64_t)0);
+    return mfn_check_launch("grid_bw_ablate");
 }
 
 }  // extern "C"

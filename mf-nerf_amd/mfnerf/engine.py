@@ -9,7 +9,7 @@ grid-stride over it.  Parameters live in one flat fp32 vector
     params = [xyz MLP (3072) | rgb MLP (7168) | grid table (L*F*entries)]
 so Adam is one launch and the gradient zeroing one memset; an fp16 mirror of the whole vector is
 refreshed by the same Adam pass and is what the grid kernels gather from.
-Multi-GPU: the caller all-reduces `grads` between backward() and optimizer() (bench.py).
+Multi-GPU: run(exchange=dp.allreduce_mean_) all-reduces `grads` between the backward and Adam.
 """
 import math
 from dataclasses import dataclass
@@ -134,6 +134,7 @@ class TrainStep:
         st.dfeat = torch.empty(cap, c.L * c.F, **f32)
         st.field_ws = torch.empty(load().mfnerf_field_bw_workspace(cap, c.rgb_width) // 4, **f32)
         st.loss_sum = torch.zeros(1, **f32)
+        st.grid_ws = torch.zeros(max(16, load().mfnerf_grid_encode_bw_workspace(self.desc)) // 4, **f32)
         self.state = st
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(seed + 1)
@@ -163,41 +164,54 @@ class TrainStep:
              ptr(self.packed), stream())
 
     # ---------------------------------------------------------------- the step
-    def forward(self, batch: Batch):
+    def run(self, batch: Batch, mark=None, exchange=None):
+        """One training step.  mark(name) is called after each stage (bench timing); exchange(grads)
+        runs between backward and Adam (the data-parallel all-reduce)."""
         c, st, s = self.cfg, self.state, stream()
         N, cap = c.n_rays, self.cap
+        mark = mark or (lambda name: None)
+        # rendering.py:27-29 (AABB + near clamp), custom_functions.py:83 (noise)
         call("mfnerf_ray_aabb_intersect", ptr(batch.rays_o), ptr(batch.rays_d), ptr(self.center),
              ptr(self.half_size), N, 1, 1, ptr(st.hit_cnt), ptr(st.hits), ptr(st.hits_idx), s)
         t1 = st.hits[:, 0, 0]
-        t1.masked_fill_((t1 >= 0) & (t1 < NEAR_DISTANCE), NEAR_DISTANCE)  # rendering.py:29
-        torch.rand(N, generator=self.gen, device=self.dev, out=st.noise)  # custom_functions.py:83
+        t1.masked_fill_((t1 >= 0) & (t1 < NEAR_DISTANCE), NEAR_DISTANCE)
+        torch.rand(N, generator=self.gen, device=self.dev, out=st.noise)
+        mark("prep")
         call("mfnerf_raymarching_train", ptr(batch.rays_o), ptr(batch.rays_d), ptr(st.hits_t), 2, ptr(self.bitfield),
              self.cascades, float(c.scale), 0.0 if c.scale <= 0.5 else 1 / 256, ptr(st.noise), self.G,
              c.max_samples, N, cap, ptr(st.rays_a), ptr(st.xyzs), ptr(st.dirs), ptr(st.deltas), ptr(st.ts),
              ptr(st.counter), ptr(st.march_ws), s)
+        mark("march")
         call("mfnerf_grid_encode_fw", ptr(st.xyzs), cap, ptr(st.counter), self.x_min, self.x_range, self.desc,
              ptr(self.p16[self.off_table:]), ptr(st.feat), s)
+        mark("grid_fw")
         call("mfnerf_field_fw", ptr(st.feat), ptr(st.dirs), cap, ptr(st.counter), ptr(self.packed), c.rgb_width, 0,
              ptr(st.sigma), ptr(st.rgb_s), s)
+        mark("field_fw")
         call("mfnerf_composite_train_fw", ptr(st.sigma), ptr(st.rgb_s), ptr(st.deltas), ptr(st.ts), ptr(st.rays_a),
              N, cap, c.T_threshold, ptr(st.total), ptr(st.opacity), ptr(st.depth), ptr(st.rgb), ptr(st.ws), s)
         bg = 1.0 if c.scale <= 0.5 else 0.0
         st.loss_sum.zero_()
         call("mfnerf_nerf_loss", ptr(st.rgb), ptr(st.opacity), ptr(batch.rgb), N, c.lambda_opacity, bg, bg, bg,
              ptr(st.dL_drgb), ptr(st.dL_dop), ptr(st.loss_sum), s)
-
-    def backward(self):
-        c, st, s = self.cfg, self.state, stream()
-        N, cap = c.n_rays, self.cap
+        mark("composite_fw")
         call("mfnerf_composite_train_bw", ptr(st.dL_dop), ptr(st.zeros_ray), ptr(st.dL_drgb), ptr(st.zeros_samp),
              ptr(st.sigma), ptr(st.rgb_s), ptr(st.ws), ptr(st.deltas), ptr(st.ts), ptr(st.rays_a), ptr(st.opacity),
              ptr(st.depth), ptr(st.rgb), N, cap, c.T_threshold, ptr(st.dsig), ptr(st.drgb_s), s)
+        mark("composite_bw")
         self.grads.zero_()
         call("mfnerf_field_bw", ptr(st.feat), ptr(st.dirs), cap, ptr(st.counter), ptr(self.packed), c.rgb_width,
              ptr(st.dsig), ptr(st.drgb_s), self.grad_scale, ptr(st.dfeat), ptr(self.grads),
              ptr(self.grads[self.off_rgb:]), ptr(st.field_ws), s)
+        mark("field_bw")
         call("mfnerf_grid_encode_bw", ptr(st.xyzs), cap, ptr(st.counter), self.x_min, self.x_range, self.desc,
-             ptr(st.dfeat), ptr(self.grads[self.off_table:]), s)
+             ptr(st.dfeat), ptr(self.grads[self.off_table:]), ptr(st.grid_ws), s)
+        mark("grid_bw")
+        if exchange is not None:
+            exchange(self.grads)
+        mark("allreduce")
+        self.optimizer()
+        mark("adam")
 
     def optimizer(self, lr=None):
         c = self.cfg
@@ -207,9 +221,7 @@ class TrainStep:
         self._pack()
 
     def step(self, batch: Batch):
-        self.forward(batch)
-        self.backward()
-        self.optimizer()
+        self.run(batch)
 
     # ---------------------------------------------------------------- occupancy (networks.py:242-271)
     @torch.no_grad()

@@ -27,9 +27,15 @@ def grid_encode_fw(x, n, table16, layout, desc, x_min=0.0, x_range=1.0, n_dev=No
     return out
 
 
-def grid_encode_bw(x, n, dL_dfeat, grad_table, layout, desc, x_min=0.0, x_range=1.0, n_dev=None):
+def grid_bw_workspace(desc, device):
+    """Zeroed private-copy workspace for grid_encode_bw (stays zero between calls)."""
+    nb = load().mfnerf_grid_encode_bw_workspace(desc)
+    return torch.zeros(max(nb, 16) // 4, dtype=torch.float32, device=device)
+
+
+def grid_encode_bw(x, n, dL_dfeat, grad_table, layout, desc, x_min=0.0, x_range=1.0, n_dev=None, workspace=None):
     call("mfnerf_grid_encode_bw", ptr(x), int(n), ptr(n_dev), float(x_min), float(x_range), desc, ptr(dL_dfeat),
-         ptr(grad_table), stream())
+         ptr(grad_table), ptr(workspace), stream())
 
 
 def pack_field_weights(params_xyz_net, params_rgb, rgb_width=64, out=None):
@@ -71,6 +77,17 @@ def pow2_grad_scale(max_abs):
     return float(2.0 ** max(0, min(24, math.floor(-math.log2(max_abs)))))
 
 
+_ws_cache = {}
+
+
+def _grid_ws(desc, device):
+    """Per-(device, layout) private-copy workspace; every backward leaves it zero again."""
+    key = (str(device), bytes(desc))
+    if key not in _ws_cache:
+        _ws_cache[key] = grid_bw_workspace(desc, device)
+    return _ws_cache[key]
+
+
 class GridEncodeFunction(torch.autograd.Function):
     """tcnn.Encoding(HashGrid/MixedFeatureGrid) forward/backward: x (N,3) in [0,1] -> (N, L*F) f16."""
 
@@ -86,7 +103,8 @@ class GridEncodeFunction(torch.autograd.Function):
     def backward(ctx, dL_dfeat):
         (x,) = ctx.saved_tensors
         g = torch.zeros(ctx.n_table, dtype=torch.float32, device=x.device)
-        grid_encode_bw(x, x.shape[0], dL_dfeat.float().contiguous(), g, ctx.layout, ctx.desc)
+        grid_encode_bw(x, x.shape[0], dL_dfeat.float().contiguous(), g, ctx.layout, ctx.desc,
+                       workspace=_grid_ws(ctx.desc, x.device))
         return None, g, None, None
 
 
@@ -128,7 +146,8 @@ class NGPFieldFunction(torch.autograd.Function):
         dfeat = torch.empty(n, layout.L * layout.F, dtype=torch.float32, device=dev)
         ws = field_bw_workspace(n, rgb_width, dev)
         field_bw(feat, dirs, n, packed, dsig, drgb, S, dfeat, g_xyz[:XYZ_NET_PARAMS], g_rgb, ws, rgb_width)
-        grid_encode_bw(xyzs, n, dfeat, g_xyz[XYZ_NET_PARAMS:], layout, desc, x_min, x_range)
+        grid_encode_bw(xyzs, n, dfeat, g_xyz[XYZ_NET_PARAMS:], layout, desc, x_min, x_range,
+                       workspace=_grid_ws(desc, dev))
         return None, None, g_xyz, g_rgb, None, None, None, None, None
 
 
