@@ -3,8 +3,10 @@
 One step = one NeRF training iteration on a synthetic Lego-like batch (BASELINE config 2:
 8192 rays/batch per GPU, Hash grid L=16 F=2 T=2^19, rgb 64x2): AABB -> ray march -> grid encode
 -> MFMA field head -> composite -> loss -> composite bw -> field bw -> grid bw -> [all-reduce] ->
-Adam.  The occupancy-grid refresh (every 16 steps in the reference) is excluded from the timed
-step as SURVEY.md 8d prescribes and reported separately (density_update_ms).
+Adam.  The timed steps replay the step as three HIP graphs (mfnerf.engine.TrainStep.capture);
+a preceding eager pass gives the per-kernel breakdown (eager_stage_ms).  The occupancy-grid
+refresh (every 16 steps in the reference) is excluded from the timed step as SURVEY.md 8d
+prescribes and reported separately (density_update_ms, value_with_occupancy_refresh).
 
 python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run (one rank per
 GPU, rank-distinct rays, one flat fp32 gradient all-reduce per step over RCCL).
@@ -42,25 +44,38 @@ def parse():
     ap.add_argument("--log2-T", type=int, default=19)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="time eager launches instead of the HIP graphs")
     return ap.parse_args()
 
 
-STAGES = ["prep", "march", "grid_fw", "field_fw", "composite_fw", "composite_bw", "field_bw", "grid_bw", "allreduce",
-          "adam"]
-
-
-def run_step(step, batch, world, ev=None):
-    """One training step (mfnerf.engine.TrainStep.run); with ev, records a CUDA event after every stage."""
-    from mfnerf import dp
-
+def _marker(ev):
     def mark(name):
         if ev is not None:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
             ev.append((name, e))
+    return mark
 
+
+def run_step(step, batch, world, ev=None, graph=False):
+    """One training step: eager (mfnerf.engine.TrainStep.run, an event after every stage) or from
+    the captured HIP graphs (TrainStep.replay: events around the fwd/bwd, grid_bw and Adam graphs)."""
+    from mfnerf import dp
+    mark = _marker(ev)
     mark("start")
-    step.run(batch, mark=mark, exchange=dp.allreduce_mean_ if world > 1 else None)
+    ex = dp.allreduce_mean_ if world > 1 else None
+    if graph:
+        step.replay(batch, mark=mark, exchange=ex)
+    else:
+        step.run(batch, mark=mark, exchange=ex)
+
+
+def stage_times(events, steps):
+    out = {}
+    for ev in events:
+        for (a, ea), (b, eb) in zip(ev[:-1], ev[1:]):
+            out[b] = out.get(b, 0.0) + ea.elapsed_time(eb)
+    return {k: v / steps for k, v in out.items()}
 
 
 # ---------------------------------------------------------------------------- CPU baseline
@@ -142,14 +157,31 @@ def main():
     for i in range(args.warmup):
         run_step(step, batches[i % len(batches)], world)
     # occupancy refresh cost (amortised every 16 steps in the reference), measured separately
+    step.update_density_grid(warmup=False)  # first call allocates the refresh scratch
     torch.cuda.synchronize()
     td = time.time()
-    for _ in range(3):
+    for _ in range(10):
         step.update_density_grid(warmup=False)
     torch.cuda.synchronize()
-    density_ms = (time.time() - td) / 3 * 1e3
+    density_ms = (time.time() - td) / 10 * 1e3
     step.set_occupancy(synthetic.ball_density_grid())  # keep the calibrated workload for the timed steps
 
+    # per-stage breakdown from an eager pass (an event after every kernel stage)
+    n_eager = min(args.steps, 50)
+    eager_ev = []
+    for i in range(n_eager):
+        ev = []
+        run_step(step, batches[i % len(batches)], world, ev)
+        eager_ev.append(ev)
+    torch.cuda.synchronize()
+    eager_stage_ms = stage_times(eager_ev, n_eager)
+
+    # the timed region: the step replayed from HIP graphs (launch overhead off the host)
+    use_graph = not args.eager
+    if use_graph:
+        step.capture()
+        for i in range(5):
+            run_step(step, batches[i % len(batches)], world, graph=True)
     events = []
     n_samples = torch.zeros((), dtype=torch.float64, device=dev)
     if world > 1:
@@ -158,7 +190,7 @@ def main():
     t0 = time.time()
     for i in range(args.steps):
         ev = []
-        run_step(step, batches[i % len(batches)], world, ev)
+        run_step(step, batches[i % len(batches)], world, ev, graph=use_graph)
         n_samples += step.state.counter[0]
         events.append(ev)
     torch.cuda.synchronize()
@@ -166,17 +198,13 @@ def main():
         torch.distributed.barrier()
     elapsed = time.time() - t0
     elapsed = dp.max_over_ranks(elapsed, dev)  # the slowest rank's clock
-
-    stage_ms = {k: 0.0 for k in STAGES}
-    for ev in events:
-        for (a, ea), (b, eb) in zip(ev[:-1], ev[1:]):
-            stage_ms[b] += ea.elapsed_time(eb)
-    stage_ms = {k: v / args.steps for k, v in stage_ms.items()}
+    stage_ms = stage_times(events, args.steps)
     mean_samples = float(n_samples) / args.steps
     rays_total = args.n_rays * args.steps * world
     value = rays_total / elapsed
 
-    dom = max(BYTES_PER_SAMPLE, key=lambda k: stage_ms[k])
+    # roofline: grid_bw (the dominant kernel), timed by events around its graph inside the timed region
+    dom = "grid_bw"
     dom_bytes = BYTES_PER_SAMPLE[dom] * mean_samples
     achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9
     if rank == 0:
@@ -195,8 +223,12 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                          "bytes_per_launch": round(dom_bytes)},
-            "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+            "graph": use_graph,
+            "segment_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+            "eager_stage_ms": {k: round(v, 4) for k, v in eager_stage_ms.items()},
             "density_update_ms": round(density_ms, 3),
+            # the reference refreshes occupancy every 16 steps (train.py:62,165): rate with it amortised
+            "value_with_occupancy_refresh": round(rays_total / (elapsed + args.steps / 16 * density_ms * 1e-3), 1),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

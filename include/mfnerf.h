@@ -199,15 +199,43 @@ int mfnerf_field_bw(const void* feat_f16, const float* dirs, int64_t n, const in
  * through the lane maps the field kernels assume (pins them on the device). */
 int mfnerf_debug_mfma_probe(const void* A, const void* B, float* D, mfnerf_stream_t stream);
 
+/* ---------------------------------------------------------------- occupancy grid refresh */
+
+/* Device-only NGP.update_density_grid (networks.py:157-271, called every 16 steps by
+ * train.py:165-168).  Three calls per refresh:
+ *   1. mfnerf_occupancy_cells: the cells to probe, as jittered world points.  warmup != 0: every
+ *      cell of every cascade (get_all_cells, networks.py:157-166); else per cascade n_uniform
+ *      uniform cells + n_uniform cells drawn uniformly among {density_grid > density_threshold}
+ *      (sample_uniform_and_occupied_cells, networks.py:168-192; the occupied list is in
+ *      ascending morton order like torch.nonzero, and an empty set yields cell_idx -1).
+ *      Outputs xyzs (n,3) f32 and cell_idx (n) i32 = cascade*G^3 + morton, with
+ *      n = mfnerf_occupancy_points(...).  Random draws: counter-based hash of (seed, call_index).
+ *   2. the caller evaluates sigma at xyzs (mfnerf_grid_encode_fw + mfnerf_field_fw density_only).
+ *   3. mfnerf_occupancy_update: tmp = 0; tmp[cell_idx] = sigmas; density_grid = where(grid < 0,
+ *      grid, max(grid*decay, tmp)) (decay = clamp(decay^(1/count_grid), 0.1, 0.95) when count_grid
+ *      is given: erode); thr = min(mean(grid[grid > 0]), density_threshold) (NaN when no cell is
+ *      positive, as Python's min(nan, x)); packbits(grid, thr) into bitfield.
+ * tmp: cascades*G^3 f32 scratch.  workspace: mfnerf_occupancy_workspace() bytes, shared by 1 and 3. */
+int64_t mfnerf_occupancy_workspace(int cascades, int grid_size);
+int64_t mfnerf_occupancy_points(int cascades, int grid_size, int64_t n_uniform, int warmup);
+int mfnerf_occupancy_cells(const float* density_grid, int cascades, int grid_size, float scale, int64_t n_uniform,
+                           int warmup, float density_threshold, uint64_t seed, uint64_t call_index, float* xyzs,
+                           int32_t* cell_idx, void* workspace, mfnerf_stream_t stream);
+int mfnerf_occupancy_update(float* density_grid, const float* sigmas, const int32_t* cell_idx, int64_t n_points,
+                            int cascades, int grid_size, float decay, const float* count_grid, float density_threshold,
+                            float* tmp, uint8_t* bitfield, void* workspace, mfnerf_stream_t stream);
+
 /* ---------------------------------------------------------------- optimizer */
 
 /* Adam (apex FusedAdam semantics, adam_w_mode=False, no weight decay; train.py:136):
  * m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= lr * (m/(1-b1^t)) / (sqrt(v/(1-b2^t)) + eps).
  * g is read as grad*grad_scale.  Optionally mirrors p into p_f16 (the fp16 compute copy).
- * step_dev (optional device i32): step counter incremented by the kernel (graph-replay safe). */
+ * step_dev (optional device i32): step counter incremented by the kernel (graph-replay safe).
+ * lr_dev (optional device f32): learning rate read on the device (a schedule that does not
+ * re-capture the graph); lr is used when it is NULL. */
 int mfnerf_adam_step(float* params, const float* grads, float* m, float* v, void* p_f16, int64_t n, float lr,
                      float beta1, float beta2, float eps, float grad_scale, int step, const int32_t* step_dev,
-                     mfnerf_stream_t stream);
+                     const float* lr_dev, mfnerf_stream_t stream);
 
 #ifdef __cplusplus
 }

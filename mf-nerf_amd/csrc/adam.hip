@@ -9,8 +9,10 @@ namespace {
 
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, __half* __restrict__ p16, int64_t n, float lr, float b1, float b2,
-                            float eps, float gscale, int step, const int32_t* __restrict__ step_dev) {
+                            float eps, float gscale, int step, const int32_t* __restrict__ step_dev,
+                            const float* __restrict__ lr_dev) {
     const int st = step_dev ? *step_dev : step;
+    if (lr_dev) lr = *lr_dev;
     // apex multi_tensor_adam (ADAM_MODE, decay 0): m/(1-b1^t), v/(1-b2^t), p -= lr*m_hat/(sqrt(v_hat)+eps)
     const float bc1 = 1.0f - powf(b1, (float)st);
     const float bc2 = 1.0f - powf(b2, (float)st);
@@ -56,7 +58,7 @@ __global__ void bump_step_kernel(int32_t* s) { *s += 1; }
 
 extern "C" int mfnerf_adam_step(float* params, const float* grads, float* m, float* v, void* p_f16, int64_t n,
                                 float lr, float beta1, float beta2, float eps, float grad_scale, int step,
-                                const int32_t* step_dev, mfnerf_stream_t stream) {
+                                const int32_t* step_dev, const float* lr_dev, mfnerf_stream_t stream) {
     if (n < 0) { mfn_set_error("adam_step: bad size"); return MFN_ERR_INVALID; }
     if (n == 0) return MFN_OK;
     if (!params || !grads || !m || !v) { mfn_set_error("adam_step: null pointer"); return MFN_ERR_INVALID; }
@@ -70,6 +72,6 @@ extern "C" int mfnerf_adam_step(float* params, const float* grads, float* m, flo
     const unsigned blocks = (unsigned)(want < 4096 ? (want < 1 ? 1 : want) : 4096);
     if (step_dev) hipLaunchKernelGGL(bump_step_kernel, dim3(1), dim3(1), 0, stream, (int32_t*)step_dev);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(threads), 0, stream, params, grads, m, v, (__half*)p_f16, n, lr,
-                       beta1, beta2, eps, grad_scale, step, step_dev);
+                       beta1, beta2, eps, grad_scale, step, step_dev, lr_dev);
     return mfn_check_launch("adam_step");
 }

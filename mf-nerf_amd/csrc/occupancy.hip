@@ -1,0 +1,305 @@
+// occupancy.hip -- the occupancy-grid refresh of models/networks.py:157-271 (train.py:165-168,
+// every 16 steps) as device-only kernels: no torch.nonzero / .item() host synchronisation.
+//
+//   mfnerf_occupancy_cells   : cells to probe -> jittered world points + flat cell index
+//       warm-up: every cell of every cascade (get_all_cells, networks.py:157-166);
+//       otherwise per cascade M uniform cells + M cells drawn uniformly from the cells whose
+//       density > threshold (sample_uniform_and_occupied_cells, networks.py:168-192).  The
+//       occupied list is built by an order-preserving compaction (ascending morton index,
+//       exactly torch.nonzero's order), so index r of the list is the reference's indices2[r].
+//   (caller runs mfnerf_grid_encode_fw + mfnerf_field_fw(density_only) on the points)
+//   mfnerf_occupancy_update  : tmp[cell] = sigma; grid = where(grid<0, grid, max(grid*decay, tmp));
+//       thr = min(mean(grid[grid>0]), threshold); packbits(grid, thr)  (networks.py:242-271).
+//
+// Randomness: torch.randint / torch.rand are replaced by a counter-based hash (seed, call, point,
+// coordinate) -- the same distributions, not torch's streams.
+#include "common.hpp"
+#include "../../include/mfnerf.h"
+
+using namespace mfn;
+
+namespace {
+
+constexpr int OCC_BLOCK = 256;
+constexpr int OCC_PER_THREAD = 16;
+constexpr int OCC_CELLS_PER_BLOCK = OCC_BLOCK * OCC_PER_THREAD;  // 4096
+
+__device__ __forceinline__ uint32_t mix64to32(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return (uint32_t)x;
+}
+__device__ __forceinline__ uint32_t rnd32(uint64_t key, uint64_t ctr) {
+    return mix64to32(key + ctr * 0x9E3779B97F4A7C15ull);
+}
+__device__ __forceinline__ uint32_t rnd_below(uint64_t key, uint64_t ctr, uint32_t n) {
+    return (uint32_t)(((uint64_t)rnd32(key, ctr) * n) >> 32);
+}
+__device__ __forceinline__ float rnd_unit(uint64_t key, uint64_t ctr) {  // [0,1), 24 bits like torch.rand
+    return (float)(rnd32(key, ctr) >> 8) * (1.0f / 16777216.0f);
+}
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* lds) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) lds[w] = v;
+    __syncthreads();
+    T s = 0;
+    for (int i = 0; i < OCC_BLOCK / 64; ++i) s += lds[i];
+    return s;
+}
+
+// per block: number of cells with density > thr
+__global__ __launch_bounds__(OCC_BLOCK) void occ_count_kernel(const float* __restrict__ grid, int64_t cells,
+                                                              float thr, int32_t* __restrict__ block_counts) {
+    __shared__ int lds[OCC_BLOCK / 64];
+    const int c = blockIdx.y, nblk = gridDim.x;
+    const int64_t base = (int64_t)c * cells + (int64_t)blockIdx.x * OCC_CELLS_PER_BLOCK + threadIdx.x * OCC_PER_THREAD;
+    const int64_t end = (int64_t)c * cells + cells;
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < OCC_PER_THREAD; ++i) k += (base + i < end && grid[base + i] > thr) ? 1 : 0;
+    k = block_sum(k, lds);
+    if (threadIdx.x == 0) block_counts[c * nblk + blockIdx.x] = k;
+}
+
+// order-preserving compaction of the occupied cells of each cascade
+__global__ __launch_bounds__(OCC_BLOCK) void occ_compact_kernel(const float* __restrict__ grid, int64_t cells,
+                                                                float thr, const int32_t* __restrict__ block_counts,
+                                                                int32_t* __restrict__ list, int32_t* __restrict__ counts) {
+    __shared__ int lds[OCC_BLOCK / 64];
+    __shared__ int wave_tot[OCC_BLOCK / 64];
+    const int c = blockIdx.y, nblk = gridDim.x, b = blockIdx.x;
+    int pre = 0;
+    for (int i = threadIdx.x; i < b; i += OCC_BLOCK) pre += block_counts[c * nblk + i];
+    pre = block_sum(pre, lds);
+    const int64_t j0 = (int64_t)b * OCC_CELLS_PER_BLOCK + threadIdx.x * OCC_PER_THREAD;
+    const float* g = grid + (int64_t)c * cells;
+    uint32_t mask = 0;
+#pragma unroll
+    for (int i = 0; i < OCC_PER_THREAD; ++i) mask |= (j0 + i < cells && g[j0 + i] > thr) ? (1u << i) : 0u;
+    const int mine = __popc(mask);
+    // exclusive scan of `mine` over the block (thread order == cell order)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int incl = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) wave_tot[w] = incl;
+    __syncthreads();
+    int wpre = 0;
+    for (int i = 0; i < w; ++i) wpre += wave_tot[i];
+    int pos = pre + wpre + incl - mine;
+    int32_t* out = list + (int64_t)c * cells;
+    while (mask) {
+        const int i = __ffs(mask) - 1;
+        mask &= mask - 1;
+        out[pos++] = (int32_t)(j0 + i);
+    }
+    if (b == nblk - 1 && threadIdx.x == OCC_BLOCK - 1) counts[c] = pos;
+}
+
+struct PointsArgs {
+    int cascades, G;
+    int64_t cells, per_cascade, n_uniform;
+    int warmup;
+    float scale;
+    uint64_t key;
+};
+
+// networks.py:253-258: s = min(2^(c-1), scale); x = (coords/(G-1)*2-1)*(s - s/G) + (2u-1)*(s/G)
+__global__ __launch_bounds__(OCC_BLOCK) void occ_points_kernel(PointsArgs a, const int32_t* __restrict__ list,
+                                                               const int32_t* __restrict__ counts,
+                                                               float* __restrict__ xyzs, int32_t* __restrict__ cell) {
+    const int64_t n = (int64_t)a.cascades * a.per_cascade;
+    for (int64_t p = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; p < n; p += (int64_t)gridDim.x * OCC_BLOCK) {
+        const int c = (int)(p / a.per_cascade);
+        const int64_t j = p - (int64_t)c * a.per_cascade;
+        uint32_t m;
+        bool ok = true;
+        if (a.warmup) {
+            m = (uint32_t)j;
+        } else if (j < a.n_uniform) {
+            const uint32_t cx = rnd_below(a.key, 8 * (uint64_t)p + 0, a.G);
+            const uint32_t cy = rnd_below(a.key, 8 * (uint64_t)p + 1, a.G);
+            const uint32_t cz = rnd_below(a.key, 8 * (uint64_t)p + 2, a.G);
+            m = morton3(cx, cy, cz);
+        } else {
+            const int cnt = counts[c];
+            ok = cnt > 0;  // empty occupied set: the reference draws no such cells
+            m = ok ? (uint32_t)list[(int64_t)c * a.cells + rnd_below(a.key, 8 * (uint64_t)p + 3, (uint32_t)cnt)] : 0u;
+        }
+        const float s = fminf(ldexpf(1.0f, c - 1), a.scale);
+        const float hgs = s / (float)a.G;
+        const float span = s - hgs;
+        const float inv = (float)(a.G - 1);
+        const uint32_t q[3] = {morton3_invert(m), morton3_invert(m >> 1), morton3_invert(m >> 2)};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float base = ((float)q[k] / inv * 2.0f - 1.0f) * span;
+            const float u = rnd_unit(a.key, 8 * (uint64_t)p + 4 + k);
+            xyzs[3 * p + k] = base + (u * 2.0f - 1.0f) * hgs;
+        }
+        cell[p] = ok ? (int32_t)((int64_t)c * a.cells + m) : -1;
+    }
+}
+
+__global__ __launch_bounds__(OCC_BLOCK) void occ_scatter_kernel(const float* __restrict__ sigma,
+                                                                const int32_t* __restrict__ cell, int64_t n,
+                                                                float* __restrict__ tmp) {
+    for (int64_t p = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; p < n; p += (int64_t)gridDim.x * OCC_BLOCK) {
+        const int32_t k = cell[p];
+        if (k >= 0) tmp[k] = sigma[p];
+    }
+}
+
+struct OccStats {
+    double sum;
+    unsigned long long count;
+    float thr;
+};
+
+__global__ __launch_bounds__(OCC_BLOCK) void occ_decay_kernel(float* __restrict__ grid, const float* __restrict__ tmp,
+                                                              const float* __restrict__ count_grid, int64_t n,
+                                                              float decay, OccStats* __restrict__ st) {
+    __shared__ double lds_d[OCC_BLOCK / 64];
+    __shared__ unsigned long long lds_u[OCC_BLOCK / 64];
+    double s = 0.0;
+    unsigned long long k = 0;
+    for (int64_t i = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * OCC_BLOCK) {
+        float v = grid[i];
+        if (!(v < 0.0f)) {
+            float d = decay;
+            if (count_grid) d = clampf(powf(decay, 1.0f / count_grid[i]), 0.1f, 0.95f);  // erode (networks.py:262)
+            v = fmaxf(v * d, tmp[i]);
+            grid[i] = v;
+        }
+        if (v > 0.0f) {
+            s += (double)v;
+            ++k;
+        }
+    }
+    s = block_sum(s, lds_d);
+    k = block_sum(k, lds_u);
+    if (threadIdx.x == 0) {
+        atomicAdd(&st->sum, s);
+        atomicAdd(&st->count, k);
+    }
+}
+
+// thr = min(mean, threshold) with Python's min(): NaN mean (no positive cell) stays NaN
+__global__ void occ_thr_kernel(OccStats* st, float threshold) {
+    const float mean = st->count ? (float)(st->sum / (double)st->count) : __builtin_nanf("");
+    st->thr = (threshold < mean) ? threshold : mean;
+}
+
+int64_t blocks_for(int64_t n, int64_t cap = 8192) {
+    const int64_t b = div_up<int64_t>(n, OCC_BLOCK);
+    return b < 1 ? 1 : (b < cap ? b : cap);
+}
+
+struct Ws {
+    int32_t* block_counts;
+    int32_t* counts;
+    int32_t* list;
+    OccStats* stats;
+};
+int64_t ws_layout(int cascades, int G, char* base, Ws* w) {
+    const int64_t cells = (int64_t)G * G * G;
+    const int64_t nblk = div_up<int64_t>(cells, OCC_CELLS_PER_BLOCK);
+    int64_t off = 0;
+    auto take = [&](int64_t bytes) { const int64_t o = off; off += (bytes + 255) / 256 * 256; return base + o; };
+    char* bc = take(4 * cascades * nblk);
+    char* ct = take(4 * cascades);
+    char* ls = take(4 * cascades * cells);
+    char* sp = take(sizeof(OccStats));
+    if (w) {
+        w->block_counts = (int32_t*)bc;
+        w->counts = (int32_t*)ct;
+        w->list = (int32_t*)ls;
+        w->stats = (OccStats*)sp;
+    }
+    return off;
+}
+
+bool bad_grid(int cascades, int G) { return cascades < 1 || cascades > 16 || G < 1 || G > 1024 || ((int64_t)G * G * G) % 8; }
+
+}  // namespace
+
+extern "C" {
+
+int64_t mfnerf_occupancy_workspace(int cascades, int grid_size) {
+    if (bad_grid(cascades, grid_size)) return -1;
+    return ws_layout(cascades, grid_size, nullptr, nullptr);
+}
+
+int64_t mfnerf_occupancy_points(int cascades, int grid_size, int64_t n_uniform, int warmup) {
+    if (bad_grid(cascades, grid_size) || n_uniform < 0) return -1;
+    const int64_t cells = (int64_t)grid_size * grid_size * grid_size;
+    return (int64_t)cascades * (warmup ? cells : 2 * n_uniform);
+}
+
+int mfnerf_occupancy_cells(const float* density_grid, int cascades, int grid_size, float scale, int64_t n_uniform,
+                           int warmup, float density_threshold, uint64_t seed, uint64_t call_index, float* xyzs,
+                           int32_t* cell_idx, void* workspace, mfnerf_stream_t stream) {
+    if (bad_grid(cascades, grid_size)) { mfn_set_error("occupancy_cells: bad cascades/grid_size"); return MFN_ERR_INVALID; }
+    if (n_uniform < 0 || (!warmup && n_uniform == 0)) { mfn_set_error("occupancy_cells: bad n_uniform"); return MFN_ERR_INVALID; }
+    if (!density_grid || !xyzs || !cell_idx || !workspace) { mfn_set_error("occupancy_cells: null pointer"); return MFN_ERR_INVALID; }
+    if (!(scale > 0.0f)) { mfn_set_error("occupancy_cells: scale must be > 0"); return MFN_ERR_INVALID; }
+    Ws w;
+    ws_layout(cascades, grid_size, (char*)workspace, &w);
+    const int64_t cells = (int64_t)grid_size * grid_size * grid_size;
+    const int64_t nblk = div_up<int64_t>(cells, OCC_CELLS_PER_BLOCK);
+    if (!warmup) {
+        hipLaunchKernelGGL(occ_count_kernel, dim3(nblk, cascades), dim3(OCC_BLOCK), 0, stream, density_grid, cells,
+                           density_threshold, w.block_counts);
+        hipLaunchKernelGGL(occ_compact_kernel, dim3(nblk, cascades), dim3(OCC_BLOCK), 0, stream, density_grid, cells,
+                           density_threshold, w.block_counts, w.list, w.counts);
+    }
+    PointsArgs a;
+    a.cascades = cascades;
+    a.G = grid_size;
+    a.cells = cells;
+    a.per_cascade = warmup ? cells : 2 * n_uniform;
+    a.n_uniform = warmup ? 0 : n_uniform;
+    a.warmup = warmup ? 1 : 0;
+    a.scale = scale;
+    a.key = (seed ^ 0x5851F42D4C957F2Dull) * 0x2545F4914F6CDD1Dull + call_index * 0x9E3779B97F4A7C15ull;
+    const int64_t n = (int64_t)cascades * a.per_cascade;
+    hipLaunchKernelGGL(occ_points_kernel, dim3(blocks_for(n)), dim3(OCC_BLOCK), 0, stream, a, w.list, w.counts, xyzs,
+                       cell_idx);
+    return mfn_check_launch("occupancy_cells");
+}
+
+int mfnerf_occupancy_update(float* density_grid, const float* sigmas, const int32_t* cell_idx, int64_t n_points,
+                            int cascades, int grid_size, float decay, const float* count_grid, float density_threshold,
+                            float* tmp, uint8_t* bitfield, void* workspace, mfnerf_stream_t stream) {
+    if (bad_grid(cascades, grid_size)) { mfn_set_error("occupancy_update: bad cascades/grid_size"); return MFN_ERR_INVALID; }
+    if (n_points < 0) { mfn_set_error("occupancy_update: bad n_points"); return MFN_ERR_INVALID; }
+    if (!density_grid || !tmp || !bitfield || !workspace || (n_points && (!sigmas || !cell_idx))) {
+        mfn_set_error("occupancy_update: null pointer");
+        return MFN_ERR_INVALID;
+    }
+    Ws w;
+    ws_layout(cascades, grid_size, (char*)workspace, &w);
+    const int64_t n = (int64_t)cascades * grid_size * grid_size * grid_size;
+    (void)hipMemsetAsync(tmp, 0, n * sizeof(float), stream);
+    (void)hipMemsetAsync(w.stats, 0, sizeof(OccStats), stream);
+    if (n_points)
+        hipLaunchKernelGGL(occ_scatter_kernel, dim3(blocks_for(n_points)), dim3(OCC_BLOCK), 0, stream, sigmas, cell_idx,
+                           n_points, tmp);
+    hipLaunchKernelGGL(occ_decay_kernel, dim3(blocks_for(n, 2048)), dim3(OCC_BLOCK), 0, stream, density_grid, tmp,
+                       count_grid, n, decay, w.stats);
+    hipLaunchKernelGGL(occ_thr_kernel, dim3(1), dim3(1), 0, stream, w.stats, density_threshold);
+    int st = mfn_check_launch("occupancy_update");
+    if (st) return st;
+    return mfnerf_packbits(density_grid, n / 8, 0.0f, &w.stats->thr, bitfield, stream);
+}
+
+}  // extern "C"

@@ -64,7 +64,11 @@ SIGNATURES = {
     "mfnerf_field_bw_workspace": (_I64, [_I64, _I]),
     "mfnerf_field_bw": (_I, [_P, _P, _I64, _P, _P, _I, _P, _P, _F, _P, _P, _P, _P, _P]),
     "mfnerf_debug_mfma_probe": (_I, [_P, _P, _P, _P]),
-    "mfnerf_adam_step": (_I, [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _I, _P, _P]),
+    "mfnerf_occupancy_workspace": (_I64, [_I, _I]),
+    "mfnerf_occupancy_points": (_I64, [_I, _I, _I64, _I]),
+    "mfnerf_occupancy_cells": (_I, [_P, _I, _I, _F, _I64, _I, _F, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P]),
+    "mfnerf_occupancy_update": (_I, [_P, _P, _P, _I64, _I, _I, _F, _P, _F, _P, _P, _P, _P]),
+    "mfnerf_adam_step": (_I, [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P]),
 }
 
 _lib = None

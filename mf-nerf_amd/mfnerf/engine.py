@@ -57,6 +57,13 @@ class _State:
     pass
 
 
+def _packed_batch(buf):
+    """Batch whose tensors are views into one (3, N, 3) buffer (rays_o, rays_d, rgb)."""
+    b = Batch(buf[0], buf[1], buf[2])
+    b.buf = buf
+    return b
+
+
 class TrainStep:
     def __init__(self, cfg: StepConfig, device="cuda", seed=0):
         self.cfg = cfg
@@ -92,7 +99,10 @@ class TrainStep:
         self.packed = torch.empty(load().mfnerf_field_packed_bytes(c.rgb_width) // 2, dtype=torch.float16,
                                   device=dev)
         self._pack()
-        self.adam_step = 0
+        self.adam_step = 0                                            # host mirror
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # Adam's t, bumped on the device
+        self.lr_dev = torch.full((1,), float(c.lr), dtype=torch.float32, device=dev)
+        self.graphs = None
 
         # scene bounding box (networks.py:18-23) and occupancy
         self.center = torch.zeros(1, 3, device=dev)
@@ -143,14 +153,15 @@ class TrainStep:
 
     # ---------------------------------------------------------------- data
     def make_batches(self, k, seed=0):
-        """k synthetic Lego-like ray batches (mfnerf.synthetic), resident on the device."""
+        """k synthetic Lego-like ray batches (mfnerf.synthetic), resident on the device; each is
+        packed in one (3, N, 3) buffer (rays_o, rays_d, rgb) so replay() refreshes with one copy."""
         poses = synthetic.camera_poses(seed=seed)
         out = []
         for i in range(k):
             o, d = synthetic.random_rays(self.cfg.n_rays, poses, seed=seed * 1000 + i)
             dn = d / d.norm(dim=1, keepdim=True)
             gt = 0.5 + 0.5 * torch.sin(3 * dn + torch.tensor([0.0, 1.0, 2.0]))  # smooth view-dependent target
-            out.append(Batch(o.to(self.dev), d.to(self.dev), gt.float().to(self.dev)))
+            out.append(_packed_batch(torch.stack([o, d, gt.float()]).to(self.dev)))
         return out
 
     def set_occupancy(self, density_grid):
@@ -164,12 +175,10 @@ class TrainStep:
              ptr(self.packed), stream())
 
     # ---------------------------------------------------------------- the step
-    def run(self, batch: Batch, mark=None, exchange=None):
-        """One training step.  mark(name) is called after each stage (bench timing); exchange(grads)
-        runs between backward and Adam (the data-parallel all-reduce)."""
+    def _fwbw(self, batch: Batch, mark):
+        """Segment 1: AABB -> march -> encode -> field -> composite -> loss -> composite bw -> field bw."""
         c, st, s = self.cfg, self.state, stream()
         N, cap = c.n_rays, self.cap
-        mark = mark or (lambda name: None)
         # rendering.py:27-29 (AABB + near clamp), custom_functions.py:83 (noise)
         call("mfnerf_ray_aabb_intersect", ptr(batch.rays_o), ptr(batch.rays_d), ptr(self.center),
              ptr(self.half_size), N, 1, 1, ptr(st.hit_cnt), ptr(st.hits), ptr(st.hits_idx), s)
@@ -204,8 +213,26 @@ class TrainStep:
              ptr(st.dsig), ptr(st.drgb_s), self.grad_scale, ptr(st.dfeat), ptr(self.grads),
              ptr(self.grads[self.off_rgb:]), ptr(st.field_ws), s)
         mark("field_bw")
-        call("mfnerf_grid_encode_bw", ptr(st.xyzs), cap, ptr(st.counter), self.x_min, self.x_range, self.desc,
-             ptr(st.dfeat), ptr(self.grads[self.off_table:]), ptr(st.grid_ws), s)
+
+    def _grid_bw(self):
+        """Segment 2: the hash-table gradient scatter (the dominant kernel)."""
+        st = self.state
+        call("mfnerf_grid_encode_bw", ptr(st.xyzs), self.cap, ptr(st.counter), self.x_min, self.x_range, self.desc,
+             ptr(st.dfeat), ptr(self.grads[self.off_table:]), ptr(st.grid_ws), stream())
+
+    def _update(self):
+        """Segment 3: Adam over the flat params (+ fp16 mirror) and the MLP weight repack."""
+        c = self.cfg
+        call("mfnerf_adam_step", ptr(self.params), ptr(self.grads), ptr(self.m), ptr(self.v), ptr(self.p16),
+             self.n_params, float(c.lr), 0.9, 0.999, c.eps, 1.0, 0, ptr(self.step_dev), ptr(self.lr_dev), stream())
+        self._pack()
+
+    def run(self, batch: Batch, mark=None, exchange=None):
+        """One training step, eagerly.  mark(name) is called after each stage (bench timing);
+        exchange(grads) runs between backward and Adam (the data-parallel all-reduce)."""
+        mark = mark or (lambda name: None)
+        self._fwbw(batch, mark)
+        self._grid_bw()
         mark("grid_bw")
         if exchange is not None:
             exchange(self.grads)
@@ -214,57 +241,89 @@ class TrainStep:
         mark("adam")
 
     def optimizer(self, lr=None):
-        c = self.cfg
+        if lr is not None:
+            self.set_lr(lr)
         self.adam_step += 1
-        call("mfnerf_adam_step", ptr(self.params), ptr(self.grads), ptr(self.m), ptr(self.v), ptr(self.p16),
-             self.n_params, float(c.lr if lr is None else lr), 0.9, 0.999, c.eps, 1.0, self.adam_step, None, stream())
-        self._pack()
+        self._update()
+
+    def set_lr(self, lr):
+        """Device-resident learning rate (train.py:137-142 cosine schedule), read by Adam."""
+        self.lr_dev.fill_(float(lr))
 
     def step(self, batch: Batch):
         self.run(batch)
 
-    # ---------------------------------------------------------------- occupancy (networks.py:242-271)
+    # ---------------------------------------------------------------- HIP graphs
+    def capture(self):
+        """Capture the step as three HIP graphs -- [fwd+bwd to field_bw], [grid_bw], [Adam+repack] --
+        over a static input batch.  Splitting at grid_bw lets the caller time the dominant kernel
+        with events and run the data-parallel all-reduce (eager RCCL) between graphs 2 and 3.
+        Call after at least one eager step (lazy library init happens outside capture)."""
+        N = self.cfg.n_rays
+        self._static = _packed_batch(torch.zeros(3, N, 3, device=self.dev))
+        torch.cuda.synchronize()
+        pool = torch.cuda.graph_pool_handle()
+        graphs = {}
+        for name, fn in (("fwbw", lambda: self._fwbw(self._static, lambda _n: None)), ("grid_bw", self._grid_bw),
+                         ("update", self._update)):
+            g = torch.cuda.CUDAGraph()
+            if name == "fwbw":
+                g.register_generator_state(self.gen)
+            with torch.cuda.graph(g, pool=pool):
+                fn()
+            graphs[name] = g
+        torch.cuda.synchronize()
+        self.graphs = graphs
+
+    def replay(self, batch: Batch, mark=None, exchange=None):
+        """One training step from the captured graphs (same kernels and buffers as run())."""
+        mark = mark or (lambda name: None)
+        g = self.graphs
+        self._static.buf.copy_(batch.buf)
+        g["fwbw"].replay()
+        mark("fwbw")
+        g["grid_bw"].replay()
+        mark("grid_bw")
+        if exchange is not None:
+            exchange(self.grads)
+        mark("allreduce")
+        self.adam_step += 1
+        g["update"].replay()
+        mark("adam")
+
+    # ---------------------------------------------------------------- occupancy (networks.py:157-271)
+    def _occ_buffers(self):
+        """Scratch for the refresh, sized for the warm-up (all cells) case, allocated once."""
+        if getattr(self, "_occ", None) is None:
+            lib, c, C, G = load(), self.cfg, self.cascades, self.G
+            n = max(lib.mfnerf_occupancy_points(C, G, G ** 3 // 4, 0), lib.mfnerf_occupancy_points(C, G, 0, 1))
+            o = _State()
+            o.n_max = n
+            o.xyz = torch.empty(n, 3, dtype=torch.float32, device=self.dev)
+            o.cell = torch.empty(n, dtype=torch.int32, device=self.dev)
+            o.feat = torch.empty(n, c.L * c.F, dtype=torch.float16, device=self.dev)
+            o.sigma = torch.empty(n, dtype=torch.float32, device=self.dev)
+            o.tmp = torch.empty(C * G ** 3, dtype=torch.float32, device=self.dev)
+            o.ws = torch.empty(lib.mfnerf_occupancy_workspace(C, G), dtype=torch.uint8, device=self.dev)
+            o.calls = 0
+            self._occ = o
+        return self._occ
+
     @torch.no_grad()
-    def update_density_grid(self, warmup=False, decay=0.95):
-        """Device-only version of NGP.update_density_grid: no .item(), the packbits threshold is
-        read from device memory."""
-        c = self.cfg
-        G, dev = self.G, self.dev
+    def update_density_grid(self, warmup=False, decay=0.95, count_grid=None, seed=0):
+        """NGP.update_density_grid(0.01*MAX_SAMPLES/sqrt(3), warmup, erode) as five device launches
+        (cells -> grid_encode_fw -> field_fw density-only -> scatter/decay/mean -> packbits); no
+        host synchronisation, so it can sit inside a captured step sequence."""
+        c, C, G, s = self.cfg, self.cascades, self.G, stream()
+        o = self._occ_buffers()
         thr = 0.01 * MAX_SAMPLES / SQRT3
-        tmp = torch.zeros_like(self.density_grid)
-        for ci in range(self.cascades):
-            if warmup:
-                r = torch.arange(G, dtype=torch.int32, device=dev)
-                coords = torch.stack(torch.meshgrid(r, r, r, indexing="ij"), -1).reshape(-1, 3).contiguous()
-            else:
-                M = G ** 3 // 4
-                coords1 = torch.randint(G, (M, 3), dtype=torch.int32, device=dev, generator=self.gen)
-                occ = self.density_grid[ci] > thr
-                # M samples among occupied cells (uniform over the occupied set) without a host sync
-                w = occ.float() + 1e-30
-                idx2 = torch.multinomial(w, M, replacement=True, generator=self.gen).int().contiguous()
-                coords2 = torch.empty(M, 3, dtype=torch.int32, device=dev)
-                call("mfnerf_morton3d_invert", ptr(idx2), M, ptr(coords2), stream())
-                coords = torch.cat([coords1, coords2]).contiguous()
-            idx = torch.empty(coords.shape[0], dtype=torch.int32, device=dev)
-            call("mfnerf_morton3d", ptr(coords), coords.shape[0], ptr(idx), stream())
-            s = min(2 ** (ci - 1), c.scale)
-            hgs = s / G
-            xyz = (coords / (G - 1) * 2 - 1) * (s - hgs)
-            xyz += (torch.rand(xyz.shape, generator=self.gen, device=dev) * 2 - 1) * hgs
-            xyz = xyz.contiguous()
-            n = xyz.shape[0]
-            feat = torch.empty(n, c.L * c.F, dtype=torch.float16, device=dev)
-            sig = torch.empty(n, device=dev)
-            call("mfnerf_grid_encode_fw", ptr(xyz), n, None, self.x_min, self.x_range, self.desc,
-                 ptr(self.p16[self.off_table:]), ptr(feat), stream())
-            call("mfnerf_field_fw", ptr(feat), None, n, None, ptr(self.packed), c.rgb_width, 1, ptr(sig), None,
-                 stream())
-            tmp[ci, idx.long()] = sig
-        self.density_grid.copy_(torch.where(self.density_grid < 0, self.density_grid,
-                                            torch.maximum(self.density_grid * decay, tmp)))
-        pos = self.density_grid > 0
-        mean = (self.density_grid * pos).sum() / pos.sum().clamp(min=1)
-        thr_dev = torch.minimum(mean, torch.tensor(thr, device=dev)).reshape(1)
-        call("mfnerf_packbits", ptr(self.density_grid), self.bitfield.numel(), 0.0, ptr(thr_dev), ptr(self.bitfield),
-             stream())
+        M = G ** 3 // 4
+        n = load().mfnerf_occupancy_points(C, G, M, int(warmup))
+        call("mfnerf_occupancy_cells", ptr(self.density_grid), C, G, float(c.scale), M, int(warmup), thr, seed,
+             o.calls, ptr(o.xyz), ptr(o.cell), ptr(o.ws), s)
+        o.calls += 1
+        call("mfnerf_grid_encode_fw", ptr(o.xyz), n, None, self.x_min, self.x_range, self.desc,
+             ptr(self.p16[self.off_table:]), ptr(o.feat), s)
+        call("mfnerf_field_fw", ptr(o.feat), None, n, None, ptr(self.packed), c.rgb_width, 1, ptr(o.sigma), None, s)
+        call("mfnerf_occupancy_update", ptr(self.density_grid), ptr(o.sigma), ptr(o.cell), n, C, G, float(decay),
+             ptr(count_grid) if count_grid is not None else None, thr, ptr(o.tmp), ptr(self.bitfield), ptr(o.ws), s)
