@@ -133,32 +133,60 @@ __device__ __forceinline__ int dpp_i(int v) {
 #define DPP_ROW_SHL(d) (0x100 | (d))
 #define DPP_ROW_SHR(d) (0x110 | (d))
 
-template <int ABLATE>  // 0 = product; debug builds: 1 plain stores, 2 levels 0-5 only, 3 levels 10-15 only
+// ABLATE: 0 = product; debug builds: 1 plain stores, 2 levels 0-5 only, 3 levels 10-15 only.
+// MAXL: level-count bound (16 or 32) sizing the LDS tile and the prefetch registers.
+template <int ABLATE, int MAXL>
 __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restrict__ X, int64_t n,
                                                              const int32_t* __restrict__ n_dev, float x_min,
                                                              float x_range, const mfnerf_grid_desc D,
                                                              const float* __restrict__ dy, float* __restrict__ grad,
                                                              float* __restrict__ priv, int64_t dense_entries) {
+    // dL/dy of the wave's chunk (16 samples x 2L floats) is staged in LDS (rows padded by one
+    // float: conflict-free column reads) and the NEXT chunk is prefetched into registers before
+    // this chunk's atomics are issued.  On gfx9 no-return atomics count in vmcnt, so a global load
+    // between atomics would make the wave wait for every earlier atomic's round trip; with the
+    // loads hoisted there is at most one such wait per chunk (64 atomics) instead of per level.
+    __shared__ float sdy_all[ENC_BLOCK / 64][16 * (2 * MAXL + 1)];
     const int L_ = D.n_levels;
     const int lane = threadIdx.x & 63, s = lane & 15, f = (lane >> 4) & 1, xb = lane >> 5;
+    const int row = 2 * L_, rs = 2 * L_ + 1, per_chunk = 16 * row;
+    float* sdy = sdy_all[threadIdx.x >> 6];
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     const int64_t chunks = div_up<int64_t>(nn, 16);
     const int64_t wave0 = ((int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x) >> 6;
     const int64_t n_waves = ((int64_t)gridDim.x * ENC_BLOCK) >> 6;
+    const int64_t n_vals = nn * row;
+
+    float pf[MAXL / 2];  // this lane's share of a chunk's dL/dy
+    float px = 0.0f, py = 0.0f, pz = 0.0f;
+    auto fetch = [&](int64_t ch) {
+        const int64_t base = ch * per_chunk;
+#pragma unroll
+        for (int k = 0; k < MAXL / 2; ++k) {
+            const int idx = lane + 64 * k;
+            pf[k] = (idx < per_chunk && base + idx < n_vals) ? dy[base + idx] : 0.0f;
+        }
+        const int64_t i = ch * 16 + s;
+        if (i < nn) { px = X[3 * i]; py = X[3 * i + 1]; pz = X[3 * i + 2]; }
+    };
+    if (wave0 < chunks) fetch(wave0);
     for (int64_t chunk = wave0; chunk < chunks; chunk += n_waves) {
         const int64_t i = chunk * 16 + s;
         const bool valid = i < nn;
-        float x = 0.0f, y = 0.0f, z = 0.0f;
-        if (valid) {
-            x = (X[3 * i] - x_min) / x_range;
-            y = (X[3 * i + 1] - x_min) / x_range;
-            z = (X[3 * i + 2] - x_min) / x_range;
+#pragma unroll
+        for (int k = 0; k < MAXL / 2; ++k) {
+            const int idx = lane + 64 * k;
+            if (idx < per_chunk) sdy[(idx / row) * rs + idx % row] = pf[k];
         }
-        const float* dyi = dy + i * (2 * L_) + f;
+        const float x = valid ? (px - x_min) / x_range : 0.0f;
+        const float y = valid ? (py - x_min) / x_range : 0.0f;
+        const float z = valid ? (pz - x_min) / x_range : 0.0f;
+        if (chunk + n_waves < chunks) fetch(chunk + n_waves);  // in flight during this chunk's atomics
+        const float* srow = sdy + s * rs + f;
         for (int l = 0; l < L_; ++l) {
             if (ABLATE == 2 && l > 5) continue;
             if (ABLATE == 3 && l < 10) continue;
-            const float g = valid ? dyi[2 * l] : 0.0f;
+            const float g = srow[2 * l];
             const LevelGeo Lg = level_geo(D.scale[l], x, y, z);
             const bool spread = priv && (int64_t)D.offset[l] + D.size[l] <= dense_entries;
             float* gt = spread ? priv + 2 * ((chunk & (GRAD_COPIES - 1)) * dense_entries + (int64_t)D.offset[l])
@@ -262,7 +290,8 @@ int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float
     const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16), ENC_BLOCK / 64);
     const int64_t blocks = want < 4096 ? want : 4096;
     const int64_t dense = workspace ? dense_entries_of(desc) : 0;
-    hipLaunchKernelGGL(grid_bw_kernel<0>, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0,
+    auto kern = desc->n_levels <= 16 ? grid_bw_kernel<0, 16> : grid_bw_kernel<0, MFN_MAX_LEVELS>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0,
                        stream, x, n, n_dev, x_min, x_range, *desc, dL_dout, grad_table, (float*)workspace, dense);
     if (dense > 0) {
         const int64_t nf = 2 * dense;  // multiple of 16 (level sizes are multiples of 8)
@@ -279,8 +308,11 @@ int mfnerf_debug_grid_bw_ablate(int mode, const float* x, int64_t n, const int32
                                 mfnerf_stream_t stream) {
     const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16), ENC_BLOCK / 64);
     const int64_t blocks = want < 4096 ? want : 4096;
-    auto k = mode == 1 ? grid_bw_kernel<1> : mode == 2 ? grid_bw_kernel<2> : mode == 3 ? grid_bw_kernel<3>
-                                                                                           : grid_bw_kernel<0>;
+    if (desc->n_levels > 16) { mfn_set_error("grid_bw_ablate: n_levels <= 16 only"); return MFN_ERR_INVALID; }
+    auto k = mode == 1   ? grid_bw_kernel<1, 16>
+             : mode == 2 ? grid_bw_kernel<2, 16>
+             : mode == 3 ? grid_bw_kernel<3, 16>
+                         : grid_bw_kernel<0, 16>;
     hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc,
                        dL_dout, grad_table, nullptr, (int64_t)0);
     return mfn_check_launch("grid_bw_ablate");

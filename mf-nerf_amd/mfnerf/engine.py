@@ -275,21 +275,26 @@ class TrainStep:
         torch.cuda.synchronize()
         self.graphs = graphs
 
-    def replay(self, batch: Batch, mark=None, exchange=None):
-        """One training step from the captured graphs (same kernels and buffers as run())."""
-        mark = mark or (lambda name: None)
+    def replay(self, batch: Batch, exchange=None, grid_bw_events=None):
+        """One training step from the captured graphs (same kernels and buffers as run()).
+        grid_bw_events: optional (start, end) timing events recorded around the grid_bw graph."""
         g = self.graphs
-        self._static.buf.copy_(batch.buf)
+        if getattr(batch, "buf", None) is not None:
+            self._static.buf.copy_(batch.buf)
+        else:
+            for dst, src in zip((self._static.rays_o, self._static.rays_d, self._static.rgb),
+                                (batch.rays_o, batch.rays_d, batch.rgb)):
+                dst.copy_(src)
         g["fwbw"].replay()
-        mark("fwbw")
+        if grid_bw_events is not None:
+            grid_bw_events[0].record()
         g["grid_bw"].replay()
-        mark("grid_bw")
+        if grid_bw_events is not None:
+            grid_bw_events[1].record()
         if exchange is not None:
             exchange(self.grads)
-        mark("allreduce")
         self.adam_step += 1
         g["update"].replay()
-        mark("adam")
 
     # ---------------------------------------------------------------- occupancy (networks.py:157-271)
     def _occ_buffers(self):
