@@ -113,20 +113,10 @@ class TrainStep:
         N, cap = c.n_rays, c.n_rays * c.max_samples
         self.cap = cap
         st = _State()
+        self.state = st
         f32 = dict(dtype=torch.float32, device=dev)
-        st.hit_cnt = torch.empty(N, dtype=torch.int32, device=dev)
-        st.hits = torch.empty(N, 1, 2, **f32)
-        st.hits_t = st.hits[:, 0]
-        st.hits_idx = torch.empty(N, 1, dtype=torch.int64, device=dev)
-        st.noise = torch.empty(N, **f32)
-        st.rays_a = torch.empty(N, 3, dtype=torch.int64, device=dev)
-        st.xyzs = torch.empty(cap, 3, **f32)
-        st.dirs = torch.empty(cap, 3, **f32)
-        st.deltas = torch.empty(cap, **f32)
-        st.ts = torch.empty(cap, **f32)
-        st.counter = torch.zeros(2, dtype=torch.int32, device=dev)
-        st.march_ws = torch.empty(max(16, load().mfnerf_raymarching_train_workspace(N)), dtype=torch.uint8,
-                                  device=dev)
+        self.mbuf = [self._march_buffers()]  # a second set is added by capture() (pipelined march)
+        self._use(self.mbuf[0])
         st.feat = torch.empty(cap, c.L * c.F, dtype=torch.float16, device=dev)
         st.sigma = torch.empty(cap, **f32)
         st.rgb_s = torch.empty(cap, 3, **f32)
@@ -145,11 +135,38 @@ class TrainStep:
         st.field_ws = torch.empty(load().mfnerf_field_bw_workspace(cap, c.rgb_width) // 4, **f32)
         st.loss_sum = torch.zeros(1, **f32)
         st.grid_ws = torch.zeros(max(16, load().mfnerf_grid_encode_bw_workspace(self.desc)) // 4, **f32)
-        self.state = st
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(seed + 1)
         # fp16 backward scale: per-sample grads are O(1/n_rays); 2^(floor(log2 N)-2) keeps them normal
         self.grad_scale = float(2.0 ** max(0, int(math.floor(math.log2(N))) - 2))
+
+    MARCH_FIELDS = ("hit_cnt", "hits", "hits_t", "hits_idx", "noise", "rays_a", "xyzs", "dirs", "deltas", "ts",
+                    "counter", "march_ws")
+
+    def _march_buffers(self):
+        """One set of ray-march outputs (and their scratch), sized for n_rays * MAX_SAMPLES."""
+        N, cap, dev = self.cfg.n_rays, self.cap, self.dev
+        f32 = dict(dtype=torch.float32, device=dev)
+        m = _State()
+        m.hit_cnt = torch.empty(N, dtype=torch.int32, device=dev)
+        m.hits = torch.empty(N, 1, 2, **f32)
+        m.hits_t = m.hits[:, 0]
+        m.hits_idx = torch.empty(N, 1, dtype=torch.int64, device=dev)
+        m.noise = torch.empty(N, **f32)
+        m.rays_a = torch.empty(N, 3, dtype=torch.int64, device=dev)
+        m.xyzs = torch.empty(cap, 3, **f32)
+        m.dirs = torch.empty(cap, 3, **f32)
+        m.deltas = torch.empty(cap, **f32)
+        m.ts = torch.empty(cap, **f32)
+        m.counter = torch.zeros(2, dtype=torch.int32, device=dev)
+        m.march_ws = torch.empty(max(16, load().mfnerf_raymarching_train_workspace(N)), dtype=torch.uint8, device=dev)
+        return m
+
+    def _use(self, mb):
+        """Point state.<march field> at the buffer set of the step being run (for callers that
+        inspect state.rays_a / state.counter / ... after a step)."""
+        for k in self.MARCH_FIELDS:
+            setattr(self.state, k, getattr(mb, k))
 
     # ---------------------------------------------------------------- data
     def make_batches(self, k, seed=0):
@@ -175,29 +192,34 @@ class TrainStep:
              ptr(self.packed), stream())
 
     # ---------------------------------------------------------------- the step
-    def _fwbw(self, batch: Batch, mark):
-        """Segment 1: AABB -> march -> encode -> field -> composite -> loss -> composite bw -> field bw."""
-        c, st, s = self.cfg, self.state, stream()
+    def _march(self, batch: Batch, mb, mark):
+        """Segment 0: AABB + near clamp + noise + ray march into the buffer set mb."""
+        c, s = self.cfg, stream()
         N, cap = c.n_rays, self.cap
         # rendering.py:27-29 (AABB + near clamp), custom_functions.py:83 (noise)
         call("mfnerf_ray_aabb_intersect", ptr(batch.rays_o), ptr(batch.rays_d), ptr(self.center),
-             ptr(self.half_size), N, 1, 1, ptr(st.hit_cnt), ptr(st.hits), ptr(st.hits_idx), s)
-        t1 = st.hits[:, 0, 0]
+             ptr(self.half_size), N, 1, 1, ptr(mb.hit_cnt), ptr(mb.hits), ptr(mb.hits_idx), s)
+        t1 = mb.hits[:, 0, 0]
         t1.masked_fill_((t1 >= 0) & (t1 < NEAR_DISTANCE), NEAR_DISTANCE)
-        torch.rand(N, generator=self.gen, device=self.dev, out=st.noise)
+        torch.rand(N, generator=self.gen, device=self.dev, out=mb.noise)
         mark("prep")
-        call("mfnerf_raymarching_train", ptr(batch.rays_o), ptr(batch.rays_d), ptr(st.hits_t), 2, ptr(self.bitfield),
-             self.cascades, float(c.scale), 0.0 if c.scale <= 0.5 else 1 / 256, ptr(st.noise), self.G,
-             c.max_samples, N, cap, ptr(st.rays_a), ptr(st.xyzs), ptr(st.dirs), ptr(st.deltas), ptr(st.ts),
-             ptr(st.counter), ptr(st.march_ws), s)
+        call("mfnerf_raymarching_train", ptr(batch.rays_o), ptr(batch.rays_d), ptr(mb.hits_t), 2, ptr(self.bitfield),
+             self.cascades, float(c.scale), 0.0 if c.scale <= 0.5 else 1 / 256, ptr(mb.noise), self.G,
+             c.max_samples, N, cap, ptr(mb.rays_a), ptr(mb.xyzs), ptr(mb.dirs), ptr(mb.deltas), ptr(mb.ts),
+             ptr(mb.counter), ptr(mb.march_ws), s)
         mark("march")
-        call("mfnerf_grid_encode_fw", ptr(st.xyzs), cap, ptr(st.counter), self.x_min, self.x_range, self.desc,
+
+    def _fwbw(self, batch: Batch, mb, mark):
+        """Segment 1: encode -> field -> composite -> loss -> composite bw -> field bw on mb's samples."""
+        c, st, s = self.cfg, self.state, stream()
+        N, cap = c.n_rays, self.cap
+        call("mfnerf_grid_encode_fw", ptr(mb.xyzs), cap, ptr(mb.counter), self.x_min, self.x_range, self.desc,
              ptr(self.p16[self.off_table:]), ptr(st.feat), s)
         mark("grid_fw")
-        call("mfnerf_field_fw", ptr(st.feat), ptr(st.dirs), cap, ptr(st.counter), ptr(self.packed), c.rgb_width, 0,
+        call("mfnerf_field_fw", ptr(st.feat), ptr(mb.dirs), cap, ptr(mb.counter), ptr(self.packed), c.rgb_width, 0,
              ptr(st.sigma), ptr(st.rgb_s), s)
         mark("field_fw")
-        call("mfnerf_composite_train_fw", ptr(st.sigma), ptr(st.rgb_s), ptr(st.deltas), ptr(st.ts), ptr(st.rays_a),
+        call("mfnerf_composite_train_fw", ptr(st.sigma), ptr(st.rgb_s), ptr(mb.deltas), ptr(mb.ts), ptr(mb.rays_a),
              N, cap, c.T_threshold, ptr(st.total), ptr(st.opacity), ptr(st.depth), ptr(st.rgb), ptr(st.ws), s)
         bg = 1.0 if c.scale <= 0.5 else 0.0
         st.loss_sum.zero_()
@@ -205,19 +227,19 @@ class TrainStep:
              ptr(st.dL_drgb), ptr(st.dL_dop), ptr(st.loss_sum), s)
         mark("composite_fw")
         call("mfnerf_composite_train_bw", ptr(st.dL_dop), ptr(st.zeros_ray), ptr(st.dL_drgb), ptr(st.zeros_samp),
-             ptr(st.sigma), ptr(st.rgb_s), ptr(st.ws), ptr(st.deltas), ptr(st.ts), ptr(st.rays_a), ptr(st.opacity),
+             ptr(st.sigma), ptr(st.rgb_s), ptr(st.ws), ptr(mb.deltas), ptr(mb.ts), ptr(mb.rays_a), ptr(st.opacity),
              ptr(st.depth), ptr(st.rgb), N, cap, c.T_threshold, ptr(st.dsig), ptr(st.drgb_s), s)
         mark("composite_bw")
         self.grads.zero_()
-        call("mfnerf_field_bw", ptr(st.feat), ptr(st.dirs), cap, ptr(st.counter), ptr(self.packed), c.rgb_width,
+        call("mfnerf_field_bw", ptr(st.feat), ptr(mb.dirs), cap, ptr(mb.counter), ptr(self.packed), c.rgb_width,
              ptr(st.dsig), ptr(st.drgb_s), self.grad_scale, ptr(st.dfeat), ptr(self.grads),
              ptr(self.grads[self.off_rgb:]), ptr(st.field_ws), s)
         mark("field_bw")
 
-    def _grid_bw(self):
+    def _grid_bw(self, mb):
         """Segment 2: the hash-table gradient scatter (the dominant kernel)."""
         st = self.state
-        call("mfnerf_grid_encode_bw", ptr(st.xyzs), self.cap, ptr(st.counter), self.x_min, self.x_range, self.desc,
+        call("mfnerf_grid_encode_bw", ptr(mb.xyzs), self.cap, ptr(mb.counter), self.x_min, self.x_range, self.desc,
              ptr(st.dfeat), ptr(self.grads[self.off_table:]), ptr(st.grid_ws), stream())
 
     def _update(self):
@@ -228,11 +250,15 @@ class TrainStep:
         self._pack()
 
     def run(self, batch: Batch, mark=None, exchange=None):
-        """One training step, eagerly.  mark(name) is called after each stage (bench timing);
-        exchange(grads) runs between backward and Adam (the data-parallel all-reduce)."""
+        """One training step, eagerly, in buffer set 0.  mark(name) is called after each stage
+        (bench timing); exchange(grads) runs between backward and Adam (the data-parallel all-reduce)."""
         mark = mark or (lambda name: None)
-        self._fwbw(batch, mark)
-        self._grid_bw()
+        mb = self.mbuf[0]
+        self._use(mb)
+        self._primed = False  # a pipelined replay() must march its own batch next
+        self._march(batch, mb, mark)
+        self._fwbw(batch, mb, mark)
+        self._grid_bw(mb)
         mark("grid_bw")
         if exchange is not None:
             exchange(self.grads)
@@ -255,46 +281,86 @@ class TrainStep:
 
     # ---------------------------------------------------------------- HIP graphs
     def capture(self):
-        """Capture the step as three HIP graphs -- [fwd+bwd to field_bw], [grid_bw], [Adam+repack] --
-        over a static input batch.  Splitting at grid_bw lets the caller time the dominant kernel
-        with events and run the data-parallel all-reduce (eager RCCL) between graphs 2 and 3.
-        Call after at least one eager step (lazy library init happens outside capture)."""
+        """Capture the step as HIP graphs over two alternating buffer sets j = 0, 1:
+        march[j] (AABB + noise + march of static batch j), fwbw[j], grid_bw[j], and update (Adam +
+        repack).  replay() runs march[j'] of the NEXT step on a side stream while grid_bw[j] of this
+        one runs on the main stream (the march needs neither this step's gradients nor its update;
+        grid_bw is bound by memory-side atomics and leaves the CUs mostly idle).  The split at
+        grid_bw also lets the caller time it with events and run the data-parallel all-reduce
+        between graphs.  Call after at least one eager step (lazy library init outside capture)."""
         N = self.cfg.n_rays
-        self._static = _packed_batch(torch.zeros(3, N, 3, device=self.dev))
+        if len(self.mbuf) == 1:
+            self.mbuf.append(self._march_buffers())
+        self._static = [_packed_batch(torch.zeros(3, N, 3, device=self.dev)) for _ in range(2)]
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
-        graphs = {}
-        for name, fn in (("fwbw", lambda: self._fwbw(self._static, lambda _n: None)), ("grid_bw", self._grid_bw),
-                         ("update", self._update)):
+        nomark = lambda _n: None  # noqa: E731
+
+        def cap(fn, rng=False):
             g = torch.cuda.CUDAGraph()
-            if name == "fwbw":
+            if rng:
                 g.register_generator_state(self.gen)
             with torch.cuda.graph(g, pool=pool):
                 fn()
-            graphs[name] = g
-        torch.cuda.synchronize()
-        self.graphs = graphs
+            return g
 
-    def replay(self, batch: Batch, exchange=None, grid_bw_events=None):
-        """One training step from the captured graphs (same kernels and buffers as run()).
-        grid_bw_events: optional (start, end) timing events recorded around the grid_bw graph."""
-        g = self.graphs
+        self.graphs = {
+            "march": [cap(lambda j=j: self._march(self._static[j], self.mbuf[j], nomark), rng=True) for j in range(2)],
+            "fwbw": [cap(lambda j=j: self._fwbw(self._static[j], self.mbuf[j], nomark)) for j in range(2)],
+            "grid_bw": [cap(lambda j=j: self._grid_bw(self.mbuf[j])) for j in range(2)],
+            "update": cap(self._update),
+        }
+        torch.cuda.synchronize()
+        self._side = torch.cuda.Stream(device=self.dev)
+        self._ev_march = [torch.cuda.Event(), torch.cuda.Event()]
+        self._ev_fwbw = torch.cuda.Event()
+        self._parity = 0
+        self._primed = False
+
+    def _stage_batch(self, j, batch):
+        dst = self._static[j]
         if getattr(batch, "buf", None) is not None:
-            self._static.buf.copy_(batch.buf)
+            dst.buf.copy_(batch.buf)
         else:
-            for dst, src in zip((self._static.rays_o, self._static.rays_d, self._static.rgb),
-                                (batch.rays_o, batch.rays_d, batch.rgb)):
-                dst.copy_(src)
-        g["fwbw"].replay()
+            for d, s_ in zip((dst.rays_o, dst.rays_d, dst.rgb), (batch.rays_o, batch.rays_d, batch.rgb)):
+                d.copy_(s_)
+
+    def _march_on_side(self, j, batch):
+        """Copy batch into static set j and march it on the side stream (after the main stream's
+        work so far: set j's buffers were last read by the grid_bw two steps back)."""
+        main = torch.cuda.current_stream()
+        self._ev_fwbw.record(main)
+        self._side.wait_event(self._ev_fwbw)
+        with torch.cuda.stream(self._side):
+            self._stage_batch(j, batch)
+            self.graphs["march"][j].replay()
+            self._ev_march[j].record(self._side)
+
+    def replay(self, batch: Batch, exchange=None, grid_bw_events=None, next_batch=None):
+        """One training step from the captured graphs (same kernels as run()).  With next_batch, the
+        next step's march is issued on the side stream to overlap this step's grid_bw; the next
+        replay() must then be called with that batch.  grid_bw_events: optional (start, end) timing
+        events recorded around the grid_bw graph."""
+        g, j = self.graphs, self._parity
+        main = torch.cuda.current_stream()
+        if not self._primed:
+            self._march_on_side(j, batch)
+        main.wait_event(self._ev_march[j])
+        self._use(self.mbuf[j])
+        g["fwbw"][j].replay()
+        if next_batch is not None:
+            self._march_on_side(1 - j, next_batch)
         if grid_bw_events is not None:
-            grid_bw_events[0].record()
-        g["grid_bw"].replay()
+            grid_bw_events[0].record(main)
+        g["grid_bw"][j].replay()
         if grid_bw_events is not None:
-            grid_bw_events[1].record()
+            grid_bw_events[1].record(main)
         if exchange is not None:
             exchange(self.grads)
         self.adam_step += 1
         g["update"].replay()
+        self._parity = 1 - j
+        self._primed = next_batch is not None
 
     # ---------------------------------------------------------------- occupancy (networks.py:157-271)
     def _occ_buffers(self):

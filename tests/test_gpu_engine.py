@@ -1,0 +1,63 @@
+"""The fused training step: eager run() vs the captured, pipelined replay() (next step's march on a
+side stream under this step's grid_bw).  Same seed -> same noise stream, so march outputs must be
+identical step by step (bit-exact, also against the C oracle) and losses equal up to the float
+atomics' summation order."""
+import numpy as np
+import pytest
+import torch
+
+from mfnerf import engine, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _make(gpu):
+    st = engine.TrainStep(engine.StepConfig(n_rays=1024, log2_T=16), device=gpu, seed=0)
+    st.set_occupancy(synthetic.ball_density_grid())
+    return st
+
+
+def _record(st):
+    s = st.state
+    n = int(s.counter[0])
+    return {"noise": s.noise.clone(), "n": n, "rays_a": s.rays_a.clone(), "xyzs": s.xyzs[:n].clone(),
+            "loss": float(s.loss_sum)}
+
+
+def test_pipelined_replay_matches_eager(gpu, oracle):
+    K = 6
+    a, b = _make(gpu), _make(gpu)
+    batches = a.make_batches(K + 1, seed=3)
+    # eager reference
+    ref = []
+    for k in range(K):
+        b.run(batches[k])
+        torch.cuda.synchronize()
+        ref.append(_record(b))
+    # pipelined graphs: step 0 eager (lazy init), capture, then replays with the next batch pre-marched
+    a.run(batches[0])
+    torch.cuda.synchronize()
+    got = [_record(a)]
+    a.capture()
+    for k in range(1, K):
+        a.replay(batches[k], next_batch=batches[k + 1] if k + 1 < K else None)
+        torch.cuda.synchronize()
+        got.append(_record(a))
+    for k in range(K):
+        r, g = ref[k], got[k]
+        assert torch.equal(g["noise"], r["noise"]), f"step {k}: noise stream differs"
+        assert g["n"] == r["n"] and torch.equal(g["rays_a"], r["rays_a"]) and torch.equal(g["xyzs"], r["xyzs"])
+        assert abs(g["loss"] - r["loss"]) <= 1e-3 * abs(r["loss"]), (k, g["loss"], r["loss"])
+    # the march each replay used is the reference's march of that batch with that noise
+    k = K - 1
+    o, d = batches[k].rays_o.cpu(), batches[k].rays_d.cpu()
+    c, h = torch.zeros(1, 3), torch.full((1, 3), 0.5)
+    _, ht, _ = oracle.ray_aabb_intersect(o, d, c, h, 1)
+    t1 = ht[:, 0, 0]
+    t1[(t1 >= 0) & (t1 < 0.01)] = 0.01
+    out = oracle.raymarching_train(o, d, ht[:, 0].contiguous(), a.bitfield.cpu(), a.cascades, 0.5, 0.0,
+                                   got[k]["noise"].cpu(), a.G, 1024)
+    rays_a_o, xyzs_o, n_o = out[0], out[1], int(out[5][0])
+    assert n_o == got[k]["n"]
+    assert torch.equal(got[k]["rays_a"].cpu(), rays_a_o)
+    assert torch.equal(got[k]["xyzs"].cpu(), xyzs_o[:n_o])

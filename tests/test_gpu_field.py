@@ -54,8 +54,46 @@ def test_grid_encode_fw_bw(gpu, name, args):
     tp = table.clone().requires_grad_(True)
     (FO.grid_encode(x, tp, olay) * dy).sum().backward()
     gref = tp.grad
+    xg, dyg = x.to(gpu), dy.to(gpu)
+    # with the private-copy workspace (the training path) and without
+    for ws in (FLD.grid_bw_workspace(desc, gpu), None):
+        gt = torch.zeros(lay.n_params, device=gpu)
+        FLD.grid_encode_bw(xg, N, dyg, gt, lay, desc, workspace=ws)
+        assert torch.allclose(gt.cpu(), gref, rtol=1e-4, atol=1e-4 * float(gref.abs().max()))
+        # accumulates (caller zeroes); the workspace is left zero for the next call
+        FLD.grid_encode_bw(xg, N, dyg, gt, lay, desc, workspace=ws)
+        assert torch.allclose(gt.cpu(), 2 * gref, rtol=1e-4, atol=2e-4 * float(gref.abs().max()))
+        if ws is not None:
+            assert int((ws != 0).sum()) == 0
+    m = 4099  # not a multiple of the 16-sample chunk: the live count comes from the device
+    tp = table.clone().requires_grad_(True)
+    (FO.grid_encode(x[:m], tp, olay) * dy[:m]).sum().backward()
+    n_dev = torch.tensor([m], dtype=torch.int32, device=gpu)
+    for ws in (FLD.grid_bw_workspace(desc, gpu), None):
+        gt = torch.zeros(lay.n_params, device=gpu)
+        FLD.grid_encode_bw(xg, N, dyg, gt, lay, desc, n_dev=n_dev, workspace=ws)
+        assert torch.allclose(gt.cpu(), tp.grad, rtol=1e-4, atol=1e-4 * float(tp.grad.abs().max()))
+
+
+def test_grid_encode_bw_along_rays(gpu):
+    """Training-shaped input: 64 consecutive samples per ray (long runs of equal coarse corners,
+    which the in-wave run merging collapses) at the Lego layout, with a zero-gradient stretch."""
+    lay = GridLayout(16, 2, 19, 16, LEGO_B)
+    olay = FO.GridLayout(16, 2, 19, 16, LEGO_B)
+    g = torch.Generator().manual_seed(5)
+    R, S = 700, 64
+    o = torch.rand(R, 1, 3, generator=g) * 0.5 + 0.25
+    d = torch.nn.functional.normalize(torch.randn(R, 1, 3, generator=g), dim=-1)
+    x = (o + d * (torch.arange(S).view(1, S, 1) * (3 ** 0.5 / 1024))).clamp(0, 1).reshape(-1, 3).contiguous()
+    N = x.shape[0]
+    dy = torch.randn(N, 32, generator=g) * 1e-3
+    dy[N // 3: N // 3 + 500] = 0.0  # terminated samples: zero gradient, nothing emitted
+    table = torch.zeros(lay.n_params).requires_grad_(True)
+    (FO.grid_encode(x, table, olay) * dy).sum().backward()
+    gref = table.grad
+    desc = lay.desc()
     gt = torch.zeros(lay.n_params, device=gpu)
-    FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc)
+    FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=FLD.grid_bw_workspace(desc, gpu))
     assert torch.allclose(gt.cpu(), gref, rtol=1e-4, atol=1e-4 * float(gref.abs().max()))
 
 
