@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of the HIP graphs")
+    ap.add_argument("--parts", type=int, default=1, help="ray-range parts per step (chain/scatter overlap)")
     return ap.parse_args()
 
 
@@ -144,7 +145,7 @@ def main():
 
     from mfnerf import dp, engine, synthetic
 
-    cfg = engine.StepConfig(n_rays=args.n_rays, log2_T=args.log2_T)
+    cfg = engine.StepConfig(n_rays=args.n_rays, log2_T=args.log2_T, n_parts=args.parts)
     step = engine.TrainStep(cfg, device=dev, seed=0)  # identical init on every rank
     step.set_occupancy(synthetic.ball_density_grid())
     batches = step.make_batches(8, seed=dp.rank_seed(100, rank))  # rank-distinct rays
@@ -181,7 +182,8 @@ def main():
         step.capture()
         for i in range(5):
             step.replay(batches[i % len(batches)], exchange=ex, next_batch=batches[(i + 1) % len(batches)])
-    gb_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    mk = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    gb_ev = [(mk(), [mk() for _ in range(step.n_parts)]) for _ in range(args.steps)]
     samples = torch.zeros(args.steps, dtype=torch.int32, device=dev)
     eager_ev = []
     if world > 1:
@@ -198,14 +200,16 @@ def main():
             ev = []
             run_step(step, batches[i % len(batches)], world, ev)
             eager_ev.append(ev)
-        samples[i:i + 1].copy_(step.state.counter[:1])
+        samples[i:i + 1].copy_(step.live_samples())
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.time() - t0
     elapsed = dp.max_over_ranks(elapsed, dev)  # the slowest rank's clock
     if use_graph:
-        grid_bw_ms = sum(a.elapsed_time(b) for a, b in gb_ev) / args.steps
+        # the parts' grid_bw scatters run back to back (part q+1's chain overlaps part q's): time
+        # from the first one's start to the last one's end
+        grid_bw_ms = sum(max(a.elapsed_time(b) for b in ends) for a, ends in gb_ev) / args.steps
     else:
         grid_bw_ms = stage_times(eager_ev, args.steps)["grid_bw"]
     mean_samples = float(samples.double().mean())

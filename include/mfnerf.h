@@ -121,10 +121,12 @@ int mfnerf_distortion_loss_bw(const float* dL_dloss, const float* ws_incl, const
 /* NeRFLoss (losses.py:47-60) + the background blend (rendering.py:153-161) and its gradient, fused:
  * pred = rgb + bg*(1-opacity); loss = mean((pred-target)^2) + lambda_opacity*mean(-o ln o),
  * o = opacity+1e-10 (train.py:178 sums the two means).  Writes dL_drgb (n,3), dL_dopacity (n);
- * loss_sum (optional, device f32) is ACCUMULATED with the loss value. */
-int mfnerf_nerf_loss(const float* rgb, const float* opacity, const float* target, int64_t n_rays, float lambda_opacity,
-                     float bg_r, float bg_g, float bg_b, float* dL_drgb, float* dL_dopacity, float* loss_sum,
-                     mfnerf_stream_t stream);
+ * loss_sum (optional, device f32) is ACCUMULATED with the loss value.  n_mean: the ray count the
+ * means are taken over (0 = n_rays); a batch computed in parts passes the full batch size so the
+ * parts' losses and gradients add up to the whole batch's. */
+int mfnerf_nerf_loss(const float* rgb, const float* opacity, const float* target, int64_t n_rays, int64_t n_mean,
+                     float lambda_opacity, float bg_r, float bg_g, float bg_b, float* dL_drgb, float* dL_dopacity,
+                     float* loss_sum, mfnerf_stream_t stream);
 
 /* ---------------------------------------------------------------- grid encoding (tcnn HashGrid / MF) */
 

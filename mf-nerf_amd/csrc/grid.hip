@@ -6,6 +6,8 @@
 // every lane keeps 32 independent 4-B corner gathers in flight.  Accumulation is fp32 (tcnn
 // accumulates in half; the difference is inside the fp16 output rounding).
 // Backward: see grid_bw_kernel (request-shaped float atomics with in-wave run merging).
+#include <cstdlib>
+
 #include "common.hpp"
 #include "../../include/mfnerf.h"
 
@@ -241,6 +243,17 @@ int64_t dense_entries_of(const mfnerf_grid_desc* d) {
     return e;
 }
 
+// grid_bw's workgroup count cap (grid-stride beyond it).  MFNERF_GRID_BW_BLOCKS overrides the
+// default for tuning experiments (tools/); read once.
+int64_t grid_bw_block_cap() {
+    static const int64_t cap = [] {
+        const char* e = getenv("MFNERF_GRID_BW_BLOCKS");
+        const long v = e ? atol(e) : 0;
+        return (int64_t)(v > 0 ? v : 4096);
+    }();
+    return cap;
+}
+
 int check_desc(const mfnerf_grid_desc* d, const char* what) {
     if (!d) { mfn_set_error("%s: null grid desc", what); return MFN_ERR_INVALID; }
     if (d->n_features != 2 || d->n_levels <= 0 || d->n_levels > MFN_MAX_LEVELS || d->n_levels % 4 != 0) {
@@ -288,7 +301,8 @@ int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float
     if (n == 0) return MFN_OK;
     if (!x || !dL_dout || !grad_table) { mfn_set_error("grid_encode_bw: null pointer"); return MFN_ERR_INVALID; }
     const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16), ENC_BLOCK / 64);
-    const int64_t blocks = want < 4096 ? want : 4096;
+    const int64_t cap = grid_bw_block_cap();
+    const int64_t blocks = want < cap ? want : cap;
     const int64_t dense = workspace ? dense_entries_of(desc) : 0;
     auto kern = desc->n_levels <= 16 ? grid_bw_kernel<0, 16> : grid_bw_kernel<0, MFN_MAX_LEVELS>;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0,

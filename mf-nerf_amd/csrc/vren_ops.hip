@@ -538,14 +538,15 @@ __global__ void distortion_bw_kernel(const float* __restrict__ dL_dloss, const f
 // pred = rgb + bg*(1-opacity) (rendering.py:153-161); loss = mean((pred-gt)^2) + lambda*mean(-o ln o),
 // o = opacity + 1e-10.  Writes dL/drgb, dL/dopacity of that scalar and accumulates it into loss_sum.
 __global__ void nerf_loss_kernel(const float* __restrict__ rgb, const float* __restrict__ opacity,
-                                 const float* __restrict__ gt, int64_t n_rays, float lambda_o, float bg0, float bg1,
+                                 const float* __restrict__ gt, int64_t n_rays, int64_t n_mean, float lambda_o,
+                                 float bg0, float bg1,
                                  float bg2, float* __restrict__ dL_drgb, float* __restrict__ dL_dop,
                                  float* __restrict__ loss_sum) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     float l = 0.0f;
     if (r < n_rays) {
         const float op = opacity[r];
-        const float inv3n = 1.0f / (3.0f * (float)n_rays), invn = 1.0f / (float)n_rays;
+        const float inv3n = 1.0f / (3.0f * (float)n_mean), invn = 1.0f / (float)n_mean;
         const float bg[3] = {bg0, bg1, bg2};
         float dop = 0.0f;
 #pragma unroll
@@ -749,14 +750,15 @@ int mfnerf_distortion_loss_bw(const float* dL_dloss, const float* ws_incl, const
     return mfn_check_launch("distortion_loss_bw");
 }
 
-int mfnerf_nerf_loss(const float* rgb, const float* opacity, const float* target, int64_t n_rays, float lambda_opacity,
-                     float bg_r, float bg_g, float bg_b, float* dL_drgb, float* dL_dopacity, float* loss_sum,
-                     mfnerf_stream_t stream) {
-    if (n_rays < 0) { mfn_set_error("nerf_loss: bad size"); return MFN_ERR_INVALID; }
+int mfnerf_nerf_loss(const float* rgb, const float* opacity, const float* target, int64_t n_rays, int64_t n_mean,
+                     float lambda_opacity, float bg_r, float bg_g, float bg_b, float* dL_drgb, float* dL_dopacity,
+                     float* loss_sum, mfnerf_stream_t stream) {
+    if (n_rays < 0 || n_mean < 0 || (n_mean > 0 && n_mean < n_rays)) { mfn_set_error("nerf_loss: bad size"); return MFN_ERR_INVALID; }
+    if (n_mean == 0) n_mean = n_rays;
     if (n_rays == 0) return MFN_OK;
     if (!rgb || !opacity || !target || !dL_drgb || !dL_dopacity) { mfn_set_error("nerf_loss: null pointer"); return MFN_ERR_INVALID; }
     hipLaunchKernelGGL(nerf_loss_kernel, dim3(blocks_for(n_rays, 256)), dim3(256), 0, stream, rgb, opacity, target,
-                       n_rays, lambda_opacity, bg_r, bg_g, bg_b, dL_drgb, dL_dopacity, loss_sum);
+                       n_rays, n_mean, lambda_opacity, bg_r, bg_g, bg_b, dL_drgb, dL_dopacity, loss_sum);
     return mfn_check_launch("nerf_loss");
 }
 

@@ -53,7 +53,7 @@ SIGNATURES = {
     "mfnerf_composite_test_fw": (_I, [_P, _P, _P, _P, _P, _I64, _I, _F, _P, _P, _P, _P, _P]),
     "mfnerf_distortion_loss_fw": (_I, [_P, _P, _P, _P, _I64, _I64, _P, _P, _P, _P]),
     "mfnerf_distortion_loss_bw": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P, _P]),
-    "mfnerf_nerf_loss": (_I, [_P, _P, _P, _I64, _F, _F, _F, _F, _P, _P, _P, _P]),
+    "mfnerf_nerf_loss": (_I, [_P, _P, _P, _I64, _I64, _F, _F, _F, _F, _P, _P, _P, _P]),
     "mfnerf_grid_encode_fw": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P]),
     "mfnerf_grid_encode_bw_workspace": (_I64, [ctypes.POINTER(GridDesc)]),
     "mfnerf_grid_encode_bw": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _P]),

@@ -1,15 +1,23 @@
 """The fused MI355X training step: one NeRF training iteration of the reference's hot path
 (train.py:164-190 -> rendering.py:121-163 -> losses.py:47-60 -> backward -> FusedAdam) as a
-fixed sequence of gfx950 kernels on one stream, with every intermediate resident in HBM and the
-sample count kept on the device (no host synchronisation, so a step is capturable in a HIP graph).
+fixed set of gfx950 kernels with every intermediate resident in HBM and the sample counts kept on
+the device (no host synchronisation, so a step is capturable in HIP graphs).
+
+Parts.  The batch's rays are split into `n_parts` equal, independent ray ranges ("parts"): each
+part is marched into its own sample buffers (own device counter, own rays_a) and runs its own
+encode -> field -> composite -> loss -> backward chain; the loss of every part is normalised by the
+FULL batch size (mfnerf_nerf_loss n_mean), so the parts' gradients add up to exactly the
+full batch's.  Parts exist so that the chain of part p+1 (MFMA/VALU work) runs on another stream
+while part p's table-gradient scatter (grid_bw, bound by memory-side atomics) keeps the memory
+system busy.  n_parts = 1 is the plain single-batch step.
 
 Buffers are sized once for the worst case (n_rays * MAX_SAMPLES samples, as the reference's
-raymarching_train does); kernels that run per sample read the live count from `counter[0]` and
-grid-stride over it.  Parameters live in one flat fp32 vector
+raymarching_train does); kernels that run per sample read the live count from their part's
+`counter[0]` and grid-stride over it.  Parameters live in one flat fp32 vector
     params = [xyz MLP (3072) | rgb MLP (7168) | grid table (L*F*entries)]
 so Adam is one launch and the gradient zeroing one memset; an fp16 mirror of the whole vector is
 refreshed by the same Adam pass and is what the grid kernels gather from.
-Multi-GPU: run(exchange=dp.allreduce_mean_) all-reduces `grads` between the backward and Adam.
+Multi-GPU: run/replay(exchange=dp.allreduce_mean_) all-reduces `grads` between backward and Adam.
 """
 import math
 from dataclasses import dataclass
@@ -44,6 +52,7 @@ class StepConfig:
     lambda_opacity: float = 1e-3
     T_threshold: float = 1e-4
     max_samples: int = MAX_SAMPLES
+    n_parts: int = 1
 
 
 @dataclass
@@ -70,6 +79,8 @@ class TrainStep:
         self.dev = torch.device(device)
         load()
         c = cfg
+        if c.n_parts < 1 or c.n_rays % c.n_parts:
+            raise ValueError(f"n_rays={c.n_rays} must split into n_parts={c.n_parts} equal parts")
         self.cascades = max(1 + int(np.ceil(np.log2(2 * c.scale))), 1)
         self.G = 128
         b = float(np.exp(np.log(c.N_max * c.scale / c.N_min) / (c.L - 1)))
@@ -110,42 +121,52 @@ class TrainStep:
         self.density_grid = torch.zeros(self.cascades, self.G ** 3, device=dev)
         self.bitfield = torch.zeros(self.cascades * self.G ** 3 // 8, dtype=torch.uint8, device=dev)
 
-        N, cap = c.n_rays, c.n_rays * c.max_samples
-        self.cap = cap
-        st = _State()
-        self.state = st
-        f32 = dict(dtype=torch.float32, device=dev)
+        N = c.n_rays
+        self.n_parts = c.n_parts
+        self.Np = N // c.n_parts                      # rays per part
+        self.cap_p = self.Np * c.max_samples          # sample capacity per part
+        self.cap = N * c.max_samples
+        self.parts = [self._part_buffers(q) for q in range(c.n_parts)]
         self.mbuf = [self._march_buffers()]  # a second set is added by capture() (pipelined march)
+        self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.state = _State()
         self._use(self.mbuf[0])
-        st.feat = torch.empty(cap, c.L * c.F, dtype=torch.float16, device=dev)
-        st.sigma = torch.empty(cap, **f32)
-        st.rgb_s = torch.empty(cap, 3, **f32)
-        st.total = torch.empty(N, dtype=torch.int64, device=dev)
-        st.opacity = torch.empty(N, **f32)
-        st.depth = torch.empty(N, **f32)
-        st.rgb = torch.empty(N, 3, **f32)
-        st.ws = torch.empty(cap, **f32)
-        st.dL_drgb = torch.empty(N, 3, **f32)
-        st.dL_dop = torch.empty(N, **f32)
-        st.zeros_ray = torch.zeros(N, **f32)       # dL/ddepth (unused by the loss)
-        st.zeros_samp = torch.zeros(cap, **f32)    # dL/dws (no distortion loss by default)
-        st.dsig = torch.empty(cap, **f32)
-        st.drgb_s = torch.empty(cap, 3, **f32)
-        st.dfeat = torch.empty(cap, c.L * c.F, **f32)
-        st.field_ws = torch.empty(load().mfnerf_field_bw_workspace(cap, c.rgb_width) // 4, **f32)
-        st.loss_sum = torch.zeros(1, **f32)
-        st.grid_ws = torch.zeros(max(16, load().mfnerf_grid_encode_bw_workspace(self.desc)) // 4, **f32)
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(seed + 1)
         # fp16 backward scale: per-sample grads are O(1/n_rays); 2^(floor(log2 N)-2) keeps them normal
         self.grad_scale = float(2.0 ** max(0, int(math.floor(math.log2(N))) - 2))
+        self._primed = False
 
-    MARCH_FIELDS = ("hit_cnt", "hits", "hits_t", "hits_idx", "noise", "rays_a", "xyzs", "dirs", "deltas", "ts",
-                    "counter", "march_ws")
+    # ---------------------------------------------------------------- buffers
+    def _part_buffers(self, q):
+        """Per-part sample/ray state of the chain (features, field outputs, compositing, grads)."""
+        c, dev, Np, cap = self.cfg, self.dev, self.Np, self.cap_p
+        f32 = dict(dtype=torch.float32, device=dev)
+        t = _State()
+        t.feat = torch.empty(cap, c.L * c.F, dtype=torch.float16, device=dev)
+        t.sigma = torch.empty(cap, **f32)
+        t.rgb_s = torch.empty(cap, 3, **f32)
+        t.total = torch.empty(Np, dtype=torch.int64, device=dev)
+        t.opacity = torch.empty(Np, **f32)
+        t.depth = torch.empty(Np, **f32)
+        t.rgb = torch.empty(Np, 3, **f32)
+        t.ws = torch.empty(cap, **f32)
+        t.dL_drgb = torch.empty(Np, 3, **f32)
+        t.dL_dop = torch.empty(Np, **f32)
+        t.zeros_ray = torch.zeros(Np, **f32)       # dL/ddepth (unused by the loss)
+        t.zeros_samp = torch.zeros(cap, **f32)     # dL/dws (no distortion loss by default)
+        t.dsig = torch.empty(cap, **f32)
+        t.drgb_s = torch.empty(cap, 3, **f32)
+        t.dfeat = torch.empty(cap, c.L * c.F, **f32)
+        t.field_ws = torch.empty(load().mfnerf_field_bw_workspace(cap, c.rgb_width) // 4, **f32)
+        t.grid_ws = torch.zeros(max(16, load().mfnerf_grid_encode_bw_workspace(self.desc)) // 4, **f32)
+        # parts > 0 accumulate their MLP weight grads privately (field_bw's slab sum is a plain +=)
+        t.mlp_grad = self.grads[:self.off_table] if q == 0 else torch.zeros(self.off_table, **f32)
+        return t
 
     def _march_buffers(self):
-        """One set of ray-march outputs (and their scratch), sized for n_rays * MAX_SAMPLES."""
-        N, cap, dev = self.cfg.n_rays, self.cap, self.dev
+        """One set of ray-march outputs: AABB hits and noise for the whole batch, samples per part."""
+        c, N, dev = self.cfg, self.cfg.n_rays, self.dev
         f32 = dict(dtype=torch.float32, device=dev)
         m = _State()
         m.hit_cnt = torch.empty(N, dtype=torch.int32, device=dev)
@@ -153,20 +174,46 @@ class TrainStep:
         m.hits_t = m.hits[:, 0]
         m.hits_idx = torch.empty(N, 1, dtype=torch.int64, device=dev)
         m.noise = torch.empty(N, **f32)
-        m.rays_a = torch.empty(N, 3, dtype=torch.int64, device=dev)
-        m.xyzs = torch.empty(cap, 3, **f32)
-        m.dirs = torch.empty(cap, 3, **f32)
-        m.deltas = torch.empty(cap, **f32)
-        m.ts = torch.empty(cap, **f32)
-        m.counter = torch.zeros(2, dtype=torch.int32, device=dev)
-        m.march_ws = torch.empty(max(16, load().mfnerf_raymarching_train_workspace(N)), dtype=torch.uint8, device=dev)
+        m.counters = torch.zeros(c.n_parts, 2, dtype=torch.int32, device=dev)  # per part (samples, rays)
+        m.part = []
+        for q in range(c.n_parts):
+            t = _State()
+            t.rays_a = torch.empty(self.Np, 3, dtype=torch.int64, device=dev)
+            t.xyzs = torch.empty(self.cap_p, 3, **f32)
+            t.dirs = torch.empty(self.cap_p, 3, **f32)
+            t.deltas = torch.empty(self.cap_p, **f32)
+            t.ts = torch.empty(self.cap_p, **f32)
+            t.counter = m.counters[q]
+            t.march_ws = torch.empty(max(16, load().mfnerf_raymarching_train_workspace(self.Np)), dtype=torch.uint8,
+                                     device=dev)
+            m.part.append(t)
         return m
 
     def _use(self, mb):
-        """Point state.<march field> at the buffer set of the step being run (for callers that
-        inspect state.rays_a / state.counter / ... after a step)."""
-        for k in self.MARCH_FIELDS:
-            setattr(self.state, k, getattr(mb, k))
+        """state.noise / state.counters / state.loss_sum of the step being run (inspection)."""
+        st = self.state
+        st.noise, st.counters, st.loss_sum, st.march = mb.noise, mb.counters, self.loss_sum, mb
+        st.parts = self.parts
+
+    def live_samples(self):
+        """Device scalar: samples marched by the current step (sum over parts)."""
+        return self.state.counters[:, 0].sum()
+
+    def gather_march(self):
+        """(rays_a (N,3) i64 with global starts, xyzs (n,3), dirs, deltas, ts) of the current step,
+        concatenated over parts in ray order -- host-synchronising, for tests and smoke()."""
+        mb = self.state.march
+        ra, xs, ds, dl, ts = [], [], [], [], []
+        base = 0
+        for q, t in enumerate(mb.part):
+            n = int(mb.counters[q, 0])
+            r = t.rays_a.clone()
+            r[:, 0] += q * self.Np
+            r[:, 1] += base
+            ra.append(r)
+            xs.append(t.xyzs[:n]); ds.append(t.dirs[:n]); dl.append(t.deltas[:n]); ts.append(t.ts[:n])
+            base += n
+        return torch.cat(ra), torch.cat(xs), torch.cat(ds), torch.cat(dl), torch.cat(ts)
 
     # ---------------------------------------------------------------- data
     def make_batches(self, k, seed=0):
@@ -193,9 +240,9 @@ class TrainStep:
 
     # ---------------------------------------------------------------- the step
     def _march(self, batch: Batch, mb, mark):
-        """Segment 0: AABB + near clamp + noise + ray march into the buffer set mb."""
+        """AABB + near clamp + noise for the whole batch, then one ray march per part into mb."""
         c, s = self.cfg, stream()
-        N, cap = c.n_rays, self.cap
+        N, Np = c.n_rays, self.Np
         # rendering.py:27-29 (AABB + near clamp), custom_functions.py:83 (noise)
         call("mfnerf_ray_aabb_intersect", ptr(batch.rays_o), ptr(batch.rays_d), ptr(self.center),
              ptr(self.half_size), N, 1, 1, ptr(mb.hit_cnt), ptr(mb.hits), ptr(mb.hits_idx), s)
@@ -203,63 +250,78 @@ class TrainStep:
         t1.masked_fill_((t1 >= 0) & (t1 < NEAR_DISTANCE), NEAR_DISTANCE)
         torch.rand(N, generator=self.gen, device=self.dev, out=mb.noise)
         mark("prep")
-        call("mfnerf_raymarching_train", ptr(batch.rays_o), ptr(batch.rays_d), ptr(mb.hits_t), 2, ptr(self.bitfield),
-             self.cascades, float(c.scale), 0.0 if c.scale <= 0.5 else 1 / 256, ptr(mb.noise), self.G,
-             c.max_samples, N, cap, ptr(mb.rays_a), ptr(mb.xyzs), ptr(mb.dirs), ptr(mb.deltas), ptr(mb.ts),
-             ptr(mb.counter), ptr(mb.march_ws), s)
+        for q, t in enumerate(mb.part):
+            r = slice(q * Np, (q + 1) * Np)
+            call("mfnerf_raymarching_train", ptr(batch.rays_o[r]), ptr(batch.rays_d[r]), ptr(mb.hits_t[r]), 2,
+                 ptr(self.bitfield), self.cascades, float(c.scale), 0.0 if c.scale <= 0.5 else 1 / 256,
+                 ptr(mb.noise[r]), self.G, c.max_samples, Np, self.cap_p, ptr(t.rays_a), ptr(t.xyzs), ptr(t.dirs),
+                 ptr(t.deltas), ptr(t.ts), ptr(t.counter), ptr(t.march_ws), s)
         mark("march")
 
-    def _fwbw(self, batch: Batch, mb, mark):
-        """Segment 1: encode -> field -> composite -> loss -> composite bw -> field bw on mb's samples."""
-        c, st, s = self.cfg, self.state, stream()
-        N, cap = c.n_rays, self.cap
-        call("mfnerf_grid_encode_fw", ptr(mb.xyzs), cap, ptr(mb.counter), self.x_min, self.x_range, self.desc,
-             ptr(self.p16[self.off_table:]), ptr(st.feat), s)
+    def _chain(self, batch: Batch, mb, q, mark):
+        """Part q: encode -> field -> composite -> loss -> composite bw -> field bw (no grid bw).
+        Part 0 also zeroes the gradient (every part's writes come after it)."""
+        c, s = self.cfg, stream()
+        t, m = self.parts[q], mb.part[q]
+        Np, cap = self.Np, self.cap_p
+        if q == 0:
+            self.grads.zero_()
+            self.loss_sum.zero_()
+        else:
+            t.mlp_grad.zero_()
+        call("mfnerf_grid_encode_fw", ptr(m.xyzs), cap, ptr(m.counter), self.x_min, self.x_range, self.desc,
+             ptr(self.p16[self.off_table:]), ptr(t.feat), s)
         mark("grid_fw")
-        call("mfnerf_field_fw", ptr(st.feat), ptr(mb.dirs), cap, ptr(mb.counter), ptr(self.packed), c.rgb_width, 0,
-             ptr(st.sigma), ptr(st.rgb_s), s)
+        call("mfnerf_field_fw", ptr(t.feat), ptr(m.dirs), cap, ptr(m.counter), ptr(self.packed), c.rgb_width, 0,
+             ptr(t.sigma), ptr(t.rgb_s), s)
         mark("field_fw")
-        call("mfnerf_composite_train_fw", ptr(st.sigma), ptr(st.rgb_s), ptr(mb.deltas), ptr(mb.ts), ptr(mb.rays_a),
-             N, cap, c.T_threshold, ptr(st.total), ptr(st.opacity), ptr(st.depth), ptr(st.rgb), ptr(st.ws), s)
+        call("mfnerf_composite_train_fw", ptr(t.sigma), ptr(t.rgb_s), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a),
+             Np, cap, c.T_threshold, ptr(t.total), ptr(t.opacity), ptr(t.depth), ptr(t.rgb), ptr(t.ws), s)
         bg = 1.0 if c.scale <= 0.5 else 0.0
-        st.loss_sum.zero_()
-        call("mfnerf_nerf_loss", ptr(st.rgb), ptr(st.opacity), ptr(batch.rgb), N, c.lambda_opacity, bg, bg, bg,
-             ptr(st.dL_drgb), ptr(st.dL_dop), ptr(st.loss_sum), s)
+        call("mfnerf_nerf_loss", ptr(t.rgb), ptr(t.opacity), ptr(batch.rgb[q * Np:(q + 1) * Np]), Np, c.n_rays,
+             c.lambda_opacity, bg, bg, bg, ptr(t.dL_drgb), ptr(t.dL_dop), ptr(self.loss_sum), s)
         mark("composite_fw")
-        call("mfnerf_composite_train_bw", ptr(st.dL_dop), ptr(st.zeros_ray), ptr(st.dL_drgb), ptr(st.zeros_samp),
-             ptr(st.sigma), ptr(st.rgb_s), ptr(st.ws), ptr(mb.deltas), ptr(mb.ts), ptr(mb.rays_a), ptr(st.opacity),
-             ptr(st.depth), ptr(st.rgb), N, cap, c.T_threshold, ptr(st.dsig), ptr(st.drgb_s), s)
+        call("mfnerf_composite_train_bw", ptr(t.dL_dop), ptr(t.zeros_ray), ptr(t.dL_drgb), ptr(t.zeros_samp),
+             ptr(t.sigma), ptr(t.rgb_s), ptr(t.ws), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a), ptr(t.opacity),
+             ptr(t.depth), ptr(t.rgb), Np, cap, c.T_threshold, ptr(t.dsig), ptr(t.drgb_s), s)
         mark("composite_bw")
-        self.grads.zero_()
-        call("mfnerf_field_bw", ptr(st.feat), ptr(mb.dirs), cap, ptr(mb.counter), ptr(self.packed), c.rgb_width,
-             ptr(st.dsig), ptr(st.drgb_s), self.grad_scale, ptr(st.dfeat), ptr(self.grads),
-             ptr(self.grads[self.off_rgb:]), ptr(st.field_ws), s)
+        call("mfnerf_field_bw", ptr(t.feat), ptr(m.dirs), cap, ptr(m.counter), ptr(self.packed), c.rgb_width,
+             ptr(t.dsig), ptr(t.drgb_s), self.grad_scale, ptr(t.dfeat), ptr(t.mlp_grad),
+             ptr(t.mlp_grad[self.off_rgb:]), ptr(t.field_ws), s)
         mark("field_bw")
 
-    def _grid_bw(self, mb):
-        """Segment 2: the hash-table gradient scatter (the dominant kernel)."""
-        st = self.state
-        call("mfnerf_grid_encode_bw", ptr(mb.xyzs), self.cap, ptr(mb.counter), self.x_min, self.x_range, self.desc,
-             ptr(st.dfeat), ptr(self.grads[self.off_table:]), ptr(st.grid_ws), stream())
+    def _grid_bw(self, mb, q):
+        """Part q's hash-table gradient scatter (the dominant kernel)."""
+        t, m = self.parts[q], mb.part[q]
+        call("mfnerf_grid_encode_bw", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min, self.x_range, self.desc,
+             ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws), stream())
+
+    def _reduce_parts(self):
+        """Fold parts 1.. MLP weight grads into grads (the table part is already shared)."""
+        for t in self.parts[1:]:
+            self.grads[:self.off_table].add_(t.mlp_grad)
 
     def _update(self):
-        """Segment 3: Adam over the flat params (+ fp16 mirror) and the MLP weight repack."""
+        """Adam over the flat params (+ fp16 mirror) and the MLP weight repack."""
         c = self.cfg
         call("mfnerf_adam_step", ptr(self.params), ptr(self.grads), ptr(self.m), ptr(self.v), ptr(self.p16),
              self.n_params, float(c.lr), 0.9, 0.999, c.eps, 1.0, 0, ptr(self.step_dev), ptr(self.lr_dev), stream())
         self._pack()
 
     def run(self, batch: Batch, mark=None, exchange=None):
-        """One training step, eagerly, in buffer set 0.  mark(name) is called after each stage
-        (bench timing); exchange(grads) runs between backward and Adam (the data-parallel all-reduce)."""
+        """One training step, eagerly on the current stream, parts in sequence, march buffer set 0.
+        mark(name) is called after each stage (bench timing); exchange(grads) runs between backward
+        and Adam (the data-parallel all-reduce)."""
         mark = mark or (lambda name: None)
         mb = self.mbuf[0]
         self._use(mb)
         self._primed = False  # a pipelined replay() must march its own batch next
         self._march(batch, mb, mark)
-        self._fwbw(batch, mb, mark)
-        self._grid_bw(mb)
-        mark("grid_bw")
+        for q in range(self.n_parts):
+            self._chain(batch, mb, q, mark)
+            self._grid_bw(mb, q)
+            mark("grid_bw")
+        self._reduce_parts()
         if exchange is not None:
             exchange(self.grads)
         mark("allreduce")
@@ -281,13 +343,14 @@ class TrainStep:
 
     # ---------------------------------------------------------------- HIP graphs
     def capture(self):
-        """Capture the step as HIP graphs over two alternating buffer sets j = 0, 1:
-        march[j] (AABB + noise + march of static batch j), fwbw[j], grid_bw[j], and update (Adam +
-        repack).  replay() runs march[j'] of the NEXT step on a side stream while grid_bw[j] of this
-        one runs on the main stream (the march needs neither this step's gradients nor its update;
-        grid_bw is bound by memory-side atomics and leaves the CUs mostly idle).  The split at
-        grid_bw also lets the caller time it with events and run the data-parallel all-reduce
-        between graphs.  Call after at least one eager step (lazy library init outside capture)."""
+        """Capture the step as HIP graphs over two alternating march buffer sets j = 0, 1:
+        march[j] (AABB + noise + per-part march of static batch j), chain[j][q] and grid_bw[j][q]
+        per part, reduce (parts' MLP grads) and update (Adam + repack).  replay() orchestrates them
+        on streams: part q's chain+grid_bw on stream q, the chain of part q+1 starting when part q's
+        chain ends (so it overlaps part q's grid_bw), and the NEXT step's march on a side stream
+        (it needs neither this step's gradients nor its update).  Splitting at grid_bw also lets the
+        caller time it and run the data-parallel all-reduce between graphs.  Call after at least one
+        eager step (lazy library init happens outside capture)."""
         N = self.cfg.n_rays
         if len(self.mbuf) == 1:
             self.mbuf.append(self._march_buffers())
@@ -304,16 +367,22 @@ class TrainStep:
                 fn()
             return g
 
+        P = self.n_parts
         self.graphs = {
             "march": [cap(lambda j=j: self._march(self._static[j], self.mbuf[j], nomark), rng=True) for j in range(2)],
-            "fwbw": [cap(lambda j=j: self._fwbw(self._static[j], self.mbuf[j], nomark)) for j in range(2)],
-            "grid_bw": [cap(lambda j=j: self._grid_bw(self.mbuf[j])) for j in range(2)],
+            "chain": [[cap(lambda j=j, q=q: self._chain(self._static[j], self.mbuf[j], q, nomark)) for q in range(P)]
+                      for j in range(2)],
+            "grid_bw": [[cap(lambda j=j, q=q: self._grid_bw(self.mbuf[j], q)) for q in range(P)] for j in range(2)],
+            "reduce": cap(self._reduce_parts) if P > 1 else None,
             "update": cap(self._update),
         }
         torch.cuda.synchronize()
         self._side = torch.cuda.Stream(device=self.dev)
+        self._part_streams = [None] + [torch.cuda.Stream(device=self.dev) for _ in range(P - 1)]
         self._ev_march = [torch.cuda.Event(), torch.cuda.Event()]
-        self._ev_fwbw = torch.cuda.Event()
+        self._ev_start = torch.cuda.Event()
+        self._ev_chain = [torch.cuda.Event() for _ in range(P)]
+        self._ev_part = [torch.cuda.Event() for _ in range(P)]
         self._parity = 0
         self._primed = False
 
@@ -325,36 +394,48 @@ class TrainStep:
             for d, s_ in zip((dst.rays_o, dst.rays_d, dst.rgb), (batch.rays_o, batch.rays_d, batch.rgb)):
                 d.copy_(s_)
 
-    def _march_on_side(self, j, batch):
-        """Copy batch into static set j and march it on the side stream (after the main stream's
-        work so far: set j's buffers were last read by the grid_bw two steps back)."""
-        main = torch.cuda.current_stream()
-        self._ev_fwbw.record(main)
-        self._side.wait_event(self._ev_fwbw)
+    def _march_on_side(self, j, batch, after):
+        """Copy batch into static set j and march it on the side stream once `after` (an event on
+        the main stream) has passed: set j's buffers were last read two steps back."""
+        self._side.wait_event(after)
         with torch.cuda.stream(self._side):
             self._stage_batch(j, batch)
             self.graphs["march"][j].replay()
             self._ev_march[j].record(self._side)
 
     def replay(self, batch: Batch, exchange=None, grid_bw_events=None, next_batch=None):
-        """One training step from the captured graphs (same kernels as run()).  With next_batch, the
-        next step's march is issued on the side stream to overlap this step's grid_bw; the next
-        replay() must then be called with that batch.  grid_bw_events: optional (start, end) timing
-        events recorded around the grid_bw graph."""
-        g, j = self.graphs, self._parity
+        """One training step from the captured graphs (the kernels of run()).  With next_batch, the
+        next step's march is issued on the side stream to overlap this step; the next replay() must
+        then be called with that batch.  grid_bw_events: optional (start, [end per part]) timing
+        events -- start before part 0's grid_bw, end after each part's grid_bw."""
+        g, j, P = self.graphs, self._parity, self.n_parts
         main = torch.cuda.current_stream()
+        self._ev_start.record(main)
         if not self._primed:
-            self._march_on_side(j, batch)
+            self._march_on_side(j, batch, self._ev_start)
         main.wait_event(self._ev_march[j])
         self._use(self.mbuf[j])
-        g["fwbw"][j].replay()
-        if next_batch is not None:
-            self._march_on_side(1 - j, next_batch)
-        if grid_bw_events is not None:
-            grid_bw_events[0].record(main)
-        g["grid_bw"][j].replay()
-        if grid_bw_events is not None:
-            grid_bw_events[1].record(main)
+        for q in range(P):
+            sq = main if q == 0 else self._part_streams[q]
+            if q > 0:
+                sq.wait_event(self._ev_chain[q - 1])
+            with torch.cuda.stream(sq):
+                g["chain"][j][q].replay()
+                self._ev_chain[q].record(sq)
+                if q == P - 1 and next_batch is not None:
+                    # set 1-j was last read by the previous step, which this chain follows; waiting
+                    # for the last chain puts the march under the grid_bw scatters, not the chains
+                    self._march_on_side(1 - j, next_batch, self._ev_chain[q])
+                if grid_bw_events is not None and q == 0:
+                    grid_bw_events[0].record(sq)
+                g["grid_bw"][j][q].replay()
+                if grid_bw_events is not None:
+                    grid_bw_events[1][q].record(sq)
+                self._ev_part[q].record(sq)
+        for q in range(1, P):
+            main.wait_event(self._ev_part[q])
+        if g["reduce"] is not None:
+            g["reduce"].replay()
         if exchange is not None:
             exchange(self.grads)
         self.adam_step += 1

@@ -11,22 +11,22 @@ from mfnerf import engine, synthetic
 pytestmark = pytest.mark.gpu
 
 
-def _make(gpu):
-    st = engine.TrainStep(engine.StepConfig(n_rays=1024, log2_T=16), device=gpu, seed=0)
+def _make(gpu, parts=2):
+    st = engine.TrainStep(engine.StepConfig(n_rays=1024, log2_T=16, n_parts=parts), device=gpu, seed=0)
     st.set_occupancy(synthetic.ball_density_grid())
     return st
 
 
 def _record(st):
-    s = st.state
-    n = int(s.counter[0])
-    return {"noise": s.noise.clone(), "n": n, "rays_a": s.rays_a.clone(), "xyzs": s.xyzs[:n].clone(),
-            "loss": float(s.loss_sum)}
+    rays_a, xyzs = st.gather_march()[:2]
+    return {"noise": st.state.noise.clone(), "n": xyzs.shape[0], "rays_a": rays_a, "xyzs": xyzs,
+            "loss": float(st.loss_sum)}
 
 
-def test_pipelined_replay_matches_eager(gpu, oracle):
+@pytest.mark.parametrize("parts", [1, 2, 4])
+def test_pipelined_replay_matches_eager(gpu, oracle, parts):
     K = 6
-    a, b = _make(gpu), _make(gpu)
+    a, b = _make(gpu, parts), _make(gpu, parts)
     batches = a.make_batches(K + 1, seed=3)
     # eager reference
     ref = []
@@ -52,7 +52,7 @@ def test_pipelined_replay_matches_eager(gpu, oracle):
     k = K - 1
     o, d = batches[k].rays_o.cpu(), batches[k].rays_d.cpu()
     c, h = torch.zeros(1, 3), torch.full((1, 3), 0.5)
-    _, ht, _ = oracle.ray_aabb_intersect(o, d, c, h, 1)
+    _, ht, _ = oracle.ray_aabb_intersect(o, d, c, h, 1)  # rays of all parts, one march
     t1 = ht[:, 0, 0]
     t1[(t1 >= 0) & (t1 < 0.01)] = 0.01
     out = oracle.raymarching_train(o, d, ht[:, 0].contiguous(), a.bitfield.cpu(), a.cascades, 0.5, 0.0,
@@ -61,3 +61,20 @@ def test_pipelined_replay_matches_eager(gpu, oracle):
     assert n_o == got[k]["n"]
     assert torch.equal(got[k]["rays_a"].cpu(), rays_a_o)
     assert torch.equal(got[k]["xyzs"].cpu(), xyzs_o[:n_o])
+
+
+def test_parts_sum_to_the_whole_batch(gpu):
+    """n_parts only changes the schedule: the loss and the gradient of one eager step are the same
+    for 1, 2 and 4 parts (up to float summation order)."""
+    out = []
+    for parts in (1, 2, 4):
+        st = _make(gpu, parts)
+        batch = st.make_batches(1, seed=9)[0]
+        st.run(batch)
+        torch.cuda.synchronize()
+        out.append((float(st.loss_sum), st.grads.clone(), st.gather_march()[0]))
+    for loss, g, ra in out[1:]:
+        assert torch.equal(ra, out[0][2])
+        assert abs(loss - out[0][0]) <= 1e-5 * abs(out[0][0])
+        tol = 1e-4 * float(out[0][1].abs().max())
+        assert torch.allclose(g, out[0][1], rtol=1e-3, atol=tol)
