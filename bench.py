@@ -66,6 +66,21 @@ def run_step(step, batch, world, ev=None):
     step.run(batch, mark=mark, exchange=dp.allreduce_mean_ if world > 1 else None)
 
 
+def pmc_traffic(kernel_prefix):
+    """HBM-side bytes per launch of a kernel from the newest committed PMC summary
+    (profiles/rNN_pmc_traffic.json, made by tools/pmc_traffic.py from separate FETCH_SIZE /
+    WRITE_SIZE rocprofv3 passes with the guide's gfx950 corrections); (None, None) if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    for k, v in d["kernels"].items():
+        if k.startswith(kernel_prefix):
+            return round(v["traffic_bytes"]), os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def stage_times(events, steps):
     out = {}
     for ev in events:
@@ -218,6 +233,7 @@ def main():
 
     # roofline: grid_bw (the dominant kernel), timed by events around it inside the timed region
     dom = "grid_bw"
+    traffic, traffic_src = pmc_traffic("grid_bw_kernel")
     dom_bytes = BYTES_PER_SAMPLE[dom] * mean_samples
     achieved = dom_bytes / (grid_bw_ms * 1e-3) / 1e9
     if rank == 0:
@@ -234,7 +250,8 @@ def main():
                        % args.log2_T, "global_batch": args.n_rays * world, "rm_s": round(mean_samples / args.n_rays, 2),
                        "parallelism": f"dp{world}", "psnr": None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "bytes_per_launch": round(dom_bytes)},
             "graph": use_graph,
             "grid_bw_ms": round(grid_bw_ms, 4),
