@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of the HIP graphs")
     ap.add_argument("--parts", type=int, default=1, help="ray-range parts per step (chain/scatter overlap)")
+    ap.add_argument("--dp", choices=("shard", "allreduce"), default="shard",
+                    help="N>1: sharded optimizer (reduce-scatter + all-gather fp16) or all-reduce + full Adam")
     return ap.parse_args()
 
 
@@ -162,6 +164,8 @@ def main():
 
     cfg = engine.StepConfig(n_rays=args.n_rays, log2_T=args.log2_T, n_parts=args.parts)
     step = engine.TrainStep(cfg, device=dev, seed=0)  # identical init on every rank
+    if world > 1 and args.dp == "shard":
+        step.shard_optimizer(rank, world)
     step.set_occupancy(synthetic.ball_density_grid())
     batches = step.make_batches(8, seed=dp.rank_seed(100, rank))  # rank-distinct rays
 
@@ -248,7 +252,8 @@ def main():
             "data": "synthetic (seeded Lego-like rays + ball-union occupancy; no dataset in the image)",
             "config": {"workload": "Lego 800x800 training step, 8192 rays/batch/GPU, Hash L16 F2 T2^%d, rgb 64x2"
                        % args.log2_T, "global_batch": args.n_rays * world, "rm_s": round(mean_samples / args.n_rays, 2),
-                       "parallelism": f"dp{world}", "psnr": None},
+                       "parallelism": f"dp{world}" + ("-sharded-adam" if world > 1 and args.dp == "shard" else ""),
+                       "psnr": None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,

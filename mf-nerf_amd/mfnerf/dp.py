@@ -1,9 +1,15 @@
-"""Data parallelism of the training step: every rank holds a full replica (table,
-MLPs, occupancy), marches its OWN rays (rank-distinct seeds -- the reference's DDP ranks draw
-identical batches, base.py:22-33 + seed_everything), and the only exchange per step is ONE
-all-reduce (mean) of the flat fp32 gradient vector between backward and Adam.  There is no
-per-step buffer broadcast (DDP's broadcast_buffers moved ~40 MiB/step in the reference); the
-occupancy grid is refreshed identically on every rank from identical parameters.
+"""Data parallelism of the training step: every rank holds the fp16 compute copy
+of the whole model (table, MLPs) and the occupancy grid, marches its OWN rays (rank-distinct seeds
+-- the reference's DDP ranks draw identical batches, base.py:22-33 + seed_everything), and
+exchanges per step either
+  * ONE all-reduce (mean) of the flat fp32 gradient, then the full Adam on every rank
+    (allreduce_mean_), or
+  * (default for world > 1, TrainStep.shard_optimizer) a reduce-scatter (mean) of the gradient,
+    Adam on this rank's 1/world shard of the fp32 master/m/v only, and an all-gather of the fp16
+    compute copy (sharded_update): 1.5 instead of 2 gradient-sized transfers per rank and 1/world
+    of the optimizer's HBM traffic; the fp32 master copy stays sharded.
+There is no per-step buffer broadcast (DDP's broadcast_buffers moved ~40 MiB/step in the
+reference); the occupancy grid is refreshed identically on every rank from identical parameters.
 Backend "nccl" is RCCL over xGMI on MI355X; "gloo" is used for the CPU tests.
 """
 import torch
@@ -15,6 +21,17 @@ def rank_seed(base, rank):
     return int(base) + 1000 * int(rank)
 
 
+def _host_staged(fn, *ts):
+    """gloo has no GPU collectives: run fn on host copies of CUDA tensors and copy results back
+    (CPU tests and single-GPU rehearsals only; RCCL takes device tensors directly)."""
+    if dist.get_backend() == "nccl" or not any(t.is_cuda for t in ts):
+        return fn(*ts)
+    hs = [t.cpu() for t in ts]
+    fn(*hs)
+    for t, h in zip(ts, hs):
+        t.copy_(h)
+
+
 def allreduce_mean_(flat):
     """In-place mean over ranks of one flat gradient tensor (one collective per step)."""
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size() == 1:
@@ -22,9 +39,51 @@ def allreduce_mean_(flat):
     if dist.get_backend() == "nccl":
         dist.all_reduce(flat, op=dist.ReduceOp.AVG)
     else:
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
-        flat.div_(dist.get_world_size())
+        def f(x):
+            dist.all_reduce(x, op=dist.ReduceOp.SUM)
+            x.div_(dist.get_world_size())
+        _host_staged(f, flat)
     return flat
+
+
+def _world():
+    if not dist.is_available() or not dist.is_initialized():
+        return 1
+    return dist.get_world_size()
+
+
+def reduce_scatter_mean_(shard, flat):
+    """shard (flat.numel()/world,) <- this rank's slice of the mean over ranks of flat."""
+    if _world() == 1:
+        shard.copy_(flat)
+        return shard
+    if dist.get_backend() == "nccl":
+        dist.reduce_scatter_tensor(shard, flat, op=dist.ReduceOp.AVG)
+    else:
+        def f(s_, x):
+            dist.reduce_scatter_tensor(s_, x, op=dist.ReduceOp.SUM)
+            s_.div_(dist.get_world_size())
+        _host_staged(f, shard, flat)
+    return shard
+
+
+def all_gather_(full, rank):
+    """full = concat over ranks of each rank's slice full[rank*k:(rank+1)*k] (in place)."""
+    w = _world()
+    if w == 1:
+        return full
+    k = full.numel() // w
+    _host_staged(lambda x: dist.all_gather_into_tensor(x, x[rank * k:(rank + 1) * k].clone()), full)
+    return full
+
+
+def sharded_update(grads, g_shard, p16, rank, adam_shard):
+    """One ZeRO-1 optimizer step: reduce-scatter(mean) grads into g_shard, adam_shard(g_shard)
+    updates this rank's fp32 master / m / v shard and writes its fp16 slice of p16, then the fp16
+    slices are all-gathered so every rank holds the full updated compute copy."""
+    reduce_scatter_mean_(g_shard, grads)
+    adam_shard(g_shard)
+    all_gather_(p16, rank)
 
 
 def max_over_ranks(x: float, device=None):

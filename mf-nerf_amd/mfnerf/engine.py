@@ -90,23 +90,28 @@ class TrainStep:
         self.off_rgb = XYZ_NET_PARAMS
         self.off_table = XYZ_NET_PARAMS + self.n_rgb
         self.n_params = self.off_table + self.layout.n_params
+        # flat buffers are padded (zeros, never updated) so any power-of-two world size shards them
+        # into float4-aligned equal slices (shard_optimizer)
+        self.n_alloc = -(-self.n_params // 16384) * 16384
         s32 = np.float32(c.scale)
         self.x_min, self.x_range = float(-s32), float(np.float32(s32) - np.float32(-s32))
 
         dev = self.dev
         g = torch.Generator().manual_seed(seed)
-        p = torch.empty(self.n_params)
+        p = torch.zeros(self.n_alloc)
         off = 0
         for o, k in [(64, 32), (16, 64), (c.rgb_width, 32), (c.rgb_width, c.rgb_width), (16, c.rgb_width)]:
             s = math.sqrt(6.0 / (o + k))  # tcnn Xavier-uniform per matrix
             p[off:off + o * k].uniform_(-s, s, generator=g)
             off += o * k
-        p[self.off_table:].uniform_(-1e-4, 1e-4, generator=g)  # tcnn grid init
+        p[self.off_table:self.n_params].uniform_(-1e-4, 1e-4, generator=g)  # tcnn grid init
         self.params = p.to(dev)
-        self.grads = torch.zeros(self.n_params, device=dev)
-        self.m = torch.zeros(self.n_params, device=dev)
-        self.v = torch.zeros(self.n_params, device=dev)
+        self.grads = torch.zeros(self.n_alloc, device=dev)
+        self.m = torch.zeros(self.n_alloc, device=dev)
+        self.v = torch.zeros(self.n_alloc, device=dev)
         self.p16 = self.params.half()
+        self._mlp32 = torch.empty(self.off_table, device=dev)  # fp32 view of the fp16 MLP weights (pack)
+        self.shard = None  # (rank, lo, hi) once shard_optimizer() is on
         self.packed = torch.empty(load().mfnerf_field_packed_bytes(c.rgb_width) // 2, dtype=torch.float16,
                                   device=dev)
         self._pack()
@@ -235,8 +240,27 @@ class TrainStep:
         call("mfnerf_packbits", ptr(self.density_grid), self.bitfield.numel(), thr, None, ptr(self.bitfield), stream())
 
     def _pack(self):
-        call("mfnerf_field_pack_weights", ptr(self.params), ptr(self.params[self.off_rgb:]), self.cfg.rgb_width,
+        """MFMA weight blob from the fp16 compute copy (the fp16 values packing the fp32 master
+        would produce), so it works on every rank when the fp32 master is sharded."""
+        self._mlp32.copy_(self.p16[:self.off_table])
+        call("mfnerf_field_pack_weights", ptr(self._mlp32), ptr(self._mlp32[self.off_rgb:]), self.cfg.rgb_width,
              ptr(self.packed), stream())
+
+    def shard_optimizer(self, rank, world):
+        """Data parallel with a sharded optimizer (mfnerf.dp.sharded_update): this rank keeps Adam
+        state only for its 1/world slice of the flat parameters; the step reduce-scatters the
+        gradient, updates the slice and all-gathers the fp16 compute copy."""
+        if world <= 1:
+            return
+        if self.n_alloc % (64 * world):
+            raise ValueError(f"world size {world} does not divide the padded parameter count {self.n_alloc}")
+        k = self.n_alloc // world
+        lo, hi = rank * k, (rank + 1) * k
+        self.shard = (rank, lo, hi)
+        self.m = torch.zeros(k, device=self.dev)
+        self.v = torch.zeros(k, device=self.dev)
+        self.g_shard = torch.zeros(k, device=self.dev)
+        self.graphs = None  # re-capture with the sharded update
 
     # ---------------------------------------------------------------- the step
     def _march(self, batch: Batch, mb, mark):
@@ -301,12 +325,36 @@ class TrainStep:
         for t in self.parts[1:]:
             self.grads[:self.off_table].add_(t.mlp_grad)
 
-    def _update(self):
-        """Adam over the flat params (+ fp16 mirror) and the MLP weight repack."""
+    def _adam(self, grads, lo, hi):
+        """Adam over params[lo:hi] with grads (hi-lo), refreshing p16[lo:hi]."""
         c = self.cfg
-        call("mfnerf_adam_step", ptr(self.params), ptr(self.grads), ptr(self.m), ptr(self.v), ptr(self.p16),
-             self.n_params, float(c.lr), 0.9, 0.999, c.eps, 1.0, 0, ptr(self.step_dev), ptr(self.lr_dev), stream())
+        call("mfnerf_adam_step", ptr(self.params[lo:hi]), ptr(grads), ptr(self.m), ptr(self.v), ptr(self.p16[lo:hi]),
+             hi - lo, float(c.lr), 0.9, 0.999, c.eps, 1.0, 0, ptr(self.step_dev), ptr(self.lr_dev), stream())
+
+    def _update(self):
+        """Adam over the flat params (+ fp16 mirror) and the MLP weight repack (unsharded)."""
+        self._adam(self.grads, 0, self.n_alloc)
         self._pack()
+
+    def _optimize(self, exchange, adam=None, pack=None):
+        """The update half of a step.  Sharded: reduce-scatter -> Adam on the shard -> all-gather
+        fp16 -> repack; else: exchange(grads) (all-reduce, optional) -> Adam -> repack.  adam/pack
+        replace the eager launches by graph replays."""
+        from . import dp
+        self.adam_step += 1
+        if self.shard is not None:
+            rank, lo, hi = self.shard
+            dp.sharded_update(self.grads, self.g_shard, self.p16, rank,
+                              adam or (lambda g: self._adam(g, lo, hi)))
+            (pack or self._pack)()
+        else:
+            if exchange is not None:
+                exchange(self.grads)
+            if adam is not None:
+                adam(None)
+                (pack or (lambda: None))()
+            else:
+                self._update()
 
     def run(self, batch: Batch, mark=None, exchange=None):
         """One training step, eagerly on the current stream, parts in sequence, march buffer set 0.
@@ -322,17 +370,13 @@ class TrainStep:
             self._grid_bw(mb, q)
             mark("grid_bw")
         self._reduce_parts()
-        if exchange is not None:
-            exchange(self.grads)
-        mark("allreduce")
-        self.optimizer()
-        mark("adam")
+        self._optimize(exchange)
+        mark("update")
 
-    def optimizer(self, lr=None):
+    def optimizer(self, lr=None, exchange=None):
         if lr is not None:
             self.set_lr(lr)
-        self.adam_step += 1
-        self._update()
+        self._optimize(exchange)
 
     def set_lr(self, lr):
         """Device-resident learning rate (train.py:137-142 cosine schedule), read by Adam."""
@@ -374,8 +418,13 @@ class TrainStep:
                       for j in range(2)],
             "grid_bw": [[cap(lambda j=j, q=q: self._grid_bw(self.mbuf[j], q)) for q in range(P)] for j in range(2)],
             "reduce": cap(self._reduce_parts) if P > 1 else None,
-            "update": cap(self._update),
         }
+        if self.shard is not None:
+            rank, lo, hi = self.shard
+            self.graphs["adam"] = cap(lambda: self._adam(self.g_shard, lo, hi))
+            self.graphs["pack"] = cap(self._pack)
+        else:
+            self.graphs["update"] = cap(self._update)
         torch.cuda.synchronize()
         self._side = torch.cuda.Stream(device=self.dev)
         self._part_streams = [None] + [torch.cuda.Stream(device=self.dev) for _ in range(P - 1)]
@@ -436,10 +485,10 @@ class TrainStep:
             main.wait_event(self._ev_part[q])
         if g["reduce"] is not None:
             g["reduce"].replay()
-        if exchange is not None:
-            exchange(self.grads)
-        self.adam_step += 1
-        g["update"].replay()
+        if self.shard is not None:
+            self._optimize(None, adam=lambda _g: g["adam"].replay(), pack=g["pack"].replay)
+        else:
+            self._optimize(exchange, adam=lambda _g: g["update"].replay())
         self._parity = 1 - j
         self._primed = next_batch is not None
 

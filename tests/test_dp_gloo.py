@@ -55,3 +55,50 @@ def test_two_rank_step_keeps_replicas_identical():
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     assert torch.equal(out[0], out[1])
+
+
+def _sharded_worker(rank, world, port, out):
+    import sys
+    sys.path[:0] = [ROOT, PKG]
+    from mfnerf import dp
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 1024  # padded flat parameter vector
+    torch.manual_seed(0)
+    p_full = torch.randn(n)
+    p_full[1000:] = 0.0  # padding: zero, zero grads -> stays zero
+    k = n // world
+    lo, hi = rank * k, (rank + 1) * k
+    # replica A: all-reduce + full Adam; replica B: sharded (this rank's fp32 master/m/v slice only)
+    pa, ma, va = p_full.clone(), torch.zeros(n), torch.zeros(n)
+    pb, mb, vb = p_full.clone(), torch.zeros(k), torch.zeros(k)
+    p16 = p_full.half()
+    g_shard = torch.zeros(k)
+    for t in range(1, 5):
+        g = torch.Generator().manual_seed(dp.rank_seed(t, rank))
+        grad = torch.randn(n, generator=g)
+        grad[1000:] = 0.0
+        ga = dp.allreduce_mean_(grad.clone())
+        adam_ref(pa, ga, ma, va, t)
+
+        def adam_shard(gs):
+            adam_ref(pb[lo:hi], gs, mb, vb, t)
+            p16[lo:hi] = pb[lo:hi].half()
+
+        dp.sharded_update(grad.clone(), g_shard, p16, rank, adam_shard)
+        # the fp16 compute copy every rank holds equals the all-reduce replica's, bit for bit
+        assert torch.equal(p16, pa.half()), t
+        assert torch.equal(pb[lo:hi], pa[lo:hi])
+    assert torch.equal(p16[1000:], torch.zeros(n - 1000, dtype=torch.float16))
+    out[rank] = p16
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharded_optimizer_matches_allreduce():
+    """ZeRO-1 update (reduce-scatter mean -> Adam on the shard -> all-gather fp16) == all-reduce
+    mean -> full Adam, bit for bit, and leaves identical compute copies on every rank."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_sharded_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    assert torch.equal(out[0], out[1])
