@@ -227,6 +227,20 @@ int mfnerf_occupancy_update(float* density_grid, const float* sigmas, const int3
                             int cascades, int grid_size, float decay, const float* count_grid, float density_threshold,
                             float* tmp, uint8_t* bitfield, void* workspace, mfnerf_stream_t stream);
 
+/* ---------------------------------------------------------------- training batch */
+
+/* One training batch from GPU-resident images (datasets/base.py:22-35 + train.py:93-105 get_rays,
+ * datasets/ray_utils.py:50-70): per ray an image index (uniform over n_img; with same_image one
+ * index for the whole batch) and a pixel index (uniform over hw), then
+ *   rays_o = c2w[:, 3], rays_d = directions[pix] @ c2w[:, :3]^T, rgb = images[img, pix].
+ * images (n_img, hw, 3) f32, poses (n_img, 3, 4) f32, directions (hw, 3) f32 (camera frame).
+ * out (3, n_rays, 3) f32 = [rays_o | rays_d | rgb]; img_idx / pix_idx (n_rays) i32 optional.
+ * Draws: counter-based hash of (seed, *call, ray); call (optional device u64) is incremented by the
+ * launch, so graph replays sample fresh batches. */
+int mfnerf_sample_rays(const float* images, const float* poses, const float* directions, int64_t n_img, int64_t hw,
+                       int64_t n_rays, int same_image, uint64_t seed, uint64_t* call, float* out, int32_t* img_idx,
+                       int32_t* pix_idx, mfnerf_stream_t stream);
+
 /* ---------------------------------------------------------------- optimizer */
 
 /* Adam (apex FusedAdam semantics, adam_w_mode=False, no weight decay; train.py:136):
@@ -234,10 +248,16 @@ int mfnerf_occupancy_update(float* density_grid, const float* sigmas, const int3
  * g is read as grad*grad_scale.  Optionally mirrors p into p_f16 (the fp16 compute copy).
  * step_dev (optional device i32): step counter incremented by the kernel (graph-replay safe).
  * lr_dev (optional device f32): learning rate read on the device (a schedule that does not
- * re-capture the graph); lr is used when it is NULL. */
+ * re-capture the graph); lr is used when it is NULL.
+ * skip (optional device i32[2]): when skip[0] != 0 the call changes nothing (params, m, v, p_f16
+ * and step_dev untouched) and increments skip[1] -- torch GradScaler's skipped step on a
+ * non-finite gradient (PL precision=16, train.py:287); skip[0] is set by mfnerf_check_finite. */
 int mfnerf_adam_step(float* params, const float* grads, float* m, float* v, void* p_f16, int64_t n, float lr,
                      float beta1, float beta2, float eps, float grad_scale, int step, const int32_t* step_dev,
-                     const float* lr_dev, mfnerf_stream_t stream);
+                     const float* lr_dev, int32_t* skip, mfnerf_stream_t stream);
+
+/* status[0] (device i32) = 1 if any of x (n f32, 16-byte aligned) is inf/nan, else 0. */
+int mfnerf_check_finite(const float* x, int64_t n, int32_t* status, mfnerf_stream_t stream);
 
 #ifdef __cplusplus
 }

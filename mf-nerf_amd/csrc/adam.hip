@@ -10,7 +10,8 @@ namespace {
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, __half* __restrict__ p16, int64_t n, float lr, float b1, float b2,
                             float eps, float gscale, int step, const int32_t* __restrict__ step_dev,
-                            const float* __restrict__ lr_dev) {
+                            const float* __restrict__ lr_dev, const int32_t* __restrict__ skip) {
+    if (skip && *skip) return;  // GradScaler: no update on a non-finite gradient
     const int st = step_dev ? *step_dev : step;
     if (lr_dev) lr = *lr_dev;
     // apex multi_tensor_adam (ADAM_MODE, decay 0): m/(1-b1^t), v/(1-b2^t), p -= lr*m_hat/(sqrt(v_hat)+eps)
@@ -52,13 +53,30 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
     }
 }
 
-__global__ void bump_step_kernel(int32_t* s) { *s += 1; }
+__global__ void bump_step_kernel(int32_t* s, int32_t* skip) {
+    if (skip && skip[0]) skip[1] += 1;  // count the skipped step
+    else *s += 1;
+}
+
+// status[0] = 1 if any x is inf/nan (status[0] must be 0 on entry); one atomic per offending wave
+__global__ void finite_kernel(const float* __restrict__ x, int64_t n, int32_t* __restrict__ status) {
+    bool bad = false;
+    const int64_t n4 = n / 4, stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        const float4 v = reinterpret_cast<const float4*>(x)[i];
+        bad |= !(isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w));
+    }
+    for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) bad |= !isfinite(x[i]);
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(status, 1);
+}
+
 
 }  // namespace
 
 extern "C" int mfnerf_adam_step(float* params, const float* grads, float* m, float* v, void* p_f16, int64_t n,
                                 float lr, float beta1, float beta2, float eps, float grad_scale, int step,
-                                const int32_t* step_dev, const float* lr_dev, mfnerf_stream_t stream) {
+                                const int32_t* step_dev, const float* lr_dev, int32_t* skip,
+                                mfnerf_stream_t stream) {
     if (n < 0) { mfn_set_error("adam_step: bad size"); return MFN_ERR_INVALID; }
     if (n == 0) return MFN_OK;
     if (!params || !grads || !m || !v) { mfn_set_error("adam_step: null pointer"); return MFN_ERR_INVALID; }
@@ -70,8 +88,20 @@ extern "C" int mfnerf_adam_step(float* params, const float* grads, float* m, flo
     const int threads = 256;
     const int64_t want = mfn::div_up<int64_t>(mfn::div_up<int64_t>(n, 4), threads);
     const unsigned blocks = (unsigned)(want < 4096 ? (want < 1 ? 1 : want) : 4096);
-    if (step_dev) hipLaunchKernelGGL(bump_step_kernel, dim3(1), dim3(1), 0, stream, (int32_t*)step_dev);
+    if (step_dev) hipLaunchKernelGGL(bump_step_kernel, dim3(1), dim3(1), 0, stream, (int32_t*)step_dev, skip);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(threads), 0, stream, params, grads, m, v, (__half*)p_f16, n, lr,
-                       beta1, beta2, eps, grad_scale, step, step_dev, lr_dev);
+                       beta1, beta2, eps, grad_scale, step, step_dev, lr_dev, skip);
     return mfn_check_launch("adam_step");
+}
+
+extern "C" int mfnerf_check_finite(const float* x, int64_t n, int32_t* status, mfnerf_stream_t stream) {
+    if (n < 0 || !status || (n > 0 && !x)) { mfn_set_error("check_finite: bad arguments"); return MFN_ERR_INVALID; }
+    if (((uintptr_t)x) & 15) { mfn_set_error("check_finite: x must be 16-byte aligned"); return MFN_ERR_INVALID; }
+    (void)hipMemsetAsync(status, 0, sizeof(int32_t), stream);
+    if (n > 0) {
+        const int64_t want = mfn::div_up<int64_t>(mfn::div_up<int64_t>(n, 4), 256);
+        hipLaunchKernelGGL(finite_kernel, dim3((unsigned)(want < 2048 ? (want < 1 ? 1 : want) : 2048)), dim3(256), 0,
+                           stream, x, n, status);
+    }
+    return mfn_check_launch("check_finite");
 }

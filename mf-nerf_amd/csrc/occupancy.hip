@@ -32,6 +32,14 @@ __device__ __forceinline__ uint32_t mix64to32(uint64_t x) {
     x ^= x >> 33;
     return (uint32_t)x;
 }
+// per-call key: the call index goes through a full avalanche (added linearly to the counter it
+// would make draw (call c, k) equal draw (call c+1, k-1))
+uint64_t splitmix64_host(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
 __device__ __forceinline__ uint32_t rnd32(uint64_t key, uint64_t ctr) {
     return mix64to32(key + ctr * 0x9E3779B97F4A7C15ull);
 }
@@ -270,7 +278,7 @@ int mfnerf_occupancy_cells(const float* density_grid, int cascades, int grid_siz
     a.n_uniform = warmup ? 0 : n_uniform;
     a.warmup = warmup ? 1 : 0;
     a.scale = scale;
-    a.key = (seed ^ 0x5851F42D4C957F2Dull) * 0x2545F4914F6CDD1Dull + call_index * 0x9E3779B97F4A7C15ull;
+    a.key = splitmix64_host(splitmix64_host(seed ^ 0x5851F42D4C957F2Dull) ^ call_index);
     const int64_t n = (int64_t)cascades * a.per_cascade;
     hipLaunchKernelGGL(occ_points_kernel, dim3(blocks_for(n)), dim3(OCC_BLOCK), 0, stream, a, w.list, w.counts, xyzs,
                        cell_idx);

@@ -68,7 +68,9 @@ SIGNATURES = {
     "mfnerf_occupancy_points": (_I64, [_I, _I, _I64, _I]),
     "mfnerf_occupancy_cells": (_I, [_P, _I, _I, _F, _I64, _I, _F, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P]),
     "mfnerf_occupancy_update": (_I, [_P, _P, _P, _I64, _I, _I, _F, _P, _F, _P, _P, _P, _P]),
-    "mfnerf_adam_step": (_I, [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P]),
+    "mfnerf_sample_rays": (_I, [_P, _P, _P, _I64, _I64, _I64, _I, ctypes.c_uint64, _P, _P, _P, _P, _P]),
+    "mfnerf_adam_step": (_I, [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _P]),
+    "mfnerf_check_finite": (_I, [_P, _I64, _P, _P]),
 }
 
 _lib = None
@@ -100,7 +102,13 @@ def call(name, *args):
 
 
 def ptr(t):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+    """Device pointer of a tensor for the C ABI (None -> NULL).  Host tensors are refused: every
+    pointer this library takes is dereferenced on the GPU."""
+    if t is None:
+        return ctypes.c_void_p(0)
+    if not t.is_cuda:
+        raise ValueError("libmfnerf_hip takes device tensors; got a host tensor")
+    return ctypes.c_void_p(t.data_ptr())
 
 
 def stream():

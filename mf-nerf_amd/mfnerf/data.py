@@ -1,0 +1,201 @@
+"""Training data for the step: the reference's NSVF dataset (datasets/nsvf.py:12-100), its ray
+utilities (datasets/ray_utils.py:8-70) and image reader (datasets/color_utils.py:19-31), and a
+GPU-resident dataset whose per-step batch (random image + pixel per ray -> rays_o, rays_d, rgb;
+datasets/base.py:22-35 + train.py:93-105) is one HIP launch (mfnerf_sample_rays), so the data side
+of a training step stays on the device and inside the step's graph.
+
+Also an analytic scene (opaque coloured balls in the unit box, exact ray-sphere first hits, white
+background) that renders ground-truth views of any camera: the image has no datasets, so tests and
+bench.py train on it.
+"""
+import glob
+import math
+import os
+
+import numpy as np
+import torch
+
+from ._lib import call, ptr, stream
+
+
+# ---------------------------------------------------------------------------- ray utilities
+def get_ray_directions(H, W, K, device="cpu", random=False, flatten=True):
+    """ray_utils.py:8-47: camera-frame directions [right down front] through pixel centres
+    (kornia create_meshgrid(H, W, normalized=False): u = column, v = row)."""
+    v, u = torch.meshgrid(torch.arange(H, dtype=torch.float32, device=device),
+                          torch.arange(W, dtype=torch.float32, device=device), indexing="ij")
+    fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+    if random:
+        d = torch.stack([(u - cx + torch.rand_like(u)) / fx, (v - cy + torch.rand_like(v)) / fy, torch.ones_like(u)], -1)
+    else:
+        d = torch.stack([(u - cx + 0.5) / fx, (v - cy + 0.5) / fy, torch.ones_like(u)], -1)
+    return d.reshape(-1, 3) if flatten else d
+
+
+def get_rays(directions, c2w):
+    """ray_utils.py:50-70: world-frame (rays_o, rays_d) for (N,3) directions and (3,4) / (N,3,4) poses."""
+    if c2w.ndim == 2:
+        rays_d = directions @ c2w[:, :3].T
+    else:
+        rays_d = (directions[:, None, :] @ c2w[..., :3].transpose(1, 2))[:, 0]
+    rays_o = c2w[..., 3].expand_as(rays_d)
+    return rays_o, rays_d
+
+
+def read_image(path, img_wh, blend_a=True):
+    """color_utils.py:19-31: float RGB in [0,1], alpha blended onto white, flattened (h*w, 3).
+    The reference resizes with cv2 (INTER_LINEAR); cv2 is not in this image, so a size change uses
+    PIL's bilinear filter instead (identical at downsample 1.0, where no resize happens)."""
+    from PIL import Image
+    im = Image.open(path)
+    img = np.asarray(im).astype(np.float32) / 255.0
+    if img.ndim == 2:
+        img = np.repeat(img[..., None], 3, -1)
+    if img.shape[2] == 4:
+        img = img[..., :3] * img[..., -1:] + (1 - img[..., -1:]) if blend_a else img[..., :3] * img[..., -1:]
+    if (img.shape[1], img.shape[0]) != tuple(img_wh):
+        chans = [np.asarray(Image.fromarray(img[..., c]).resize(tuple(img_wh), Image.BILINEAR)) for c in range(3)]
+        img = np.stack(chans, -1)
+    return img.reshape(-1, 3)
+
+
+# ---------------------------------------------------------------------------- NSVF
+class NSVFDataset:
+    """datasets/nsvf.py: intrinsics.txt / bbox.txt / pose/*.txt / rgb/*.png under root_dir.
+    Poses are shifted by the bbox centre and scaled by 2*scale (scene inside [-0.5,0.5]^3, with the
+    reference's 1.05 enlargement and its Lego (1.1) / Mic (1.2) fixes); splits by file prefix
+    (train 0_, val 1_, test 2_ for Synthetic scenes, 1_ for real ones)."""
+
+    def __init__(self, root_dir, split="train", downsample=1.0):
+        self.root_dir, self.split, self.downsample = root_dir, split, downsample
+        self.read_intrinsics()
+        xyz_min, xyz_max = np.loadtxt(os.path.join(root_dir, "bbox.txt"))[:6].reshape(2, 3)
+        self.shift = (xyz_max + xyz_min) / 2
+        self.scale = (xyz_max - xyz_min).max() / 2 * 1.05
+        if "Mic" in root_dir:
+            self.scale *= 1.2
+        elif "Lego" in root_dir:
+            self.scale *= 1.1
+        self.read_meta(split)
+
+    def read_intrinsics(self):
+        r = self.root_dir
+        if "Synthetic" in r or "Ignatius" in r:
+            with open(os.path.join(r, "intrinsics.txt")) as f:
+                fx = fy = float(f.readline().split()[0]) * self.downsample
+            if "Synthetic" in r:
+                w = h = int(800 * self.downsample)
+            else:
+                w, h = int(1920 * self.downsample), int(1080 * self.downsample)
+            K = np.float32([[fx, 0, w / 2], [0, fy, h / 2], [0, 0, 1]])
+        else:
+            K = np.loadtxt(os.path.join(r, "intrinsics.txt"), dtype=np.float32)[:3, :3]
+            if "BlendedMVS" in r:
+                w, h = int(768 * self.downsample), int(576 * self.downsample)
+            elif "Tanks" in r:
+                w, h = int(1920 * self.downsample), int(1080 * self.downsample)
+            else:
+                raise ValueError(f"unknown NSVF scene family: {r}")
+            K[:2] *= self.downsample
+        self.K = torch.FloatTensor(K)
+        self.directions = get_ray_directions(h, w, self.K)
+        self.img_wh = (w, h)
+
+    def read_meta(self, split):
+        r = self.root_dir
+        prefix = {"train": "0_", "trainval": "[0-1]_", "trainvaltest": "[0-2]_", "val": "1_"}.get(split)
+        if prefix is None:
+            if split != "test":
+                raise ValueError(f"{split} split not recognized!")
+            prefix = "2_" if "Synthetic" in r else "1_"
+        img_paths = sorted(glob.glob(os.path.join(r, "rgb", prefix + "*.png")))
+        pose_paths = sorted(glob.glob(os.path.join(r, "pose", prefix + "*.txt")))
+        poses, rays = [], []
+        for ip, pp in zip(img_paths, pose_paths):
+            c2w = np.loadtxt(pp)[:3]
+            c2w[:, 3] -= self.shift
+            c2w[:, 3] /= 2 * self.scale
+            poses.append(c2w)
+            img = read_image(ip, self.img_wh)
+            if "Jade" in r or "Fountain" in r:
+                img[np.all(img <= 0.1, axis=-1)] = 1.0
+            rays.append(img)
+        self.rays = torch.FloatTensor(np.stack(rays)) if rays else torch.zeros(0, 0, 3)
+        self.poses = torch.FloatTensor(np.stack(poses)) if poses else torch.zeros(0, 3, 4)
+
+
+# ---------------------------------------------------------------------------- GPU-resident batches
+class DeviceDataset:
+    """Images (n_img, hw, 3), poses (n_img, 3, 4) and camera directions (hw, 3) resident in HBM;
+    sample(out) draws one training batch into a (3, N, 3) buffer with one launch (graph-safe: the
+    draw counter lives on the device).  strategy: 'all_images' or 'same_image' (base.py:25-28)."""
+
+    def __init__(self, images, poses, directions, K=None, img_wh=None, device="cuda", seed=0,
+                 strategy="all_images"):
+        self.images = images.float().contiguous().to(device)
+        self.poses = poses.float().contiguous().to(device)
+        self.directions = directions.float().contiguous().to(device)
+        self.K, self.img_wh = K, img_wh
+        self.n_img, self.hw = self.images.shape[0], self.images.shape[1]
+        assert self.poses.shape == (self.n_img, 3, 4) and self.directions.shape == (self.hw, 3)
+        self.seed = int(seed)
+        self.same_image = {"all_images": 0, "same_image": 1}[strategy]
+        self.calls = torch.zeros(1, dtype=torch.int64, device=device)  # device draw counter
+
+    @classmethod
+    def from_nsvf(cls, ds: NSVFDataset, device="cuda", **kw):
+        return cls(ds.rays, ds.poses, ds.directions, K=ds.K, img_wh=ds.img_wh, device=device, **kw)
+
+    def sample(self, out, img_idx=None, pix_idx=None):
+        """out (3, N, 3) f32 <- [rays_o | rays_d | rgb] of N random rays."""
+        n = out.shape[1]
+        call("mfnerf_sample_rays", ptr(self.images), ptr(self.poses), ptr(self.directions), self.n_img, self.hw, n,
+             self.same_image, self.seed, ptr(self.calls), ptr(out), ptr(img_idx), ptr(pix_idx), stream())
+        return out
+
+
+# ---------------------------------------------------------------------------- analytic scene
+class BallScene:
+    """Opaque coloured balls inside [-0.5, 0.5]^3; render(o, d) = colour of the first ball hit,
+    white where nothing is hit (the synthetic-scene background of rendering.py:153-155)."""
+
+    def __init__(self, n_balls=8, seed=0, radius=(0.08, 0.2)):
+        g = torch.Generator().manual_seed(seed)
+        self.r = torch.rand(n_balls, generator=g) * (radius[1] - radius[0]) + radius[0]
+        self.c = (torch.rand(n_balls, 3, generator=g) - 0.5) * (1.0 - 2 * self.r[:, None]).clamp(min=0)
+        self.rgb = torch.rand(n_balls, 3, generator=g) * 0.8 + 0.1
+
+    def render(self, o, d):
+        o, d = o.double(), d.double()
+        dn = d / d.norm(dim=-1, keepdim=True)
+        oc = o[:, None, :] - self.c.double()[None]                     # (N, B, 3)
+        b = (oc * dn[:, None, :]).sum(-1)
+        cc = (oc * oc).sum(-1) - self.r.double()[None] ** 2
+        disc = b * b - cc
+        t = -b - torch.sqrt(disc.clamp(min=0))
+        t = torch.where((disc > 0) & (t > 0), t, torch.full_like(t, math.inf))
+        tmin, idx = t.min(-1)
+        out = torch.ones(o.shape[0], 3, dtype=torch.float64)
+        hit = torch.isfinite(tmin)
+        out[hit] = self.rgb.double()[idx[hit]]
+        return out.float()
+
+    def density_grid(self, G=128, cascades=1):
+        """Occupancy prior (density 100 inside balls, 0 elsewhere) in the reference's Morton order."""
+        from . import synthetic
+        return synthetic.balls_to_grid(self.c.numpy(), self.r.numpy(), G=G, cascades=cascades)
+
+
+def ball_scene_views(scene, n_views, W, focal, radius=1.5, seed=0):
+    """n_views cameras on a sphere looking at the origin (synthetic.camera_poses), W x W pinhole
+    intrinsics, ground-truth images rendered analytically: (images (n, W*W, 3), poses (n,3,4),
+    directions (W*W, 3), K)."""
+    from . import synthetic
+    poses = synthetic.camera_poses(n_cams=n_views, seed=seed, radius=radius)
+    K = torch.tensor([[focal, 0, W / 2], [0, focal, W / 2], [0, 0, 1]], dtype=torch.float32)
+    dirs = get_ray_directions(W, W, K)
+    imgs = []
+    for p in poses:
+        o, d = get_rays(dirs, p)
+        imgs.append(scene.render(o, d))
+    return torch.stack(imgs), poses, dirs, K

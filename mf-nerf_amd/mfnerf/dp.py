@@ -86,6 +86,17 @@ def sharded_update(grads, g_shard, p16, rank, adam_shard):
     all_gather_(p16, rank)
 
 
+def allreduce_max_(t):
+    """In-place elementwise max over ranks (the non-finite-gradient flag)."""
+    if _world() == 1:
+        return t
+    if dist.get_backend() == "nccl":
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    else:
+        _host_staged(lambda x: dist.all_reduce(x, op=dist.ReduceOp.MAX), t)
+    return t
+
+
 def max_over_ranks(x: float, device=None):
     """Slowest rank's value (bench timing)."""
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size() == 1:

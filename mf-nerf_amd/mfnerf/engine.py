@@ -53,6 +53,7 @@ class StepConfig:
     T_threshold: float = 1e-4
     max_samples: int = MAX_SAMPLES
     n_parts: int = 1
+    skip_nonfinite: bool = True  # GradScaler semantics: no optimizer step on an inf/nan gradient
 
 
 @dataclass
@@ -112,6 +113,7 @@ class TrainStep:
         self.p16 = self.params.half()
         self._mlp32 = torch.empty(self.off_table, device=dev)  # fp32 view of the fp16 MLP weights (pack)
         self.shard = None  # (rank, lo, hi) once shard_optimizer() is on
+        self.finite_status = torch.zeros(2, dtype=torch.int32, device=dev)  # [non-finite flag, skipped steps]
         self.packed = torch.empty(load().mfnerf_field_packed_bytes(c.rgb_width) // 2, dtype=torch.float16,
                                   device=dev)
         self._pack()
@@ -141,6 +143,14 @@ class TrainStep:
         # fp16 backward scale: per-sample grads are O(1/n_rays); 2^(floor(log2 N)-2) keeps them normal
         self.grad_scale = float(2.0 ** max(0, int(math.floor(math.log2(N))) - 2))
         self._primed = False
+        self.dataset = None
+
+    def attach_dataset(self, ds):
+        """Draw every step's batch on the device from ds (mfnerf.data.DeviceDataset): run() and
+        replay() then take no batch; inside graphs the draw is part of the march graph."""
+        self.dataset = ds
+        self._sampled = _packed_batch(torch.zeros(3, self.cfg.n_rays, 3, device=self.dev))
+        self.graphs = None
 
     # ---------------------------------------------------------------- buffers
     def _part_buffers(self, q):
@@ -325,16 +335,46 @@ class TrainStep:
         for t in self.parts[1:]:
             self.grads[:self.off_table].add_(t.mlp_grad)
 
+    def _check(self, grads):
+        """finite_status[0] = any(grads is inf/nan) (when skip_nonfinite)."""
+        if self.cfg.skip_nonfinite:
+            call("mfnerf_check_finite", ptr(grads), grads.numel(), ptr(self.finite_status), stream())
+
     def _adam(self, grads, lo, hi):
-        """Adam over params[lo:hi] with grads (hi-lo), refreshing p16[lo:hi]."""
+        """Adam over params[lo:hi] with grads (hi-lo), refreshing p16[lo:hi]; a no-op when the
+        finite check flagged this step."""
         c = self.cfg
         call("mfnerf_adam_step", ptr(self.params[lo:hi]), ptr(grads), ptr(self.m), ptr(self.v), ptr(self.p16[lo:hi]),
-             hi - lo, float(c.lr), 0.9, 0.999, c.eps, 1.0, 0, ptr(self.step_dev), ptr(self.lr_dev), stream())
+             hi - lo, float(c.lr), 0.9, 0.999, c.eps, 1.0, 0, ptr(self.step_dev), ptr(self.lr_dev),
+             ptr(self.finite_status) if c.skip_nonfinite else None, stream())
 
     def _update(self):
-        """Adam over the flat params (+ fp16 mirror) and the MLP weight repack (unsharded)."""
+        """Finite check + Adam over the flat params (+ fp16 mirror) + MLP weight repack (unsharded)."""
+        self._check(self.grads)
         self._adam(self.grads, 0, self.n_alloc)
         self._pack()
+
+    def _shard_adam(self, check, adam):
+        """Sharded: each rank checks its gradient shard, the flag is max-reduced over ranks (one
+        int, so every rank takes the same decision), then Adam on the shard."""
+        from . import dp
+        check()
+        if self.cfg.skip_nonfinite:
+            dp.allreduce_max_(self.finite_status[:1])
+        adam()
+
+    def full_params(self):
+        """The fp32 master parameters (all-gathered over ranks when the optimizer is sharded)."""
+        if self.shard is None:
+            return self.params
+        from . import dp
+        full = self.params.clone()
+        dp.all_gather_(full, self.shard[0])
+        return full
+
+    def skipped_steps(self):
+        """Optimizer steps skipped on non-finite gradients so far (host read)."""
+        return int(self.finite_status[1])
 
     def _optimize(self, exchange, adam=None, pack=None):
         """The update half of a step.  Sharded: reduce-scatter -> Adam on the shard -> all-gather
@@ -345,7 +385,7 @@ class TrainStep:
         if self.shard is not None:
             rank, lo, hi = self.shard
             dp.sharded_update(self.grads, self.g_shard, self.p16, rank,
-                              adam or (lambda g: self._adam(g, lo, hi)))
+                              adam or (lambda g: self._shard_adam(lambda: self._check(g), lambda: self._adam(g, lo, hi))))
             (pack or self._pack)()
         else:
             if exchange is not None:
@@ -356,13 +396,17 @@ class TrainStep:
             else:
                 self._update()
 
-    def run(self, batch: Batch, mark=None, exchange=None):
+    def run(self, batch: Batch = None, mark=None, exchange=None):
         """One training step, eagerly on the current stream, parts in sequence, march buffer set 0.
         mark(name) is called after each stage (bench timing); exchange(grads) runs between backward
-        and Adam (the data-parallel all-reduce)."""
+        and Adam (the data-parallel all-reduce).  batch=None: drawn from the attached dataset."""
         mark = mark or (lambda name: None)
+        if batch is None:
+            batch = self._sampled
+            self.dataset.sample(batch.buf)
         mb = self.mbuf[0]
         self._use(mb)
+        self.last_batch = batch
         self._primed = False  # a pipelined replay() must march its own batch next
         self._march(batch, mb, mark)
         for q in range(self.n_parts):
@@ -412,8 +456,13 @@ class TrainStep:
             return g
 
         P = self.n_parts
+        def march(j):
+            if self.dataset is not None:
+                self.dataset.sample(self._static[j].buf)
+            self._march(self._static[j], self.mbuf[j], nomark)
+
         self.graphs = {
-            "march": [cap(lambda j=j: self._march(self._static[j], self.mbuf[j], nomark), rng=True) for j in range(2)],
+            "march": [cap(lambda j=j: march(j), rng=True) for j in range(2)],
             "chain": [[cap(lambda j=j, q=q: self._chain(self._static[j], self.mbuf[j], q, nomark)) for q in range(P)]
                       for j in range(2)],
             "grid_bw": [[cap(lambda j=j, q=q: self._grid_bw(self.mbuf[j], q)) for q in range(P)] for j in range(2)],
@@ -421,6 +470,7 @@ class TrainStep:
         }
         if self.shard is not None:
             rank, lo, hi = self.shard
+            self.graphs["check"] = cap(lambda: self._check(self.g_shard))
             self.graphs["adam"] = cap(lambda: self._adam(self.g_shard, lo, hi))
             self.graphs["pack"] = cap(self._pack)
         else:
@@ -448,22 +498,35 @@ class TrainStep:
         the main stream) has passed: set j's buffers were last read two steps back."""
         self._side.wait_event(after)
         with torch.cuda.stream(self._side):
-            self._stage_batch(j, batch)
+            if batch is not None:
+                self._stage_batch(j, batch)
             self.graphs["march"][j].replay()
             self._ev_march[j].record(self._side)
 
-    def replay(self, batch: Batch, exchange=None, grid_bw_events=None, next_batch=None):
-        """One training step from the captured graphs (the kernels of run()).  With next_batch, the
-        next step's march is issued on the side stream to overlap this step; the next replay() must
-        then be called with that batch.  grid_bw_events: optional (start, [end per part]) timing
-        events -- start before part 0's grid_bw, end after each part's grid_bw."""
+    def replay(self, batch: Batch = None, exchange=None, grid_bw_events=None, next_batch=None, prefetch=None):
+        """One training step from the captured graphs (the kernels of run()).  With next_batch (or,
+        with an attached dataset, prefetch=True, its default), the next step's march is issued on
+        the side stream to overlap this step; the next replay() must then be called with that batch
+        (or, with a dataset, the next replay() trains on the batch already drawn).  Pass
+        prefetch=False before anything that must precede the next march (an occupancy refresh).
+        grid_bw_events: optional (start, [end per part]) timing events -- start before part 0's
+        grid_bw, end after each part's grid_bw."""
         g, j, P = self.graphs, self._parity, self.n_parts
+        if self.dataset is not None:
+            batch = None
+            if prefetch is None:
+                prefetch = True
+        elif prefetch is None:
+            prefetch = next_batch is not None
+        elif prefetch and next_batch is None:
+            raise ValueError("prefetch needs next_batch (or an attached dataset)")
         main = torch.cuda.current_stream()
         self._ev_start.record(main)
         if not self._primed:
             self._march_on_side(j, batch, self._ev_start)
         main.wait_event(self._ev_march[j])
         self._use(self.mbuf[j])
+        self.last_batch = self._static[j]
         for q in range(P):
             sq = main if q == 0 else self._part_streams[q]
             if q > 0:
@@ -471,7 +534,7 @@ class TrainStep:
             with torch.cuda.stream(sq):
                 g["chain"][j][q].replay()
                 self._ev_chain[q].record(sq)
-                if q == P - 1 and next_batch is not None:
+                if q == P - 1 and prefetch:
                     # set 1-j was last read by the previous step, which this chain follows; waiting
                     # for the last chain puts the march under the grid_bw scatters, not the chains
                     self._march_on_side(1 - j, next_batch, self._ev_chain[q])
@@ -486,11 +549,12 @@ class TrainStep:
         if g["reduce"] is not None:
             g["reduce"].replay()
         if self.shard is not None:
-            self._optimize(None, adam=lambda _g: g["adam"].replay(), pack=g["pack"].replay)
+            self._optimize(None, adam=lambda _g: self._shard_adam(g["check"].replay, g["adam"].replay),
+                           pack=g["pack"].replay)
         else:
             self._optimize(exchange, adam=lambda _g: g["update"].replay())
         self._parity = 1 - j
-        self._primed = next_batch is not None
+        self._primed = bool(prefetch)
 
     # ---------------------------------------------------------------- occupancy (networks.py:157-271)
     def _occ_buffers(self):

@@ -25,6 +25,37 @@ def _meshgrid3d(G, device=None):
     return torch.stack([d, h, w], -1).reshape(-1, 3)
 
 
+@torch.no_grad()
+def mark_invisible_cells(density_grid, grid_coords, scale, K, poses, img_wh, chunk=64 ** 3):
+    """networks.py:199-240 on a (C, G^3) density grid (in place): cells seen by no camera, or too
+    near one, get -1 (never updated again), the others 0.  Returns count_grid (the fraction of
+    cameras seeing each cell; used by the erode option of the occupancy refresh)."""
+    cascades, G = density_grid.shape[0], round(density_grid.shape[1] ** (1 / 3))
+    count_grid = torch.zeros_like(density_grid)
+    N_cams = poses.shape[0]
+    w2c_R = rearrange(poses[:, :3, :3], "n a b -> n b a")
+    w2c_T = -w2c_R @ poses[:, :3, 3:]
+    indices = vren.morton3D(grid_coords).long()
+    for c in range(cascades):
+        for i in range(0, len(indices), chunk):
+            xyzs = grid_coords[i:i + chunk] / (G - 1) * 2 - 1
+            s = min(2 ** (c - 1), scale)
+            half_grid_size = s / G
+            xyzs_w = (xyzs * (s - half_grid_size)).T
+            xyzs_c = w2c_R @ xyzs_w + w2c_T
+            uvd = K @ xyzs_c
+            uv = uvd[:, :2] / uvd[:, 2:]
+            in_image = (uvd[:, 2] >= 0) & (uv[:, 0] >= 0) & (uv[:, 0] < img_wh[0]) & \
+                       (uv[:, 1] >= 0) & (uv[:, 1] < img_wh[1])
+            covered_by_cam = (uvd[:, 2] >= NEAR_DISTANCE) & in_image
+            count_grid[c, indices[i:i + chunk]] = count = covered_by_cam.sum(0) / N_cams
+            too_near_to_cam = (uvd[:, 2] < NEAR_DISTANCE) & in_image
+            too_near_to_any_cam = too_near_to_cam.any(0)
+            valid_mask = (count > 0) & (~too_near_to_any_cam)
+            density_grid[c, indices[i:i + chunk]] = torch.where(valid_mask, 0., -1.)
+    return count_grid
+
+
 class NGP(nn.Module):
     def __init__(self, scale, hparams, rgb_act="Sigmoid"):
         super().__init__()
@@ -105,29 +136,8 @@ class NGP(nn.Module):
     @torch.no_grad()
     def mark_invisible_cells(self, K, poses, img_wh, chunk=64 ** 3):
         """networks.py:199-240."""
-        N_cams = poses.shape[0]
-        self.count_grid = torch.zeros_like(self.density_grid)
-        w2c_R = rearrange(poses[:, :3, :3], "n a b -> n b a")
-        w2c_T = -w2c_R @ poses[:, :3, 3:]
-        cells = self.get_all_cells()
-        for c in range(self.cascades):
-            indices, coords = cells[c]
-            for i in range(0, len(indices), chunk):
-                xyzs = coords[i:i + chunk] / (self.grid_size - 1) * 2 - 1
-                s = min(2 ** (c - 1), self.scale)
-                half_grid_size = s / self.grid_size
-                xyzs_w = (xyzs * (s - half_grid_size)).T
-                xyzs_c = w2c_R @ xyzs_w + w2c_T
-                uvd = K @ xyzs_c
-                uv = uvd[:, :2] / uvd[:, 2:]
-                in_image = (uvd[:, 2] >= 0) & (uv[:, 0] >= 0) & (uv[:, 0] < img_wh[0]) & \
-                           (uv[:, 1] >= 0) & (uv[:, 1] < img_wh[1])
-                covered_by_cam = (uvd[:, 2] >= NEAR_DISTANCE) & in_image
-                self.count_grid[c, indices[i:i + chunk]] = count = covered_by_cam.sum(0) / N_cams
-                too_near_to_cam = (uvd[:, 2] < NEAR_DISTANCE) & in_image
-                too_near_to_any_cam = too_near_to_cam.any(0)
-                valid_mask = (count > 0) & (~too_near_to_any_cam)
-                self.density_grid[c, indices[i:i + chunk]] = torch.where(valid_mask, 0., -1.)
+        self.count_grid = mark_invisible_cells(self.density_grid, self.grid_coords, self.scale, K, poses, img_wh,
+                                               chunk)
 
     @torch.no_grad()
     def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False):

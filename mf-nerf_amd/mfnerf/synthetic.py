@@ -62,6 +62,12 @@ def ball_density_grid(G=128, cascades=1, scale=0.5, n_balls=12, radius=(0.065, 0
     g = np.random.default_rng(seed)
     centers = g.uniform(-0.5 + radius[1], 0.5 - radius[1], size=(n_balls, 3))
     radii = g.uniform(radius[0], radius[1], size=n_balls)
+    return balls_to_grid(centers, radii, G=G, cascades=cascades, scale=scale, occupied=occupied)
+
+
+def balls_to_grid(centers, radii, G=128, cascades=1, scale=0.5, occupied=10.0):
+    """(C, G^3) f32 density grid, `occupied` in the cells whose centre lies inside a ball."""
+    centers, radii = np.asarray(centers, np.float64), np.asarray(radii, np.float64)
     grid = np.zeros((cascades, G ** 3), np.float32)
     ii = np.arange(G, dtype=np.int64)
     x, y, z = np.meshgrid(ii, ii, ii, indexing="ij")

@@ -163,3 +163,18 @@ def test_engine_refresh_end_to_end(gpu):
         got = st.density_grid.cpu().reshape(-1)
         assert torch.equal(got[~dup], ref_g.reshape(-1)[~dup])
         assert OO.cell_points_ok(o.xyz[:n].cpu(), cell, st.cascades, st.G, st.cfg.scale)
+
+
+def test_consecutive_refreshes_draw_independent_cells(gpu):
+    """The uniform cells of refresh calls 0, 1, 2 overlap only at the random-coincidence rate."""
+    C, G = 1, 128
+    grid = torch.zeros(C, G ** 3, device=gpu)
+    M = 20000
+    cells = []
+    for k in range(3):
+        _, cell, _ = _cells(gpu, grid, C, G, 0.5, M, False, seed=1, call_index=k)
+        cells.append(set(cell[:M].tolist()))
+    expect = M * M / G ** 3  # ~190 coincidences between two independent draws
+    for a in range(3):
+        for b in range(a + 1, 3):
+            assert len(cells[a] & cells[b]) < 2 * expect + 50

@@ -1,0 +1,100 @@
+"""Training harness on the GPU: device batch sampling (base.py:22-35 + get_rays), the GradScaler
+skip on non-finite gradients, checkpoints in the reference's key layout, and an end-to-end run
+(occupancy cadence, cosine LR, pipelined graphs, test-time renderer) that must learn a scene."""
+import math
+
+import pytest
+import torch
+
+from mfnerf import data, engine
+from mfnerf.trainer import HParams, Trainer
+
+pytestmark = pytest.mark.gpu
+
+
+def test_sample_rays_matches_torch(gpu):
+    g = torch.Generator().manual_seed(0)
+    n_img, hw, N = 5, 300, 4096
+    imgs, poses, dirs = torch.rand(n_img, hw, 3, generator=g), torch.randn(n_img, 3, 4, generator=g), \
+        torch.randn(hw, 3, generator=g)
+    ds = data.DeviceDataset(imgs, poses, dirs, device=gpu, seed=3)
+    out = torch.empty(3, N, 3, device=gpu)
+    ii, pp = torch.empty(N, dtype=torch.int32, device=gpu), torch.empty(N, dtype=torch.int32, device=gpu)
+    ds.sample(out, ii, pp)
+    oc, ic, pc = out.cpu(), ii.cpu().long(), pp.cpu().long()
+    assert torch.equal(oc[2], imgs[ic, pc])
+    o, d = data.get_rays(dirs[pc], poses[ic])
+    assert torch.equal(oc[0], o) and torch.allclose(oc[1], d, atol=1e-5)
+    assert set(ic.tolist()) == set(range(n_img)) and len(set(pc.tolist())) > 0.9 * hw
+    # the device counter advances: a second draw differs; same_image draws one image per batch
+    out2 = torch.empty(3, N, 3, device=gpu)
+    ds.sample(out2)
+    assert not torch.equal(out2.cpu(), oc)
+    same = data.DeviceDataset(imgs, poses, dirs, device=gpu, strategy="same_image")
+    same.sample(out, ii, pp)
+    assert len(set(ii.cpu().tolist())) == 1
+
+
+def test_sample_rays_batches_are_independent(gpu):
+    """Consecutive draws share no structure: over 1e8 (image, pixel) pairs, batches c, c+1, c+2
+    have ~0 pairs in common (a counter hash with the call added linearly made batch c+2 batch c
+    shifted by one ray -- the model then trains on two alternating batches)."""
+    n_img, hw, N = 1000, 100000, 4096
+    ds = data.DeviceDataset(torch.zeros(n_img, hw, 3), torch.zeros(n_img, 3, 4), torch.zeros(hw, 3), device=gpu)
+    out = torch.empty(3, N, 3, device=gpu)
+    ii, pp = torch.empty(N, dtype=torch.int32, device=gpu), torch.empty(N, dtype=torch.int32, device=gpu)
+    sets = []
+    for _ in range(4):
+        ds.sample(out, ii, pp)
+        sets.append(set((ii.long() * hw + pp.long()).cpu().tolist()))
+    for a in range(4):
+        for b in range(a + 1, 4):
+            assert len(sets[a] & sets[b]) < 10, (a, b, len(sets[a] & sets[b]))
+
+
+def test_nonfinite_gradient_skips_the_step(gpu):
+    st = engine.TrainStep(engine.StepConfig(n_rays=256, log2_T=14), device=gpu)
+    p0, m0, s0 = st.params.clone(), st.m.clone(), int(st.step_dev)
+    st.grads.normal_()
+    st.grads[12345] = float("nan")
+    st._update()
+    assert torch.equal(st.params, p0) and torch.equal(st.m, m0) and int(st.step_dev) == s0
+    assert st.skipped_steps() == 1
+    st.grads.normal_()
+    st._update()
+    assert not torch.equal(st.params, p0) and int(st.step_dev) == s0 + 1 and st.skipped_steps() == 1
+
+
+def _ball_views(n, W=64, seed=0):
+    focal = 0.5 * W / math.tan(0.5 * 0.6911112)  # the Lego field of view
+    return data.ball_scene_views(data.BallScene(n_balls=6, seed=1), n, W, focal, seed=seed)
+
+
+def test_trainer_learns_a_scene_and_checkpoints(gpu, tmp_path):
+    imgs, poses, dirs, K = _ball_views(100)
+    t_imgs, t_poses, _, _ = _ball_views(4, seed=7)
+    ds = data.DeviceDataset(imgs, poses, dirs, K=K, img_wh=(64, 64), device=gpu, seed=5)
+    hp = HParams(batch_size=4096, T=16, num_epochs=2, steps_per_epoch=600)
+    tr = Trainer(hp, ds, device=gpu)
+    hist = tr.fit(log_every=200)
+    psnr, per_view = tr.evaluate(t_imgs, t_poses, dirs)
+    white = sum(float(-10 * torch.log10(((1 - im) ** 2).mean())) for im in t_imgs) / len(t_imgs)
+    print("\nTRAIN", [(h["step"], round(h["psnr"], 2), round(h["loss"], 5), round(h["rm_s"], 1), h["lr"])
+                      for h in hist], "\nTEST psnr", round(psnr, 2), [round(v, 2) for v in per_view],
+          "white-image baseline", round(white, 2))
+    assert psnr > white + 8.0 and psnr > 25.0
+    assert abs(hist[-1]["lr"] - hp.lr * 0.01) < 1e-9 and hist[-1]["skipped"] == 0
+    # checkpoint round trip (reference key layout) into a fresh trainer and into the NGP mirror
+    path = str(tmp_path / "ck.ckpt")
+    tr.save(path)
+    tr2 = Trainer(hp, ds, device=gpu)
+    tr2.load(path)
+    assert torch.equal(tr2.step.p16[:tr.step.n_params], tr.step.p16[:tr.step.n_params])
+    assert torch.equal(tr2.step.bitfield, tr.step.bitfield)
+    psnr2, _ = tr2.evaluate(t_imgs, t_poses, dirs)
+    assert abs(psnr2 - psnr) < 1e-3
+    sd = torch.load(path, map_location="cpu", weights_only=True)["state_dict"]
+    from mfnerf.networks import NGP
+    m = NGP(0.5, hp)
+    m.load_state_dict({k[6:]: v for k, v in sd.items() if k.startswith("model.")}, strict=False)
+    assert torch.equal(m.rgb_net.params.detach(), tr.step.params[tr.step.off_rgb:tr.step.off_table].cpu())
