@@ -165,19 +165,29 @@ class BallScene:
         self.c = (torch.rand(n_balls, 3, generator=g) - 0.5) * (1.0 - 2 * self.r[:, None]).clamp(min=0)
         self.rgb = torch.rand(n_balls, 3, generator=g) * 0.8 + 0.1
 
+    @classmethod
+    def matching_grid(cls, seed=0, n_balls=12, radius=(0.065, 0.18)):
+        """The balls of synthetic.ball_density_grid(seed=seed) (the bench's calibrated occupancy)."""
+        sc = cls(n_balls=n_balls, seed=seed, radius=radius)
+        g = np.random.default_rng(seed)
+        sc.c = torch.from_numpy(g.uniform(-0.5 + radius[1], 0.5 - radius[1], size=(n_balls, 3))).float()
+        sc.r = torch.from_numpy(g.uniform(radius[0], radius[1], size=n_balls)).float()
+        return sc
+
     def render(self, o, d):
         o, d = o.double(), d.double()
+        c, r, rgb = (t.double().to(o.device) for t in (self.c, self.r, self.rgb))
         dn = d / d.norm(dim=-1, keepdim=True)
-        oc = o[:, None, :] - self.c.double()[None]                     # (N, B, 3)
+        oc = o[:, None, :] - c[None]                                   # (N, B, 3)
         b = (oc * dn[:, None, :]).sum(-1)
-        cc = (oc * oc).sum(-1) - self.r.double()[None] ** 2
+        cc = (oc * oc).sum(-1) - r[None] ** 2
         disc = b * b - cc
         t = -b - torch.sqrt(disc.clamp(min=0))
         t = torch.where((disc > 0) & (t > 0), t, torch.full_like(t, math.inf))
         tmin, idx = t.min(-1)
-        out = torch.ones(o.shape[0], 3, dtype=torch.float64)
+        out = torch.ones(o.shape[0], 3, dtype=torch.float64, device=o.device)
         hit = torch.isfinite(tmin)
-        out[hit] = self.rgb.double()[idx[hit]]
+        out[hit] = rgb[idx[hit]]
         return out.float()
 
     def density_grid(self, G=128, cascades=1):
@@ -186,16 +196,17 @@ class BallScene:
         return synthetic.balls_to_grid(self.c.numpy(), self.r.numpy(), G=G, cascades=cascades)
 
 
-def ball_scene_views(scene, n_views, W, focal, radius=1.5, seed=0):
+def ball_scene_views(scene, n_views, W, focal, radius=1.5, seed=0, device="cpu"):
     """n_views cameras on a sphere looking at the origin (synthetic.camera_poses), W x W pinhole
-    intrinsics, ground-truth images rendered analytically: (images (n, W*W, 3), poses (n,3,4),
-    directions (W*W, 3), K)."""
+    intrinsics, ground-truth images rendered analytically on `device`: (images (n, W*W, 3),
+    poses (n,3,4), directions (W*W, 3), K) -- images on `device`, the rest on the host."""
     from . import synthetic
     poses = synthetic.camera_poses(n_cams=n_views, seed=seed, radius=radius)
     K = torch.tensor([[focal, 0, W / 2], [0, focal, W / 2], [0, 0, 1]], dtype=torch.float32)
     dirs = get_ray_directions(W, W, K)
+    dd = dirs.to(device)
     imgs = []
     for p in poses:
-        o, d = get_rays(dirs, p)
+        o, d = get_rays(dd, p.to(device))
         imgs.append(scene.render(o, d))
     return torch.stack(imgs), poses, dirs, K
