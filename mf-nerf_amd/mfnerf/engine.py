@@ -50,6 +50,7 @@ class StepConfig:
     lr: float = 1e-2
     eps: float = 1e-15
     lambda_opacity: float = 1e-3
+    lambda_distortion: float = 0.0  # NeRFLoss(lambda_distortion) = --distortion_loss_w (losses.py:40-60)
     T_threshold: float = 1e-4
     max_samples: int = MAX_SAMPLES
     n_parts: int = 1
@@ -170,6 +171,12 @@ class TrainStep:
         t.dL_dop = torch.empty(Np, **f32)
         t.zeros_ray = torch.zeros(Np, **f32)       # dL/ddepth (unused by the loss)
         t.zeros_samp = torch.zeros(cap, **f32)     # dL/dws (no distortion loss by default)
+        if c.lambda_distortion > 0:                # losses.py:6-37 + 55-58
+            t.dist_loss = torch.empty(Np, **f32)
+            t.ws_incl = torch.empty(cap, **f32)
+            t.wts_incl = torch.empty(cap, **f32)
+            t.dL_ddist = torch.full((Np,), c.lambda_distortion / c.n_rays, **f32)  # d(lambda*mean)/dloss_r
+            t.dL_dws = torch.empty(cap, **f32)
         t.dsig = torch.empty(cap, **f32)
         t.drgb_s = torch.empty(cap, 3, **f32)
         t.dfeat = torch.empty(cap, c.L * c.F, **f32)
@@ -314,8 +321,16 @@ class TrainStep:
         bg = 1.0 if c.scale <= 0.5 else 0.0
         call("mfnerf_nerf_loss", ptr(t.rgb), ptr(t.opacity), ptr(batch.rgb[q * Np:(q + 1) * Np]), Np, c.n_rays,
              c.lambda_opacity, bg, bg, bg, ptr(t.dL_drgb), ptr(t.dL_dop), ptr(self.loss_sum), s)
+        dL_dws = t.zeros_samp
+        if c.lambda_distortion > 0:
+            call("mfnerf_distortion_loss_fw", ptr(t.ws), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a), Np, cap,
+                 ptr(t.dist_loss), ptr(t.ws_incl), ptr(t.wts_incl), s)
+            self.loss_sum.add_(t.dist_loss.sum() * (c.lambda_distortion / c.n_rays))
+            call("mfnerf_distortion_loss_bw", ptr(t.dL_ddist), ptr(t.ws_incl), ptr(t.wts_incl), ptr(t.ws),
+                 ptr(m.deltas), ptr(m.ts), ptr(m.rays_a), Np, cap, ptr(t.dL_dws), s)
+            dL_dws = t.dL_dws
         mark("composite_fw")
-        call("mfnerf_composite_train_bw", ptr(t.dL_dop), ptr(t.zeros_ray), ptr(t.dL_drgb), ptr(t.zeros_samp),
+        call("mfnerf_composite_train_bw", ptr(t.dL_dop), ptr(t.zeros_ray), ptr(t.dL_drgb), ptr(dL_dws),
              ptr(t.sigma), ptr(t.rgb_s), ptr(t.ws), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a), ptr(t.opacity),
              ptr(t.depth), ptr(t.rgb), Np, cap, c.T_threshold, ptr(t.dsig), ptr(t.drgb_s), s)
         mark("composite_bw")

@@ -66,14 +66,14 @@ def psnr(pred, gt):
 
 class Trainer:
     def __init__(self, hp: HParams, train, device="cuda", rank=0, world=1, graphs=True):
-        if hp.distortion_loss_w != 0 or hp.random_bg:
-            raise NotImplementedError("the fused step trains with distortion_loss_w=0 and a fixed background")
+        if hp.random_bg:
+            raise NotImplementedError("the fused step trains with a fixed background (random_bg off)")
         if hp.rgb_layers != 2:
             raise NotImplementedError("the fused field head implements rgb_layers=2")
         self.hp, self.train = hp, train
         cfg = engine.StepConfig(n_rays=hp.batch_size, scale=hp.scale, L=hp.L, F=hp.F, log2_T=hp.T, N_min=hp.N_min,
                                 N_max=hp.N_max, grid=hp.grid, N_tables=hp.N_tables, rgb_width=hp.rgb_channels,
-                                lr=hp.lr)
+                                lr=hp.lr, lambda_distortion=hp.distortion_loss_w)
         self.step = engine.TrainStep(cfg, device=device, seed=hp.seed)
         if world > 1:
             self.step.shard_optimizer(rank, world)

@@ -78,3 +78,29 @@ def test_parts_sum_to_the_whole_batch(gpu):
         assert abs(loss - out[0][0]) <= 1e-5 * abs(out[0][0])
         tol = 1e-4 * float(out[0][1].abs().max())
         assert torch.allclose(g, out[0][1], rtol=1e-3, atol=tol)
+
+
+def test_distortion_loss_in_the_fused_step(gpu, oracle):
+    """--distortion_loss_w > 0: the step adds lambda*mean(distortion) to the loss and feeds its
+    dL/dws into the compositing backward (losses.py:55-58), per part, checked against the oracle."""
+    lam = 1e-2
+    st = engine.TrainStep(engine.StepConfig(n_rays=512, log2_T=16, n_parts=2, lambda_distortion=lam), device=gpu)
+    st.set_occupancy(synthetic.ball_density_grid())
+    ref = engine.TrainStep(engine.StepConfig(n_rays=512, log2_T=16, n_parts=2), device=gpu)
+    ref.set_occupancy(synthetic.ball_density_grid())
+    batch = st.make_batches(1, seed=4)[0]
+    st.run(batch)
+    ref.run(batch)
+    torch.cuda.synchronize()
+    dist_total = 0.0
+    cpu = lambda x: x.detach().cpu()  # noqa: E731
+    for q, t in enumerate(st.parts):
+        m = st.state.march.part[q]
+        n = int(st.state.counters[q, 0])
+        loss, wsi, wtsi = oracle.distortion_loss_fw(cpu(t.ws[:n]), cpu(m.deltas[:n]), cpu(m.ts[:n]), cpu(m.rays_a))
+        dist_total += float(loss.sum())
+        g = oracle.distortion_loss_bw(torch.full((st.Np,), lam / 512), wsi, wtsi, cpu(t.ws[:n]), cpu(m.deltas[:n]),
+                                      cpu(m.ts[:n]), cpu(m.rays_a))
+        assert torch.allclose(cpu(t.dL_dws[:n]), g, rtol=1e-4, atol=1e-9)
+    # same params, noise and batch in both steps: the losses differ by exactly the distortion term
+    assert abs(float(st.loss_sum) - float(ref.loss_sum) - lam * dist_total / 512) <= 1e-5 * float(st.loss_sum)
