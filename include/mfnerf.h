@@ -99,6 +99,19 @@ int mfnerf_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, 
                               const float* depth, const float* rgb, int64_t n_rays, int64_t n_samples,
                               float T_threshold, float* dL_dsigmas, float* dL_drgbs, mfnerf_stream_t stream);
 
+/* Fused training compositing for the default loss (no distortion term): mfnerf_composite_train_fw,
+ * mfnerf_nerf_loss (target, n_mean, lambda_opacity, bg) and mfnerf_composite_train_bw with
+ * dL_ddepth = 0, dL_dws = 0 in one pass (one wave per ray); the same outputs as the three calls,
+ * bit-identical.  loss_slots (optional, 64 device f32) ACCUMULATES the loss value spread over 64
+ * partial sums (their sum is the loss).  Replaces the chain at rendering.py:121-163 + losses.py:47-60
+ * + custom_functions.py:148-159 in one training step. */
+int mfnerf_composite_train_fused(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
+                                 const int64_t* rays_a, int64_t n_rays, int64_t n_samples, float T_threshold,
+                                 const float* target, int64_t n_mean, float lambda_opacity, float bg_r, float bg_g,
+                                 float bg_b, int64_t* total_samples, float* opacity, float* depth, float* rgb,
+                                 float* ws, float* dL_drgb, float* dL_dopacity, float* dL_dsigmas, float* dL_drgbs,
+                                 float* loss_slots, mfnerf_stream_t stream);
+
 /* vren.composite_test_fw (binding.cpp:176-201, volumerendering.cu:205-285).  sigmas (n_alive,N_samples),
  * rgbs (n_alive,N_samples,3), deltas, ts (n_alive,N_samples); in place on alive_indices, opacity,
  * depth, rgb (indexed by ray). */

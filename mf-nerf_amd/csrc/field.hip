@@ -158,18 +158,32 @@ struct FwdTile {
     float rgb[3];    // sigmoid outputs on lanes h==0 (fp32)
 };
 
-template <bool DENSITY_ONLY>
-__device__ __forceinline__ void forward_tile(const _Float16* lds, int lane, const _Float16* __restrict__ feat,
-                                             const float* __restrict__ dirs, int64_t s, bool valid, FwdTile& T) {
-    const int h = lane >> 5;
-    const f32x16 z = {};
+// Loads of one tile's inputs (feature row halves for this lane, direction), used directly or as
+// the next tile's prefetch.
+struct TileIn {
+    half8 x[2];
+    float d[3];
+};
+
+__device__ __forceinline__ void load_tile_in(const _Float16* __restrict__ feat, const float* __restrict__ dirs,
+                                             int64_t s, bool valid, int h, bool want_dirs, TileIn& I) {
     if (valid) {
         const half8* row = reinterpret_cast<const half8*>(feat + s * 32);
-        T.x[0] = row[h];
-        T.x[1] = row[2 + h];
+        I.x[0] = row[h];
+        I.x[1] = row[2 + h];
+        if (want_dirs) { I.d[0] = dirs[3 * s]; I.d[1] = dirs[3 * s + 1]; I.d[2] = dirs[3 * s + 2]; }
     } else {
-        T.x[0] = half8{}; T.x[1] = half8{};
+        I.x[0] = half8{}; I.x[1] = half8{};
+        I.d[0] = I.d[1] = I.d[2] = 0.0f;
     }
+}
+
+template <bool DENSITY_ONLY>
+__device__ __forceinline__ void forward_tile(const _Float16* lds, int lane, const TileIn& I, bool valid, FwdTile& T) {
+    const int h = lane >> 5;
+    const f32x16 z = {};
+    T.x[0] = I.x[0];
+    T.x[1] = I.x[1];
     // xyz layer 1: Y1^T = W1 X^T
     f32x16 y1a = mfma(lds_frag(lds, F1 + 0, lane), T.x[0], z);
     y1a = mfma(lds_frag(lds, F1 + 1, lane), T.x[1], y1a);
@@ -186,7 +200,7 @@ __device__ __forceinline__ void forward_tile(const _Float16* lds, int lane, cons
     T.h0 = (float)T.hb[0];        // row 0 on lanes h==0
     if (DENSITY_ONLY) return;
     float shv[16];
-    if (valid) sh4(dirs[3 * s], dirs[3 * s + 1], dirs[3 * s + 2], shv);
+    if (valid) sh4(I.d[0], I.d[1], I.d[2], shv);
     else {
 #pragma unroll
         for (int i = 0; i < 16; ++i) shv[i] = 0.0f;
@@ -244,8 +258,10 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_fw_kernel(const _Float16* _
     for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile < tiles; tile += (int64_t)gridDim.x * 4) {
         const int64_t s = tile * 32 + r;
         const bool valid = s < nn;
+        TileIn I;
+        load_tile_in(feat, dirs, s, valid, h, !DENSITY_ONLY, I);
         FwdTile T;
-        forward_tile<DENSITY_ONLY>(lds, lane, feat, dirs, s, valid, T);
+        forward_tile<DENSITY_ONLY>(lds, lane, I, valid, T);
         if (valid && h == 0) {
             sigma[s] = __expf(T.h0);  // TruncExp forward (custom_functions.py:166)
             if (!DENSITY_ONLY) {
@@ -259,46 +275,73 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_fw_kernel(const _Float16* _
 }
 
 // ---------------------------------------------------------------- backward
+//
+// Data gradients chain through accumulators exactly like the forward ("T" orientation: channel on
+// the MFMA row, sample on the lane).  Weight gradients dW = dY^T X reduce over SAMPLES, which must
+// therefore sit in the MFMA K dimension, i.e. inside each lane's registers -- the transpose of the
+// T operands.  That transpose runs on the matrix core: D = Top x I (A = a T operand, B = an
+// identity fragment) is the "S" orientation (sample on the row, channel on the lane), and an S
+// accumulator packed to f16 IS an operand with K = samples.  Exact (products with 1.0, one
+// non-zero term per output), no LDS round trip, no wave-level synchronisation.
+//   dW[out][in] (32x32 tile) += S(dY)[out-tile] x S(X)[in-tile], K = the tile's 32 samples (2 MFMAs)
 
-constexpr int TP_STRIDE = 40;  // halfs per LDS transpose row (32 samples + 8 pad: 80 B)
+// identity B fragments, appended after the weight fragments in LDS: ID_BASE + 2*perm + (off/16)
+constexpr int ID_BASE = N_FRAGS;
+constexpr int ID_N0 = ID_BASE, ID_N16 = ID_BASE + 1, ID_P0 = ID_BASE + 2, ID_P16 = ID_BASE + 3;
+constexpr int N_FRAGS_BW = N_FRAGS + 4;
 
-// write an accumulator tile (rows = channels 32*mt + (i&3)+8(i>>2)+4h, col = sample r) as f16 [ch][sample]
-template <int I0, int I1>
-__device__ __forceinline__ void tp_store_acc(_Float16* buf, const f32x16& a, int ch0, int r, int h) {
+__device__ __forceinline__ void load_frags_bw(_Float16* lds, const _Float16* __restrict__ packed) {
+    const uint4* src = reinterpret_cast<const uint4*>(packed);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    for (int i = threadIdx.x; i < N_FRAGS * 64; i += blockDim.x) dst[i] = src[i];
+    // identity: lane (n = lane&31, h), element j = 1 iff off + k_of(j, h, perm) == n
+    for (int i = threadIdx.x; i < 4 * 64; i += blockDim.x) {
+        const int fi = i >> 6, ln = i & 63, nn = ln & 31, hh = ln >> 5;
+        const int perm = fi >> 1, off = 16 * (fi & 1);
+        half8 v;
 #pragma unroll
-    for (int i = I0; i < I1; ++i) buf[(ch0 + (i & 3) + 8 * (i >> 2) + 4 * h) * TP_STRIDE + r] = (_Float16)a[i];
-}
-// write a packed operand (element j = channel kbase + k_of(j,h,perm)) as [ch][sample]
-__device__ __forceinline__ void tp_store_op(_Float16* buf, const half8& v, int kbase, int perm, int r, int h) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) buf[(kbase + k_of(j, h, perm)) * TP_STRIDE + r] = v[j];
-}
-__device__ __forceinline__ half8 tp_frag(const _Float16* buf, int row0, int q, int lane) {
-    const int r = lane & 31, h = lane >> 5;
-    return *reinterpret_cast<const half8*>(buf + (row0 + r) * TP_STRIDE + 16 * q + 8 * h);
-}
-__device__ __forceinline__ void lds_sync_wave() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int j = 0; j < 8; ++j) v[j] = (_Float16)((off + k_of(j, hh, perm) == nn) ? 1.0f : 0.0f);
+        *reinterpret_cast<half8*>(lds + ((ID_BASE + fi) * 64 + ln) * 8) = v;
+    }
+    __syncthreads();
 }
 
-// dW tile accumulate with v_mfma_f32_16x16x32_f16 (K = the tile's 32 samples in one instruction):
-// acc[16x16] += A(buf_a rows 16*MT.., samples) x B(buf_b rows 16*NT.., samples)^T
-__device__ __forceinline__ half8 tp_frag16(const _Float16* buf, int row0, int lane) {
-    return *reinterpret_cast<const half8*>(buf + (row0 + (lane & 15)) * TP_STRIDE + 8 * (lane >> 4));
+// S operands (K = samples 0..15 / 16..31 of the tile) of one 32-channel tile given as two T chunks
+struct SOp { half8 k[2]; };
+
+__device__ __forceinline__ SOp to_s(const _Float16* lds, int lane, const half8& lo, int lo_id, const half8& hi,
+                                    int hi_id) {
+    const f32x16 z = {};
+    f32x16 a = mfma(lo, lds_frag(lds, lo_id, lane), z);
+    a = mfma(hi, lds_frag(lds, hi_id, lane), a);
+    SOp o;
+    o.k[0] = pack8<0, false>(a);
+    o.k[1] = pack8<8, false>(a);
+    return o;
 }
-#define DW16(ACC, BA, MT, BB, NT) \
-    ACC = __builtin_amdgcn_mfma_f32_16x16x32_f16(tp_frag16(BA, 16 * (MT), lane), tp_frag16(BB, 16 * (NT), lane), ACC, 0, 0, 0)
+// a tile with only its low 16 channels present (the 16-wide layer outputs)
+__device__ __forceinline__ SOp to_s16(const _Float16* lds, int lane, const half8& lo, int lo_id) {
+    const f32x16 z = {};
+    const f32x16 a = mfma(lo, lds_frag(lds, lo_id, lane), z);
+    SOp o;
+    o.k[0] = pack8<0, false>(a);
+    o.k[1] = pack8<8, false>(a);
+    return o;
+}
+__device__ __forceinline__ void dw_acc(f32x16& acc, const SOp& dy, const SOp& x) {
+    acc = mfma(dy.k[0], x.k[0], acc);
+    acc = mfma(dy.k[1], x.k[1], acc);
+}
 
 constexpr int N_DW = N_XYZ_PARAMS + N_RGB_PARAMS;  // 10240 floats per slab row
 
-// add one 16x16 dW tile (D row = 4*(lane>>4)+i, col = lane&15) into a row-major fp32 LDS image
-__device__ __forceinline__ void dw_add16(float* img, const f32x4& a, int mt, int nt, int rows, int cols, int lane) {
-    const int col = 16 * nt + (lane & 15);
+// add one 32x32 dW tile (row = out 32*ot + (i&3)+8(i>>2)+4h, col = in 32*it + lane&31) into a
+// row-major fp32 LDS image of a (rows x cols) matrix
+__device__ __forceinline__ void dw_add32(float* img, const f32x16& a, int ot, int it, int rows, int cols, int lane) {
+    const int col = 32 * it + (lane & 31), h = lane >> 5;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int row = 16 * mt + 4 * (lane >> 4) + i;
+    for (int i = 0; i < 16; ++i) {
+        const int row = 32 * ot + (i & 3) + 8 * (i >> 2) + 4 * h;
         if (row < rows && col < cols) atomicAdd(img + row * cols + col, a[i]);
     }
 }
@@ -308,40 +351,50 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
     const _Float16* __restrict__ packed, const float* __restrict__ dL_dsigma, const float* __restrict__ dL_drgb,
     float grad_scale, float* __restrict__ dL_dfeat, float* __restrict__ slab) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    _Float16* lds = reinterpret_cast<_Float16*>(smem);
-    load_frags(lds, packed, N_FRAGS);
+    _Float16* lds_base = reinterpret_cast<_Float16*>(smem);
+    load_frags_bw(lds_base, packed);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
-    // per-wave transpose buffers: A (64 ch x 40) and B (64 ch x 40) f16
-    _Float16* ta = lds + N_FRAGS * FRAG_HALFS + wid * (2 * 64 * TP_STRIDE);
-    _Float16* tb = ta + 64 * TP_STRIDE;
     const float S = grad_scale, invS = 1.0f / grad_scale;
     const f32x16 z = {};
-    // persistent weight-gradient accumulators, 16x16 tiles [m-tile][n-tile] (160 registers)
-    f32x4 dw1[4][2], dw2[4], dwr1[4][2], dwr2[4][4], dwr3[4];
+    // persistent weight-gradient accumulators, 32x32 tiles [out-tile][in-tile] (192 registers)
+    f32x16 dw1[2], dw2[2], dwr1[2], dwr2[2][2], dwr3[2];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-        dw2[a] = f32x4{}; dwr3[a] = f32x4{};
-#pragma unroll
-        for (int b = 0; b < 2; ++b) { dw1[a][b] = f32x4{}; dwr1[a][b] = f32x4{}; }
-#pragma unroll
-        for (int b = 0; b < 4; ++b) dwr2[a][b] = f32x4{};
+    for (int a = 0; a < 2; ++a) {
+        dw1[a] = z; dw2[a] = z; dwr1[a] = z; dwr3[a] = z; dwr2[a][0] = z; dwr2[a][1] = z;
     }
 
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     const int64_t tiles = div_up<int64_t>(nn, 32);
-    for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile < tiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t stride = (int64_t)gridDim.x * 4;
+    // the next tile's inputs are loaded while this tile computes
+    TileIn nI;
+    float ngs = 0.f, ng0 = 0.f, ng1 = 0.f, ng2 = 0.f;
+    auto fetch = [&](int64_t tile) {
+        const int64_t s = tile * 32 + r;
+        const bool v = s < nn;
+        load_tile_in(feat, dirs, s, v, h, true, nI);
+        ngs = ng0 = ng1 = ng2 = 0.0f;
+        if (v && h == 0) {
+            ngs = dL_dsigma[s];
+            ng0 = dL_drgb[3 * s]; ng1 = dL_drgb[3 * s + 1]; ng2 = dL_drgb[3 * s + 2];
+        }
+    };
+    const int64_t tile0 = (int64_t)blockIdx.x * 4 + wid;
+    if (tile0 < tiles) fetch(tile0);
+    for (int64_t tile = tile0; tile < tiles; tile += stride) {
+        // the fragment reads are loop-invariant; an opaque base keeps the compiler from hoisting
+        // all 48 of them (192 registers) out of the loop
+        int opaque = 0;
+        asm volatile("" : "+s"(opaque));
+        const _Float16* lds = lds_base + opaque;
         const int64_t s = tile * 32 + r;
         const bool valid = s < nn;
+        const TileIn I = nI;
+        const float gs = ngs, g0 = ng0, g1 = ng1, g2 = ng2;
+        if (tile + stride < tiles) fetch(tile + stride);
         FwdTile T;
-        forward_tile<false>(lds, lane, feat, dirs, s, valid, T);
-        float gs = 0.0f, g0 = 0.0f, g1 = 0.0f, g2 = 0.0f;
-        if (valid && h == 0) {
-            gs = dL_dsigma[s];
-            g0 = dL_drgb[3 * s]; g1 = dL_drgb[3 * s + 1]; g2 = dL_drgb[3 * s + 2];
-        }
-        // Layer by layer, each weight gradient right after its data gradient, so at most two dY
-        // tiles are live next to the 12 persistent dW accumulators.
+        forward_tile<false>(lds, lane, I, valid, T);
         // -- rgb layer 3: dO (rows 0..2 on lanes h==0) = dL/drgb * sigmoid'
         f32x16 dO = z;
         if (h == 0) {
@@ -350,14 +403,11 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
             dO[2] = g2 * S * T.rgb[2] * (1.0f - T.rgb[2]);
         }
         const half8 dOb = pack8<0, false>(dO);
-        //    dWr3 (16xW) += dO^T R2   (A rows 0..31 of dO: rows >= 3 are zero)
-        tp_store_acc<0, 16>(ta, dO, 0, r, h);
-        tp_store_op(tb, T.r2[0][0], 0, 1, r, h); tp_store_op(tb, T.r2[0][1], 16, 1, r, h);
-        tp_store_op(tb, T.r2[1][0], 32, 1, r, h); tp_store_op(tb, T.r2[1][1], 48, 1, r, h);
-        lds_sync_wave();
-        #pragma unroll
-        for (int b = 0; b < 4; ++b) DW16(dwr3[b], ta, 0, tb, b);
-        lds_sync_wave();
+        {   // dWr3 (16 x W) += dO^T R2
+            const SOp d = to_s16(lds, lane, dOb, ID_P0);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) dw_acc(dwr3[t], d, to_s(lds, lane, T.r2[t][0], ID_P0, T.r2[t][1], ID_P16));
+        }
         //    dR2 = Wr3^T dO, masked by R2 > 0
         half8 dr2p[2][2];
         {
@@ -368,17 +418,16 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
             dr2p[0][0] = pack8<0, false>(a0); dr2p[0][1] = pack8<8, false>(a0);
             dr2p[1][0] = pack8<0, false>(a1); dr2p[1][1] = pack8<8, false>(a1);
         }
-        // -- rgb layer 2: dWr2 (WxW) += dR2^T R1
-        tp_store_op(ta, dr2p[0][0], 0, 1, r, h); tp_store_op(ta, dr2p[0][1], 16, 1, r, h);
-        tp_store_op(ta, dr2p[1][0], 32, 1, r, h); tp_store_op(ta, dr2p[1][1], 48, 1, r, h);
-        tp_store_op(tb, T.r1[0][0], 0, 1, r, h); tp_store_op(tb, T.r1[0][1], 16, 1, r, h);
-        tp_store_op(tb, T.r1[1][0], 32, 1, r, h); tp_store_op(tb, T.r1[1][1], 48, 1, r, h);
-        lds_sync_wave();
+        {   // -- rgb layer 2: dWr2 (WxW) += dR2^T R1
+            const SOp x0 = to_s(lds, lane, T.r1[0][0], ID_P0, T.r1[0][1], ID_P16);
+            const SOp x1 = to_s(lds, lane, T.r1[1][0], ID_P0, T.r1[1][1], ID_P16);
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) DW16(dwr2[a][b], ta, a, tb, b);
-        lds_sync_wave();
+            for (int o = 0; o < 2; ++o) {
+                const SOp d = to_s(lds, lane, dr2p[o][0], ID_P0, dr2p[o][1], ID_P16);
+                dw_acc(dwr2[o][0], d, x0);
+                dw_acc(dwr2[o][1], d, x1);
+            }
+        }
         //    dR1 = Wr2^T dR2, masked by R1 > 0
         half8 dr1p[2][2];
         {
@@ -395,16 +444,11 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
             dr1p[0][0] = pack8<0, false>(a0); dr1p[0][1] = pack8<8, false>(a0);
             dr1p[1][0] = pack8<0, false>(a1); dr1p[1][1] = pack8<8, false>(a1);
         }
-        // -- rgb layer 1: dWr1 (Wx32) += dR1^T [SH;h]
-        tp_store_op(ta, dr1p[0][0], 0, 1, r, h); tp_store_op(ta, dr1p[0][1], 16, 1, r, h);
-        tp_store_op(ta, dr1p[1][0], 32, 1, r, h); tp_store_op(ta, dr1p[1][1], 48, 1, r, h);
-        tp_store_op(tb, T.sh, 0, 0, r, h); tp_store_op(tb, T.hb, 16, 1, r, h);
-        lds_sync_wave();
-        #pragma unroll
-        for (int a = 0; a < 4; ++a)
+        {   // -- rgb layer 1: dWr1 (Wx32) += dR1^T [SH;h]   (SH natural order, h perm order)
+            const SOp x = to_s(lds, lane, T.sh, ID_N0, T.hb, ID_P16);
 #pragma unroll
-            for (int b = 0; b < 2; ++b) DW16(dwr1[a][b], ta, a, tb, b);
-        lds_sync_wave();
+            for (int o = 0; o < 2; ++o) dw_acc(dwr1[o], to_s(lds, lane, dr1p[o][0], ID_P0, dr1p[o][1], ID_P16), x);
+        }
         //    d[SH;h] = Wr1^T dR1 (rows 16..31 = dh) + TruncExp backward into h[0]
         half8 dhb;
         {
@@ -417,15 +461,11 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
             if (h == 0) dsh[8] += gs * S * __expf(fminf(fmaxf(T.h0, -15.0f), 15.0f));
             dhb = pack8<8, false>(dsh);
         }
-        // -- xyz layer 2: dW2 (16x64) += dh^T Y1 (A rows 0..15 = dh, rows 16..31 = 0)
-        tp_store_op(ta, dhb, 0, 1, r, h);
-        tp_store_op(ta, half8{}, 16, 1, r, h);
-        tp_store_op(tb, T.y1[0][0], 0, 1, r, h); tp_store_op(tb, T.y1[0][1], 16, 1, r, h);
-        tp_store_op(tb, T.y1[1][0], 32, 1, r, h); tp_store_op(tb, T.y1[1][1], 48, 1, r, h);
-        lds_sync_wave();
-        #pragma unroll
-        for (int b = 0; b < 4; ++b) DW16(dw2[b], ta, 0, tb, b);
-        lds_sync_wave();
+        {   // -- xyz layer 2: dW2 (16x64) += dh^T Y1
+            const SOp d = to_s16(lds, lane, dhb, ID_P0);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) dw_acc(dw2[t], d, to_s(lds, lane, T.y1[t][0], ID_P0, T.y1[t][1], ID_P16));
+        }
         //    dY1 = W2^T dh, masked by Y1 > 0
         half8 dy1p[2][2];
         {
@@ -436,16 +476,11 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
             dy1p[0][0] = pack8<0, false>(a0); dy1p[0][1] = pack8<8, false>(a0);
             dy1p[1][0] = pack8<0, false>(a1); dy1p[1][1] = pack8<8, false>(a1);
         }
-        // -- xyz layer 1: dW1 (64x32) += dY1^T X
-        tp_store_op(ta, dy1p[0][0], 0, 1, r, h); tp_store_op(ta, dy1p[0][1], 16, 1, r, h);
-        tp_store_op(ta, dy1p[1][0], 32, 1, r, h); tp_store_op(ta, dy1p[1][1], 48, 1, r, h);
-        tp_store_op(tb, T.x[0], 0, 0, r, h); tp_store_op(tb, T.x[1], 16, 0, r, h);
-        lds_sync_wave();
-        #pragma unroll
-        for (int a = 0; a < 4; ++a)
+        {   // -- xyz layer 1: dW1 (64x32) += dY1^T X   (X natural order)
+            const SOp x = to_s(lds, lane, T.x[0], ID_N0, T.x[1], ID_N16);
 #pragma unroll
-            for (int b = 0; b < 2; ++b) DW16(dw1[a][b], ta, a, tb, b);
-        lds_sync_wave();
+            for (int o = 0; o < 2; ++o) dw_acc(dw1[o], to_s(lds, lane, dy1p[o][0], ID_P0, dy1p[o][1], ID_P16), x);
+        }
         //    dX = W1^T dY1 -> global fp32 (features (i&3)+8(i>>2)+4h)
         {
             f32x16 dx = z;
@@ -465,7 +500,7 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
 
     // ---- block reduction of the per-wave dW partials into an fp32 LDS image, then one slab row
     __syncthreads();
-    float* img = reinterpret_cast<float*>(smem);  // reuses the fragment area (N_DW*4 <= frags+buffers)
+    float* img = reinterpret_cast<float*>(smem);  // reuses the fragment area (N_DW*4 <= fragments)
     for (int i = threadIdx.x; i < N_DW; i += blockDim.x) img[i] = 0.0f;
     __syncthreads();
     float* ix = img;
@@ -473,16 +508,13 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
     float* ir2 = ir + RGB_W * 32;
     float* ir3 = ir2 + RGB_W * RGB_W;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-        dw_add16(ix + 64 * 32, dw2[a], 0, a, 16, 64, lane);
-        dw_add16(ir3, dwr3[a], 0, a, 16, RGB_W, lane);
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            dw_add16(ix, dw1[a][b], a, b, 64, 32, lane);
-            dw_add16(ir, dwr1[a][b], a, b, RGB_W, 32, lane);
-        }
-#pragma unroll
-        for (int b = 0; b < 4; ++b) dw_add16(ir2, dwr2[a][b], a, b, RGB_W, RGB_W, lane);
+    for (int a = 0; a < 2; ++a) {
+        dw_add32(ix, dw1[a], a, 0, 64, 32, lane);
+        dw_add32(ix + 64 * 32, dw2[a], 0, a, 16, 64, lane);
+        dw_add32(ir, dwr1[a], a, 0, RGB_W, 32, lane);
+        dw_add32(ir2, dwr2[a][0], a, 0, RGB_W, RGB_W, lane);
+        dw_add32(ir2, dwr2[a][1], a, 1, RGB_W, RGB_W, lane);
+        dw_add32(ir3, dwr3[a], 0, a, 16, RGB_W, lane);
     }
     __syncthreads();
     float* row = slab + (int64_t)blockIdx.x * N_DW;
@@ -508,7 +540,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 }
 
 constexpr int BW_BLOCKS = 256;
-constexpr size_t BW_LDS = (size_t)N_FRAGS * FRAG_HALFS * 2 + 4 * 2 * 64 * TP_STRIDE * 2;
+constexpr size_t BW_LDS = (size_t)N_FRAGS_BW * FRAG_HALFS * 2;
 static_assert((size_t)N_DW * 4 <= BW_LDS, "reduction image must fit the bw LDS");
 
 // debug: one MFMA with A (32x16) and B (16x32) f16 row-major -> D (32x32) f32, to pin the lane maps

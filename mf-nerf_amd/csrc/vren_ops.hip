@@ -468,6 +468,119 @@ __global__ __launch_bounds__(256) void composite_bw_wave_kernel(
     }
 }
 
+// Fused training compositing for the default loss (no distortion term): composite_train_fw ->
+// background blend + NeRFLoss and its gradient -> composite_train_bw with dL/ddepth = 0 and
+// dL/dws = 0, one wave per ray, one launch.  Pass 1 is composite_fw_wave_kernel's loop and also
+// stores each sample's post-sample transmittance into dL_dsigmas (as scratch); pass 2 reads w and
+// T back (same lane, same address) instead of re-walking the transmittance chain, so the result is
+// bit-identical to the three separate kernels (the dropped terms are exact zeros).  The loss value
+// goes to 64 partial sums (loss_slots[blockIdx % 64]) to spread the atomics.
+constexpr int LOSS_SLOTS = 64;
+
+__global__ __launch_bounds__(256) void composite_fused_wave_kernel(
+    const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
+    const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t n_rays, float T_thr,
+    const float* __restrict__ target, int64_t n_mean, float lambda_o, float bg0, float bg1, float bg2,
+    int64_t* __restrict__ total_samples, float* __restrict__ opacity, float* __restrict__ depth,
+    float* __restrict__ rgb, float* __restrict__ ws, float* __restrict__ dL_drgb, float* __restrict__ dL_dop,
+    float* __restrict__ dL_dsigmas, float* __restrict__ dL_drgbs, float* __restrict__ loss_slots) {
+    __shared__ float lsum[4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t n = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    float l = 0.0f;
+    if (n < n_rays) {
+        const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
+        const int N = (int)rays_a[3 * n + 2];
+        // ---- pass 1: forward (composite_fw_wave_kernel)
+        float T = 1.0f, R = 0.f, G = 0.f, B = 0.f, D = 0.f, O = 0.f;
+        int total = N;
+        bool ended = false;
+        for (int k0 = 0; k0 < N; k0 += 64) {
+            const int nv = min(64, N - k0);
+            const int64_t s = start + k0 + lane;
+            const bool valid = lane < nv;
+            float w = 0.0f, tn = 0.0f;
+            if (!ended) {
+                const float a = valid ? 1.0f - fast_exp(-sigmas[s] * deltas[s]) : 0.0f;
+                int stop;
+                const float myT = t_chain(a, T, T_thr, lane, nv, &stop);
+                if (valid && lane <= stop) {
+                    w = a * myT;
+                    tn = myT * (1.0f - a);
+                    R = fmaf(w, rgbs[3 * s], R); G = fmaf(w, rgbs[3 * s + 1], G); B = fmaf(w, rgbs[3 * s + 2], B);
+                    D = fmaf(w, ts[s], D);
+                    O += w;
+                }
+                if (stop < 64) { ended = true; total = k0 + stop; }
+            }
+            if (valid) { ws[s] = w; dL_dsigmas[s] = tn; }
+        }
+        R = wave_sum(R); G = wave_sum(G); B = wave_sum(B); D = wave_sum(D); O = wave_sum(O);
+        // ---- loss (nerf_loss_kernel, same expression order), wave-uniform
+        const float inv3n = 1.0f / (3.0f * (float)n_mean), invn = 1.0f / (float)n_mean;
+        const float bg[3] = {bg0, bg1, bg2}, col[3] = {R, G, B};
+        float gcol[3], dop = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float e = col[c] + bg[c] * (1.0f - O) - target[3 * ray + c];
+            l += e * e * inv3n;
+            gcol[c] = 2.0f * e * inv3n;
+            dop -= bg[c] * gcol[c];
+        }
+        const float o = O + 1e-10f;
+        l += lambda_o * (-o * logf(o)) * invn;
+        const float go = dop + lambda_o * (-(logf(o) + 1.0f)) * invn;
+        if (lane == 0) {
+            opacity[ray] = O; depth[ray] = D;
+            rgb[3 * ray] = R; rgb[3 * ray + 1] = G; rgb[3 * ray + 2] = B;
+            total_samples[ray] = total;
+            dL_drgb[3 * ray] = gcol[0]; dL_drgb[3 * ray + 1] = gcol[1]; dL_drgb[3 * ray + 2] = gcol[2];
+            dL_dop[ray] = go;
+        }
+        // ---- pass 2: backward (composite_bw_wave_kernel with dL_ddepth = dL_dws = 0)
+        const int last = ended ? total : N - 1;  // the last accumulated sample
+        const float gr = gcol[0], gg = gcol[1], gb = gcol[2];
+        float cr = 0.f, cg = 0.f, cb = 0.f;
+        for (int k0 = 0; k0 < N; k0 += 64) {
+            const int64_t s = start + k0 + lane;
+            const bool valid = k0 + lane < N;
+            const bool act = k0 + lane <= last;
+            if (k0 > last) {  // after termination: zero gradients
+                if (valid) {
+                    dL_dsigmas[s] = 0.0f;
+                    dL_drgbs[3 * s] = 0.0f; dL_drgbs[3 * s + 1] = 0.0f; dL_drgbs[3 * s + 2] = 0.0f;
+                }
+                continue;
+            }
+            float w = 0.f, tn = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f, dl = 0.f;
+            if (act) {
+                w = ws[s]; tn = dL_dsigmas[s]; dl = deltas[s];
+                c0 = rgbs[3 * s]; c1 = rgbs[3 * s + 1]; c2 = rgbs[3 * s + 2];
+            }
+            const float pr = wave_incl_scan(w * c0, lane) + cr, pg = wave_incl_scan(w * c1, lane) + cg;
+            const float pb = wave_incl_scan(w * c2, lane) + cb;
+            cr = readlane_f(pr, 63); cg = readlane_f(pg, 63); cb = readlane_f(pb, 63);
+            float dsig = 0.0f, d0 = 0.0f, d1 = 0.0f, d2 = 0.0f;
+            if (act) {
+                d0 = gr * w; d1 = gg * w; d2 = gb * w;
+                float acc = gr * fmaf(c0, tn, -(R - pr));
+                acc = fmaf(gg, fmaf(c1, tn, -(G - pg)), acc);
+                acc = fmaf(gb, fmaf(c2, tn, -(B - pb)), acc);
+                acc = fmaf(go, 1 - O, acc);
+                dsig = dl * acc;
+            }
+            if (valid) {
+                dL_dsigmas[s] = dsig;
+                dL_drgbs[3 * s] = d0; dL_drgbs[3 * s + 1] = d1; dL_drgbs[3 * s + 2] = d2;
+            }
+        }
+    }
+    if (lane == 0) lsum[wid] = l;
+    __syncthreads();
+    if (threadIdx.x == 0 && loss_slots)
+        atomicAdd(loss_slots + (blockIdx.x & (LOSS_SLOTS - 1)), (lsum[0] + lsum[1]) + (lsum[2] + lsum[3]));
+}
+
 __global__ void composite_test_kernel(const float* __restrict__ sigmas, const float* __restrict__ rgbs,
                                       const float* __restrict__ deltas, const float* __restrict__ ts,
                                       int64_t* __restrict__ alive, int64_t n_alive, int N_samples, float T_thr,
@@ -704,6 +817,27 @@ int mfnerf_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, 
                        dL_dopacity, dL_ddepth, dL_drgb, dL_dws, sigmas, rgbs, ws, deltas, ts, rays_a, opacity,
                        depth, rgb, n_rays, T_threshold, dL_dsigmas, dL_drgbs);
     return mfn_check_launch("composite_train_bw");
+}
+
+int mfnerf_composite_train_fused(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
+                                 const int64_t* rays_a, int64_t n_rays, int64_t n_samples, float T_threshold,
+                                 const float* target, int64_t n_mean, float lambda_opacity, float bg_r, float bg_g,
+                                 float bg_b, int64_t* total_samples, float* opacity, float* depth, float* rgb,
+                                 float* ws, float* dL_drgb, float* dL_dopacity, float* dL_dsigmas, float* dL_drgbs,
+                                 float* loss_slots, mfnerf_stream_t stream) {
+    if (n_rays < 0 || n_samples < 0 || n_mean < 0 || (n_mean > 0 && n_mean < n_rays)) {
+        mfn_set_error("composite_train_fused: bad sizes"); return MFN_ERR_INVALID;
+    }
+    if (n_mean == 0) n_mean = n_rays;
+    if (n_rays == 0) return MFN_OK;
+    if (!rays_a || !target || !total_samples || !opacity || !depth || !rgb || !dL_drgb || !dL_dopacity ||
+        (n_samples > 0 && (!sigmas || !rgbs || !deltas || !ts || !ws || !dL_dsigmas || !dL_drgbs))) {
+        mfn_set_error("composite_train_fused: null pointer"); return MFN_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(composite_fused_wave_kernel, dim3(blocks_for(n_rays, 4)), dim3(256), 0, stream, sigmas, rgbs,
+                       deltas, ts, rays_a, n_rays, T_threshold, target, n_mean, lambda_opacity, bg_r, bg_g, bg_b,
+                       total_samples, opacity, depth, rgb, ws, dL_drgb, dL_dopacity, dL_dsigmas, dL_drgbs, loss_slots);
+    return mfn_check_launch("composite_train_fused");
 }
 
 int mfnerf_composite_test_fw(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,

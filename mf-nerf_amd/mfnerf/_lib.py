@@ -50,6 +50,8 @@ SIGNATURES = {
                                      _P, _P, _P, _P, _P, _P]),
     "mfnerf_composite_train_fw": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _F, _P, _P, _P, _P, _P, _P]),
     "mfnerf_composite_train_bw": (_I, [_P] * 13 + [_I64, _I64, _F, _P, _P, _P]),
+    "mfnerf_composite_train_fused": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _F, _P, _I64, _F, _F, _F, _F]
+                                     + [_P] * 10 + [_P]),
     "mfnerf_composite_test_fw": (_I, [_P, _P, _P, _P, _P, _I64, _I, _F, _P, _P, _P, _P, _P]),
     "mfnerf_distortion_loss_fw": (_I, [_P, _P, _P, _P, _I64, _I64, _P, _P, _P, _P]),
     "mfnerf_distortion_loss_bw": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P, _P]),

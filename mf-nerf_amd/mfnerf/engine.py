@@ -65,7 +65,10 @@ class Batch:
 
 
 class _State:
-    pass
+    @property
+    def loss_sum(self):
+        """The step's loss (device scalar): the sum of the loss partial sums."""
+        return self.loss_slots.sum()
 
 
 def _packed_batch(buf):
@@ -136,7 +139,8 @@ class TrainStep:
         self.cap = N * c.max_samples
         self.parts = [self._part_buffers(q) for q in range(c.n_parts)]
         self.mbuf = [self._march_buffers()]  # a second set is added by capture() (pipelined march)
-        self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
+        # the step's loss as 64 partial sums (spread atomics); loss_sum is their sum
+        self.loss_slots = torch.zeros(64, dtype=torch.float32, device=dev)
         self.state = _State()
         self._use(self.mbuf[0])
         self.gen = torch.Generator(device=dev)
@@ -169,8 +173,7 @@ class TrainStep:
         t.ws = torch.empty(cap, **f32)
         t.dL_drgb = torch.empty(Np, 3, **f32)
         t.dL_dop = torch.empty(Np, **f32)
-        t.zeros_ray = torch.zeros(Np, **f32)       # dL/ddepth (unused by the loss)
-        t.zeros_samp = torch.zeros(cap, **f32)     # dL/dws (no distortion loss by default)
+        t.zeros_ray = torch.zeros(Np, **f32)       # dL/ddepth (unused by the loss; unfused path)
         if c.lambda_distortion > 0:                # losses.py:6-37 + 55-58
             t.dist_loss = torch.empty(Np, **f32)
             t.ws_incl = torch.empty(cap, **f32)
@@ -214,8 +217,12 @@ class TrainStep:
     def _use(self, mb):
         """state.noise / state.counters / state.loss_sum of the step being run (inspection)."""
         st = self.state
-        st.noise, st.counters, st.loss_sum, st.march = mb.noise, mb.counters, self.loss_sum, mb
+        st.noise, st.counters, st.loss_slots, st.march = mb.noise, mb.counters, self.loss_slots, mb
         st.parts = self.parts
+
+    @property
+    def loss_sum(self):
+        return self.loss_slots.sum()
 
     def live_samples(self):
         """Device scalar: samples marched by the current step (sum over parts)."""
@@ -307,7 +314,7 @@ class TrainStep:
         Np, cap = self.Np, self.cap_p
         if q == 0:
             self.grads.zero_()
-            self.loss_sum.zero_()
+            self.loss_slots.zero_()
         else:
             t.mlp_grad.zero_()
         call("mfnerf_grid_encode_fw", ptr(m.xyzs), cap, ptr(m.counter), self.x_min, self.x_range, self.desc,
@@ -316,24 +323,31 @@ class TrainStep:
         call("mfnerf_field_fw", ptr(t.feat), ptr(m.dirs), cap, ptr(m.counter), ptr(self.packed), c.rgb_width, 0,
              ptr(t.sigma), ptr(t.rgb_s), s)
         mark("field_fw")
-        call("mfnerf_composite_train_fw", ptr(t.sigma), ptr(t.rgb_s), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a),
-             Np, cap, c.T_threshold, ptr(t.total), ptr(t.opacity), ptr(t.depth), ptr(t.rgb), ptr(t.ws), s)
         bg = 1.0 if c.scale <= 0.5 else 0.0
-        call("mfnerf_nerf_loss", ptr(t.rgb), ptr(t.opacity), ptr(batch.rgb[q * Np:(q + 1) * Np]), Np, c.n_rays,
-             c.lambda_opacity, bg, bg, bg, ptr(t.dL_drgb), ptr(t.dL_dop), ptr(self.loss_sum), s)
-        dL_dws = t.zeros_samp
-        if c.lambda_distortion > 0:
+        target = ptr(batch.rgb[q * Np:(q + 1) * Np])
+        if c.lambda_distortion <= 0:
+            # composite fw -> bg blend + NeRFLoss -> composite bw in one wave-per-ray launch
+            call("mfnerf_composite_train_fused", ptr(t.sigma), ptr(t.rgb_s), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a),
+                 Np, cap, c.T_threshold, target, c.n_rays, c.lambda_opacity, bg, bg, bg, ptr(t.total),
+                 ptr(t.opacity), ptr(t.depth), ptr(t.rgb), ptr(t.ws), ptr(t.dL_drgb), ptr(t.dL_dop), ptr(t.dsig),
+                 ptr(t.drgb_s), ptr(self.loss_slots), s)
+            mark("composite")
+        else:
+            call("mfnerf_composite_train_fw", ptr(t.sigma), ptr(t.rgb_s), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a),
+                 Np, cap, c.T_threshold, ptr(t.total), ptr(t.opacity), ptr(t.depth), ptr(t.rgb), ptr(t.ws), s)
+            call("mfnerf_nerf_loss", ptr(t.rgb), ptr(t.opacity), target, Np, c.n_rays, c.lambda_opacity, bg, bg, bg,
+                 ptr(t.dL_drgb), ptr(t.dL_dop), ptr(self.loss_slots), s)
+            # losses.py:6-37 + 55-58
             call("mfnerf_distortion_loss_fw", ptr(t.ws), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a), Np, cap,
                  ptr(t.dist_loss), ptr(t.ws_incl), ptr(t.wts_incl), s)
-            self.loss_sum.add_(t.dist_loss.sum() * (c.lambda_distortion / c.n_rays))
+            self.loss_slots[:1].add_(t.dist_loss.sum() * (c.lambda_distortion / c.n_rays))
             call("mfnerf_distortion_loss_bw", ptr(t.dL_ddist), ptr(t.ws_incl), ptr(t.wts_incl), ptr(t.ws),
                  ptr(m.deltas), ptr(m.ts), ptr(m.rays_a), Np, cap, ptr(t.dL_dws), s)
-            dL_dws = t.dL_dws
-        mark("composite_fw")
-        call("mfnerf_composite_train_bw", ptr(t.dL_dop), ptr(t.zeros_ray), ptr(t.dL_drgb), ptr(dL_dws),
-             ptr(t.sigma), ptr(t.rgb_s), ptr(t.ws), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a), ptr(t.opacity),
-             ptr(t.depth), ptr(t.rgb), Np, cap, c.T_threshold, ptr(t.dsig), ptr(t.drgb_s), s)
-        mark("composite_bw")
+            mark("composite_fw")
+            call("mfnerf_composite_train_bw", ptr(t.dL_dop), ptr(t.zeros_ray), ptr(t.dL_drgb), ptr(t.dL_dws),
+                 ptr(t.sigma), ptr(t.rgb_s), ptr(t.ws), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a), ptr(t.opacity),
+                 ptr(t.depth), ptr(t.rgb), Np, cap, c.T_threshold, ptr(t.dsig), ptr(t.drgb_s), s)
+            mark("composite_bw")
         call("mfnerf_field_bw", ptr(t.feat), ptr(m.dirs), cap, ptr(m.counter), ptr(self.packed), c.rgb_width,
              ptr(t.dsig), ptr(t.drgb_s), self.grad_scale, ptr(t.dfeat), ptr(t.mlp_grad),
              ptr(t.mlp_grad[self.off_rgb:]), ptr(t.field_ws), s)

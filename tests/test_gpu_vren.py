@@ -256,3 +256,70 @@ def test_errors_like_check_input(gpu):
         V.morton3D(torch.zeros(4, 3, dtype=torch.int32))  # CPU tensor
     with pytest.raises(RuntimeError):
         V.morton3D(torch.zeros(3, 4, dtype=torch.int32, device=gpu).t())  # non-contiguous
+
+
+def _fused_vs_separate(gpu, oracle, rays_a, sig, rgbs, deltas, ts, seed=0, lam=1e-3):
+    """mfnerf_composite_train_fused against the three separate launches (bit for bit) and the
+    oracle's fw/bw driven by the loss gradient (1e-4)."""
+    from mfnerf._lib import call, ptr, stream
+    thr, n_rays, n = 1e-4, rays_a.shape[0], sig.shape[0]
+    g = torch.Generator().manual_seed(seed)
+    target = torch.rand(n_rays, 3, generator=g)
+    S, C, Dt, Tt, R, T = _to(gpu, sig, rgbs, deltas, ts, rays_a, target)
+    f32 = dict(dtype=torch.float32, device=gpu)
+
+    def outs():
+        return dict(total=torch.zeros(n_rays, dtype=torch.int64, device=gpu), op=torch.zeros(n_rays, **f32),
+                    de=torch.zeros(n_rays, **f32), rgb=torch.zeros(n_rays, 3, **f32), ws=torch.zeros(n, **f32),
+                    g_rgb=torch.zeros(n_rays, 3, **f32), g_op=torch.zeros(n_rays, **f32),
+                    dsig=torch.zeros(n, **f32), drgb=torch.zeros(n, 3, **f32), loss=torch.zeros(64, **f32))
+    a, b = outs(), outs()
+    call("mfnerf_composite_train_fused", ptr(S), ptr(C), ptr(Dt), ptr(Tt), ptr(R), n_rays, n, thr, ptr(T), n_rays, lam,
+         1.0, 1.0, 1.0, ptr(a["total"]), ptr(a["op"]), ptr(a["de"]), ptr(a["rgb"]), ptr(a["ws"]), ptr(a["g_rgb"]),
+         ptr(a["g_op"]), ptr(a["dsig"]), ptr(a["drgb"]), ptr(a["loss"]), stream())
+    call("mfnerf_composite_train_fw", ptr(S), ptr(C), ptr(Dt), ptr(Tt), ptr(R), n_rays, n, thr, ptr(b["total"]),
+         ptr(b["op"]), ptr(b["de"]), ptr(b["rgb"]), ptr(b["ws"]), stream())
+    call("mfnerf_nerf_loss", ptr(b["rgb"]), ptr(b["op"]), ptr(T), n_rays, n_rays, lam, 1.0, 1.0, 1.0,
+         ptr(b["g_rgb"]), ptr(b["g_op"]), ptr(b["loss"]), stream())
+    zr, zs = torch.zeros(n_rays, **f32), torch.zeros(n, **f32)
+    call("mfnerf_composite_train_bw", ptr(b["g_op"]), ptr(zr), ptr(b["g_rgb"]), ptr(zs), ptr(S), ptr(C),
+         ptr(b["ws"]), ptr(Dt), ptr(Tt), ptr(R), ptr(b["op"]), ptr(b["de"]), ptr(b["rgb"]), n_rays, n, thr,
+         ptr(b["dsig"]), ptr(b["drgb"]), stream())
+    torch.cuda.synchronize()
+    for k in a:
+        if k == "loss":
+            assert abs(float(a[k].sum()) - float(b[k].sum())) <= 1e-6 * abs(float(b[k].sum()))
+        else:
+            assert torch.equal(a[k], b[k]), k
+    # the oracle, driven by the same loss gradient
+    ref = oracle.composite_train_fw(sig, rgbs, deltas, ts, rays_a, thr)
+    amb = _ambiguous_rays(sig, deltas, rays_a, thr)
+    assert torch.equal(a["total"].cpu()[~amb], ref[0][~amb])
+    _, op, de, rgb, ws = ref
+    g_rgb, g_op = a["g_rgb"].cpu(), a["g_op"].cpu()
+    ref_b = oracle.composite_train_bw(g_op, torch.zeros(n_rays), g_rgb, torch.zeros(n), sig, rgbs, ws, deltas, ts,
+                                      rays_a, op, de, rgb, thr)
+    keep = ~amb[torch.repeat_interleave(torch.arange(n_rays), rays_a[:, 2])] if n == int(rays_a[:, 2].sum()) else None
+    for got, want in zip((a["dsig"].cpu(), a["drgb"].cpu()), ref_b):
+        if keep is not None:
+            got, want = got[keep], want[keep]
+        assert torch.allclose(got, want, rtol=1e-4, atol=1e-4 * float(want.abs().max()))
+
+
+def test_composite_train_fused_fixed64(gpu, oracle):
+    rays_a, sig, rgbs, deltas, ts = fixed64_batch()
+    _fused_vs_separate(gpu, oracle, rays_a, sig, rgbs, deltas, ts)
+
+
+def test_composite_train_fused_on_marched_lego(gpu, oracle):
+    """Variable-length rays (many beyond one 64-sample chunk), misses (0 samples) included."""
+    o, d, bf, _ = lego_inputs(4096, seed=9)
+    ht = aabb_hits(oracle, o, d)
+    ref, _ = _march_both(gpu, oracle, o, d, ht, bf, 1, 0.5, 0.0)
+    rays_a, _, _, deltas, ts, cnt = ref
+    n = int(cnt[0])
+    assert int(rays_a[:, 2].max()) > 128 and int((rays_a[:, 2] == 0).sum()) > 0
+    g = torch.Generator().manual_seed(8)
+    sig = torch.exp(torch.randn(n, generator=g) * 2)
+    rgbs = torch.rand(n, 3, generator=g)
+    _fused_vs_separate(gpu, oracle, rays_a, sig, rgbs, deltas[:n].contiguous(), ts[:n].contiguous(), seed=3)
