@@ -168,6 +168,13 @@ int mfnerf_grid_encode_fw(const float* x, int64_t n, const int32_t* n_dev, float
                           const mfnerf_grid_desc* desc, const void* table_f16, void* out_f16,
                           mfnerf_stream_t stream);
 
+/* mfnerf_grid_encode_fw with a level-major output: out_planes (n_levels, plane_stride) half2, the
+ * features of level l of point i at [l*plane_stride + i] (plane_stride >= n).  Work is split by
+ * level over the 8 XCDs so each XCD's L2 holds only its levels' tables. */
+int mfnerf_grid_encode_fw_planar(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                                 const mfnerf_grid_desc* desc, const void* table_f16, void* out_planes,
+                                 int64_t plane_stride, mfnerf_stream_t stream);
+
 /* Scatter dL/dout (n, n_levels*F) f32 into grad_table (n_entries*F) f32 by float atomics
  * (accumulates; caller zeroes).  workspace (optional, mfnerf_grid_encode_bw_workspace() bytes,
  * ZERO on the first call; the call leaves it zero again): private copies of the dense coarse
@@ -196,17 +203,19 @@ int mfnerf_field_pack_weights(const float* params_xyz, const float* params_rgb, 
 
 /* NGP.forward (networks.py:134-155) on encoded features:
  *   h = xyz_mlp(feat); sigma = exp(h[0]); rgb = sigmoid(rgb_mlp([SH4((d/|d|+1)/2), h])).
- * feat (n,32) f16, dirs (n,3) f32 (ignored when density_only) -> sigma (n) f32, rgb (n,3) f32. */
-int mfnerf_field_fw(const void* feat_f16, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
+ * feat: feat_plane_stride == 0 -> (n,32) f16 row-major (tcnn layout, mfnerf_grid_encode_fw);
+ *       > 0 -> (16, feat_plane_stride) half2 level planes (mfnerf_grid_encode_fw_planar).
+ * dirs (n,3) f32 (ignored when density_only) -> sigma (n) f32, rgb (n,3) f32. */
+int mfnerf_field_fw(const void* feat_f16, int64_t feat_plane_stride, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
                     int rgb_width, int density_only, float* sigma, float* rgb, mfnerf_stream_t stream);
 
-/* Backward of mfnerf_field_fw (recomputes the forward).  dL_dsigma (n), dL_drgb (n,3) f32 ->
+/* Backward of mfnerf_field_fw (recomputes the forward; same feat layouts).  dL_dsigma (n), dL_drgb (n,3) f32 ->
  * dL_dfeat (n,32) f32, and ADDS the weight grads into grad_xyz / grad_rgb (tcnn layout f32).
  * grad_scale: power-of-two factor applied to the incoming grads before the fp16 MFMA products
  * and removed from every output (keeps O(1e-6) per-sample grads out of the fp16 subnormals).
  * workspace: mfnerf_field_bw_workspace() bytes (per-workgroup weight-grad slab). */
 int64_t mfnerf_field_bw_workspace(int64_t n, int rgb_width);
-int mfnerf_field_bw(const void* feat_f16, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
+int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
                     int rgb_width, const float* dL_dsigma, const float* dL_drgb, float grad_scale, float* dL_dfeat,
                     float* grad_xyz, float* grad_rgb, void* workspace, mfnerf_stream_t stream);
 

@@ -165,12 +165,28 @@ struct TileIn {
     float d[3];
 };
 
-__device__ __forceinline__ void load_tile_in(const _Float16* __restrict__ feat, const float* __restrict__ dirs,
-                                             int64_t s, bool valid, int h, bool want_dirs, TileIn& I) {
+// feat layouts: plane_stride == 0 -> row-major (n, 32) f16 (tcnn's encoding output); > 0 ->
+// level-major planes (16, plane_stride) half2 (mfnerf_grid_encode_fw_planar).
+__device__ __forceinline__ void load_tile_in(const _Float16* __restrict__ feat, int64_t plane_stride,
+                                             const float* __restrict__ dirs, int64_t s, bool valid, int h,
+                                             bool want_dirs, TileIn& I) {
     if (valid) {
-        const half8* row = reinterpret_cast<const half8*>(feat + s * 32);
-        I.x[0] = row[h];
-        I.x[1] = row[2 + h];
+        if (plane_stride > 0) {
+            // x[0] element j = feature 8h+j = level 4h + j/2; x[1]: level 8 + 4h + j/2
+            const uint32_t* P = reinterpret_cast<const uint32_t*>(feat);
+            uint32_t u[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                u[k] = P[(int64_t)(4 * h + k) * plane_stride + s];
+                u[4 + k] = P[(int64_t)(8 + 4 * h + k) * plane_stride + s];
+            }
+            I.x[0] = *reinterpret_cast<const half8*>(&u[0]);
+            I.x[1] = *reinterpret_cast<const half8*>(&u[4]);
+        } else {
+            const half8* row = reinterpret_cast<const half8*>(feat + s * 32);
+            I.x[0] = row[h];
+            I.x[1] = row[2 + h];
+        }
         if (want_dirs) { I.d[0] = dirs[3 * s]; I.d[1] = dirs[3 * s + 1]; I.d[2] = dirs[3 * s + 2]; }
     } else {
         I.x[0] = half8{}; I.x[1] = half8{};
@@ -244,6 +260,7 @@ __device__ __forceinline__ void load_frags(_Float16* lds, const _Float16* __rest
 
 template <bool DENSITY_ONLY>
 __global__ __launch_bounds__(FIELD_BLOCK) void field_fw_kernel(const _Float16* __restrict__ feat,
+                                                                int64_t plane_stride,
                                                                 const float* __restrict__ dirs, int64_t n,
                                                                 const int32_t* __restrict__ n_dev,
                                                                 const _Float16* __restrict__ packed,
@@ -259,7 +276,7 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_fw_kernel(const _Float16* _
         const int64_t s = tile * 32 + r;
         const bool valid = s < nn;
         TileIn I;
-        load_tile_in(feat, dirs, s, valid, h, !DENSITY_ONLY, I);
+        load_tile_in(feat, plane_stride, dirs, s, valid, h, !DENSITY_ONLY, I);
         FwdTile T;
         forward_tile<DENSITY_ONLY>(lds, lane, I, valid, T);
         if (valid && h == 0) {
@@ -347,7 +364,7 @@ __device__ __forceinline__ void dw_add32(float* img, const f32x16& a, int ot, in
 }
 
 __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
-    const _Float16* __restrict__ feat, const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev,
+    const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev,
     const _Float16* __restrict__ packed, const float* __restrict__ dL_dsigma, const float* __restrict__ dL_drgb,
     float grad_scale, float* __restrict__ dL_dfeat, float* __restrict__ slab) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -373,7 +390,7 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
     auto fetch = [&](int64_t tile) {
         const int64_t s = tile * 32 + r;
         const bool v = s < nn;
-        load_tile_in(feat, dirs, s, v, h, true, nI);
+        load_tile_in(feat, plane_stride, dirs, s, v, h, true, nI);
         ngs = ng0 = ng1 = ng2 = 0.0f;
         if (v && h == 0) {
             ngs = dL_dsigma[s];
@@ -574,10 +591,11 @@ int mfnerf_field_pack_weights(const float* params_xyz, const float* params_rgb, 
     return mfn_check_launch("field_pack_weights");
 }
 
-int mfnerf_field_fw(const void* feat_f16, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
+int mfnerf_field_fw(const void* feat_f16, int64_t feat_plane_stride, const float* dirs, int64_t n,
+                    const int32_t* n_dev, const void* packed,
                     int rgb_width, int density_only, float* sigma, float* rgb, mfnerf_stream_t stream) {
     if (rgb_width != RGB_W) { mfn_set_error("field: rgb_width=%d unsupported (this build: %d)", rgb_width, RGB_W); return MFN_ERR_INVALID; }
-    if (n < 0) { mfn_set_error("field_fw: bad size"); return MFN_ERR_INVALID; }
+    if (n < 0 || (feat_plane_stride != 0 && feat_plane_stride < n)) { mfn_set_error("field_fw: bad size"); return MFN_ERR_INVALID; }
     if (n == 0) return MFN_OK;
     if (!feat_f16 || !packed || !sigma || (!density_only && (!dirs || !rgb))) {
         mfn_set_error("field_fw: null pointer"); return MFN_ERR_INVALID;
@@ -587,10 +605,12 @@ int mfnerf_field_fw(const void* feat_f16, const float* dirs, int64_t n, const in
     const unsigned blocks = (unsigned)(want < 2048 ? want : 2048);
     if (density_only)
         hipLaunchKernelGGL(field_fw_kernel<true>, dim3(blocks), dim3(FIELD_BLOCK), 8 * FRAG_HALFS * 2, stream,
-                           (const _Float16*)feat_f16, dirs, n, n_dev, (const _Float16*)packed, sigma, rgb);
+                           (const _Float16*)feat_f16, feat_plane_stride, dirs, n, n_dev, (const _Float16*)packed,
+                           sigma, rgb);
     else
         hipLaunchKernelGGL(field_fw_kernel<false>, dim3(blocks), dim3(FIELD_BLOCK), 24 * FRAG_HALFS * 2, stream,
-                           (const _Float16*)feat_f16, dirs, n, n_dev, (const _Float16*)packed, sigma, rgb);
+                           (const _Float16*)feat_f16, feat_plane_stride, dirs, n, n_dev, (const _Float16*)packed,
+                           sigma, rgb);
     return mfn_check_launch("field_fw");
 }
 
@@ -600,17 +620,20 @@ int64_t mfnerf_field_bw_workspace(int64_t n, int rgb_width) {
     return (int64_t)BW_BLOCKS * N_DW * 4;
 }
 
-int mfnerf_field_bw(const void* feat_f16, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
+int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float* dirs, int64_t n,
+                    const int32_t* n_dev, const void* packed,
                     int rgb_width, const float* dL_dsigma, const float* dL_drgb, float grad_scale, float* dL_dfeat,
                     float* grad_xyz, float* grad_rgb, void* workspace, mfnerf_stream_t stream) {
     if (rgb_width != RGB_W) { mfn_set_error("field: rgb_width=%d unsupported (this build: %d)", rgb_width, RGB_W); return MFN_ERR_INVALID; }
-    if (n < 0 || !(grad_scale > 0.0f)) { mfn_set_error("field_bw: bad size or grad_scale"); return MFN_ERR_INVALID; }
+    if (n < 0 || !(grad_scale > 0.0f) || (feat_plane_stride != 0 && feat_plane_stride < n)) {
+        mfn_set_error("field_bw: bad size, plane stride or grad_scale"); return MFN_ERR_INVALID;
+    }
     if (n == 0) return MFN_OK;
     if (!feat_f16 || !dirs || !packed || !dL_dsigma || !dL_drgb || !dL_dfeat || !grad_xyz || !grad_rgb || !workspace) {
         mfn_set_error("field_bw: null pointer"); return MFN_ERR_INVALID;
     }
     hipLaunchKernelGGL(field_bw_kernel, dim3(BW_BLOCKS), dim3(FIELD_BLOCK), BW_LDS, stream, (const _Float16*)feat_f16,
-                       dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb, grad_scale, dL_dfeat,
+                       feat_plane_stride, dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb, grad_scale, dL_dfeat,
                        (float*)workspace);
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((N_DW + 63) / 64), dim3(256), 0, stream, (const float*)workspace,
                        BW_BLOCKS, grad_xyz, grad_rgb);

@@ -109,6 +109,72 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_fw_kernel(const float* __restr
     }
 }
 
+// Planar (level-major) forward, XCD-partitioned: blocks b and b+8 share an XCD (round-robin
+// dispatch), so block group b % 8 owns the levels {l : snake(l % 16) == b % 8} (levels p and 15-p
+// for L = 16) for every sample.  Each XCD's L2 then holds only its levels' tables (<= 4 MB of
+// fp16 features), instead of every XCD streaming the whole 23 MB table through its 4 MB L2.
+// out: n_levels planes of plane_stride half2 (features of level l of sample i at out[l*stride+i]),
+// so each group's stores are contiguous.  Placement only affects speed, never the result.
+__device__ __forceinline__ int level_group(int l) {
+    const int q = l & 15;
+    return q < 8 ? q : 15 - q;
+}
+
+__global__ __launch_bounds__(ENC_BLOCK) void grid_fw_planar_kernel(const float* __restrict__ X, int64_t n,
+                                                                    const int32_t* __restrict__ n_dev, float x_min,
+                                                                    float x_range, const mfnerf_grid_desc D,
+                                                                    const __half2* __restrict__ table,
+                                                                    __half2* __restrict__ out, int64_t plane_stride) {
+    const int grp = blockIdx.x & 7;
+    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
+    const int64_t stride = (int64_t)(gridDim.x >> 3) * ENC_BLOCK;
+    for (int64_t i = (int64_t)(blockIdx.x >> 3) * ENC_BLOCK + threadIdx.x; i < nn; i += stride) {
+        const float x = (X[3 * i] - x_min) / x_range;
+        const float y = (X[3 * i + 1] - x_min) / x_range;
+        const float z = (X[3 * i + 2] - x_min) / x_range;
+        for (int l = 0; l < D.n_levels; ++l) {
+            if (level_group(l) != grp) continue;
+            const LevelGeo L = level_geo(D.scale[l], x, y, z);
+            const __half2* tab = table + D.offset[l];
+            const uint32_t size = D.size[l], res = D.res[l];
+            const bool dense = D.table_kind[l] == 0 && (uint64_t)res * res * res <= size;
+            const bool pow2 = (size & (size - 1)) == 0;
+            __half2 v[8];
+            // The two x-corners of a (y,z) row are adjacent entries -- dense levels: idx+1 (one
+            // unaligned 8-B load unless it wraps past the table end); hashed power-of-two levels
+            // with even x: idx^1 (one aligned 8-B load) -- so each row costs one gather lane
+            // instead of two (the kernel is bound by per-lane gather addresses).
+#pragma unroll
+            for (int yz = 0; yz < 4; ++yz) {
+                const uint32_t gy = L.g[1] + (yz & 1), gz = L.g[2] + (yz >> 1);
+                const uint32_t i0 = corner_index(D, l, L.g[0], gy, gz);
+                if (dense && i0 + 1 < size) {
+                    const uint2 u = *reinterpret_cast<const uint2*>(tab + i0);
+                    v[2 * yz] = *reinterpret_cast<const __half2*>(&u.x);
+                    v[2 * yz + 1] = *reinterpret_cast<const __half2*>(&u.y);
+                } else if (!dense && pow2 && D.table_kind[l] == 0 && (L.g[0] & 1) == 0) {
+                    const uint2 u = *reinterpret_cast<const uint2*>(tab + (i0 & ~1u));
+                    const bool lo = (i0 & 1) == 0;
+                    v[2 * yz] = *reinterpret_cast<const __half2*>(lo ? &u.x : &u.y);
+                    v[2 * yz + 1] = *reinterpret_cast<const __half2*>(lo ? &u.y : &u.x);
+                } else {
+                    v[2 * yz] = tab[i0];
+                    v[2 * yz + 1] = tab[corner_index(D, l, L.g[0] + 1, gy, gz)];
+                }
+            }
+            float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const float w = corner_weight(L, c);
+                const float2 f = __half22float2(v[c]);
+                a0 = fmaf(w, f.x, a0);
+                a1 = fmaf(w, f.y, a1);
+            }
+            out[(int64_t)l * plane_stride + i] = __floats2half2_rn(a0, a1);
+        }
+    }
+}
+
 // Backward.  The table gradient is a scatter-add; on MI355X a float atomic executes at the memory
 // side and costs one request per distinct 64-B line of a wave-instruction -- lanes of one line are
 // free, lanes on the SAME address are not coalesced (tools/atomic_probe2.hip) -- so the kernel is
@@ -285,6 +351,21 @@ int mfnerf_grid_encode_fw(const float* x, int64_t n, const int32_t* n_dev, float
     hipLaunchKernelGGL(grid_fw_kernel, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0,
                        stream, x, n, n_dev, x_min, x_range, *desc, (const __half2*)table_f16, (__half*)out_f16);
     return mfn_check_launch("grid_encode_fw");
+}
+
+int mfnerf_grid_encode_fw_planar(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                                 const mfnerf_grid_desc* desc, const void* table_f16, void* out_planes,
+                                 int64_t plane_stride, mfnerf_stream_t stream) {
+    int st = check_desc(desc, "grid_encode_fw_planar");
+    if (st) return st;
+    if (n < 0 || plane_stride < n) { mfn_set_error("grid_encode_fw_planar: bad size"); return MFN_ERR_INVALID; }
+    if (n == 0) return MFN_OK;
+    if (!x || !table_f16 || !out_planes) { mfn_set_error("grid_encode_fw_planar: null pointer"); return MFN_ERR_INVALID; }
+    const int64_t want = div_up<int64_t>(n, ENC_BLOCK);
+    const int64_t per_group = want < 2048 ? want : 2048;
+    hipLaunchKernelGGL(grid_fw_planar_kernel, dim3((unsigned)(8 * per_group)), dim3(ENC_BLOCK), 0, stream, x, n, n_dev,
+                       x_min, x_range, *desc, (const __half2*)table_f16, (__half2*)out_planes, plane_stride);
+    return mfn_check_launch("grid_encode_fw_planar");
 }
 
 int64_t mfnerf_grid_encode_bw_workspace(const mfnerf_grid_desc* desc) {

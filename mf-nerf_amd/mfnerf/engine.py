@@ -163,7 +163,8 @@ class TrainStep:
         c, dev, Np, cap = self.cfg, self.dev, self.Np, self.cap_p
         f32 = dict(dtype=torch.float32, device=dev)
         t = _State()
-        t.feat = torch.empty(cap, c.L * c.F, dtype=torch.float16, device=dev)
+        # encoded features as level planes (L, cap) of half2 (mfnerf_grid_encode_fw_planar)
+        t.feat = torch.empty(c.L, cap, c.F, dtype=torch.float16, device=dev)
         t.sigma = torch.empty(cap, **f32)
         t.rgb_s = torch.empty(cap, 3, **f32)
         t.total = torch.empty(Np, dtype=torch.int64, device=dev)
@@ -317,10 +318,10 @@ class TrainStep:
             self.loss_slots.zero_()
         else:
             t.mlp_grad.zero_()
-        call("mfnerf_grid_encode_fw", ptr(m.xyzs), cap, ptr(m.counter), self.x_min, self.x_range, self.desc,
-             ptr(self.p16[self.off_table:]), ptr(t.feat), s)
+        call("mfnerf_grid_encode_fw_planar", ptr(m.xyzs), cap, ptr(m.counter), self.x_min, self.x_range, self.desc,
+             ptr(self.p16[self.off_table:]), ptr(t.feat), cap, s)
         mark("grid_fw")
-        call("mfnerf_field_fw", ptr(t.feat), ptr(m.dirs), cap, ptr(m.counter), ptr(self.packed), c.rgb_width, 0,
+        call("mfnerf_field_fw", ptr(t.feat), cap, ptr(m.dirs), cap, ptr(m.counter), ptr(self.packed), c.rgb_width, 0,
              ptr(t.sigma), ptr(t.rgb_s), s)
         mark("field_fw")
         bg = 1.0 if c.scale <= 0.5 else 0.0
@@ -348,7 +349,7 @@ class TrainStep:
                  ptr(t.sigma), ptr(t.rgb_s), ptr(t.ws), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a), ptr(t.opacity),
                  ptr(t.depth), ptr(t.rgb), Np, cap, c.T_threshold, ptr(t.dsig), ptr(t.drgb_s), s)
             mark("composite_bw")
-        call("mfnerf_field_bw", ptr(t.feat), ptr(m.dirs), cap, ptr(m.counter), ptr(self.packed), c.rgb_width,
+        call("mfnerf_field_bw", ptr(t.feat), cap, ptr(m.dirs), cap, ptr(m.counter), ptr(self.packed), c.rgb_width,
              ptr(t.dsig), ptr(t.drgb_s), self.grad_scale, ptr(t.dfeat), ptr(t.mlp_grad),
              ptr(t.mlp_grad[self.off_rgb:]), ptr(t.field_ws), s)
         mark("field_bw")
@@ -595,7 +596,7 @@ class TrainStep:
             o.n_max = n
             o.xyz = torch.empty(n, 3, dtype=torch.float32, device=self.dev)
             o.cell = torch.empty(n, dtype=torch.int32, device=self.dev)
-            o.feat = torch.empty(n, c.L * c.F, dtype=torch.float16, device=self.dev)
+            o.feat = torch.empty(c.L, n, c.F, dtype=torch.float16, device=self.dev)  # level planes
             o.sigma = torch.empty(n, dtype=torch.float32, device=self.dev)
             o.tmp = torch.empty(C * G ** 3, dtype=torch.float32, device=self.dev)
             o.ws = torch.empty(lib.mfnerf_occupancy_workspace(C, G), dtype=torch.uint8, device=self.dev)
@@ -616,8 +617,8 @@ class TrainStep:
         call("mfnerf_occupancy_cells", ptr(self.density_grid), C, G, float(c.scale), M, int(warmup), thr, seed,
              o.calls, ptr(o.xyz), ptr(o.cell), ptr(o.ws), s)
         o.calls += 1
-        call("mfnerf_grid_encode_fw", ptr(o.xyz), n, None, self.x_min, self.x_range, self.desc,
-             ptr(self.p16[self.off_table:]), ptr(o.feat), s)
-        call("mfnerf_field_fw", ptr(o.feat), None, n, None, ptr(self.packed), c.rgb_width, 1, ptr(o.sigma), None, s)
+        call("mfnerf_grid_encode_fw_planar", ptr(o.xyz), n, None, self.x_min, self.x_range, self.desc,
+             ptr(self.p16[self.off_table:]), ptr(o.feat), o.n_max, s)
+        call("mfnerf_field_fw", ptr(o.feat), o.n_max, None, n, None, ptr(self.packed), c.rgb_width, 1, ptr(o.sigma), None, s)
         call("mfnerf_occupancy_update", ptr(self.density_grid), ptr(o.sigma), ptr(o.cell), n, C, G, float(decay),
              ptr(count_grid) if count_grid is not None else None, thr, ptr(o.tmp), ptr(self.bitfield), ptr(o.ws), s)

@@ -54,7 +54,7 @@ def field_fw(feat, dirs, n, packed, rgb_width=64, density_only=False, n_dev=None
         sigma = torch.empty(n, dtype=torch.float32, device=dev)
     if rgb is None and not density_only:
         rgb = torch.empty(n, 3, dtype=torch.float32, device=dev)
-    call("mfnerf_field_fw", ptr(feat), ptr(dirs), int(n), ptr(n_dev), ptr(packed), int(rgb_width),
+    call("mfnerf_field_fw", ptr(feat), 0, ptr(dirs), int(n), ptr(n_dev), ptr(packed), int(rgb_width),
          int(bool(density_only)), ptr(sigma), ptr(rgb), stream())
     return sigma, rgb
 
@@ -66,7 +66,7 @@ def field_bw_workspace(n, rgb_width=64, device="cuda"):
 
 def field_bw(feat, dirs, n, packed, dL_dsigma, dL_drgb, grad_scale, dL_dfeat, grad_xyz_net, grad_rgb, workspace,
              rgb_width=64, n_dev=None):
-    call("mfnerf_field_bw", ptr(feat), ptr(dirs), int(n), ptr(n_dev), ptr(packed), int(rgb_width), ptr(dL_dsigma),
+    call("mfnerf_field_bw", ptr(feat), 0, ptr(dirs), int(n), ptr(n_dev), ptr(packed), int(rgb_width), ptr(dL_dsigma),
          ptr(dL_drgb), float(grad_scale), ptr(dL_dfeat), ptr(grad_xyz_net), ptr(grad_rgb), ptr(workspace), stream())
 
 

@@ -170,3 +170,52 @@ def test_field_bw(gpu, wscale, sig_on):
         # vs pure fp32 autograd: the fp16 quantisation tcnn's backward has too (~1% rms)
         cos = float(torch.nn.functional.cosine_similarity(got.flatten(), r32.flatten(), dim=0))
         assert cos > 0.9995, cos
+
+
+@pytest.mark.parametrize("name,args", [_layouts()[0], _layouts()[2]])
+def test_planar_encode_and_field_match_row_major(gpu, name, args):
+    """The training path's level-major encode (XCD-partitioned, paired x-corner loads) equals the
+    row-major tcnn-layout encode bit for bit, and the field kernels read either layout to the same
+    outputs and data gradients (bit for bit; the weight gradients' in-workgroup sum runs through
+    LDS atomics, so their last bits depend on wave order)."""
+    lay = GridLayout(*args)
+    desc = lay.desc()
+    g = torch.Generator().manual_seed(11)
+    N, cap = 5003, 5120
+    x = torch.rand(N, 3, generator=g)
+    x[:8] = torch.tensor([0.0, 1.0]).repeat(12)[:24].view(8, 3)
+    table16 = ((torch.rand(lay.n_params, generator=g) - 0.5)).half().to(gpu)
+    xg = x.to(gpu)
+    row = FLD.grid_encode_fw(xg, N, table16, lay, desc)
+    planes = torch.full((lay.L, cap, 2), float("nan"), dtype=torch.float16, device=gpu)
+    n_dev = torch.tensor([N], dtype=torch.int32, device=gpu)
+    call("mfnerf_grid_encode_fw_planar", ptr(xg), cap, ptr(n_dev), 0.0, 1.0, desc, ptr(table16), ptr(planes), cap,
+         torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(planes[:, :N].permute(1, 0, 2).reshape(N, -1), row)
+    if lay.L != 16:
+        return
+    _, dirs, px, pr = _field_inputs(N, seed=12)
+    packed = FLD.pack_field_weights(px.to(gpu), pr.to(gpu))
+    dg = dirs.to(gpu)
+    s1, c1 = FLD.field_fw(row, dg, N, packed)
+    s2 = torch.empty(N, device=gpu)
+    c2 = torch.empty(N, 3, device=gpu)
+    st = torch.cuda.current_stream().cuda_stream
+    call("mfnerf_field_fw", ptr(planes), cap, ptr(dg), N, None, ptr(packed), 64, 0, ptr(s2), ptr(c2), st)
+    torch.cuda.synchronize()
+    assert torch.equal(s1, s2) and torch.equal(c1, c2)
+    dsig = (torch.randn(N, generator=g) * 1e-6).to(gpu)
+    drgb = (torch.randn(N, 3, generator=g) * 1e-5).to(gpu)
+    outs = []
+    for feat, stride in ((row, 0), (planes, cap)):
+        dfeat = torch.empty(N, 32, device=gpu)
+        gx, gr = torch.zeros(3072, device=gpu), torch.zeros(7168, device=gpu)
+        ws = FLD.field_bw_workspace(N, 64, gpu)
+        call("mfnerf_field_bw", ptr(feat), stride, ptr(dg), N, None, ptr(packed), 64, ptr(dsig), ptr(drgb), 4096.0,
+             ptr(dfeat), ptr(gx), ptr(gr), ptr(ws), st)
+        torch.cuda.synchronize()
+        outs.append((dfeat, gx, gr))
+    assert torch.equal(outs[0][0], outs[1][0])
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6 * float(b.abs().max()))

@@ -29,12 +29,16 @@ def main():
     batch = step.last_batch
     n_live = int(m.counter[0])
     zeros_samp = torch.zeros(cap, device=dev)
+    planes = torch.empty(c.L, cap, 2, dtype=torch.float16, device=dev)
+    rowmajor = torch.empty(cap, 2 * c.L, dtype=torch.float16, device=dev)
     s = stream
 
     stages = {
         "grid_fw": lambda: call("mfnerf_grid_encode_fw", ptr(m.xyzs), cap, ptr(m.counter), step.x_min, step.x_range,
-                                step.desc, ptr(step.p16[step.off_table:]), ptr(t.feat), s()),
-        "field_fw": lambda: call("mfnerf_field_fw", ptr(t.feat), ptr(m.dirs), cap, ptr(m.counter), ptr(step.packed),
+                                step.desc, ptr(step.p16[step.off_table:]), ptr(rowmajor), s()),
+        "grid_fw_planar": lambda: call("mfnerf_grid_encode_fw_planar", ptr(m.xyzs), cap, ptr(m.counter), step.x_min,
+                                       step.x_range, step.desc, ptr(step.p16[step.off_table:]), ptr(planes), cap, s()),
+        "field_fw": lambda: call("mfnerf_field_fw", ptr(t.feat), cap, ptr(m.dirs), cap, ptr(m.counter), ptr(step.packed),
                                  c.rgb_width, 0, ptr(t.sigma), ptr(t.rgb_s), s()),
         "composite_fw": lambda: call("mfnerf_composite_train_fw", ptr(t.sigma), ptr(t.rgb_s), ptr(m.deltas),
                                      ptr(m.ts), ptr(m.rays_a), Np, cap, c.T_threshold, ptr(t.total), ptr(t.opacity),
@@ -49,7 +53,7 @@ def main():
                                   ptr(m.rays_a), Np, cap, c.T_threshold, ptr(batch.rgb), c.n_rays, c.lambda_opacity,
                                   1.0, 1.0, 1.0, ptr(t.total), ptr(t.opacity), ptr(t.depth), ptr(t.rgb), ptr(t.ws),
                                   ptr(t.dL_drgb), ptr(t.dL_dop), ptr(t.dsig), ptr(t.drgb_s), ptr(step.loss_slots), s()),
-        "field_bw": lambda: call("mfnerf_field_bw", ptr(t.feat), ptr(m.dirs), cap, ptr(m.counter), ptr(step.packed),
+        "field_bw": lambda: call("mfnerf_field_bw", ptr(t.feat), cap, ptr(m.dirs), cap, ptr(m.counter), ptr(step.packed),
                                  c.rgb_width, ptr(t.dsig), ptr(t.drgb_s), step.grad_scale, ptr(t.dfeat),
                                  ptr(t.mlp_grad), ptr(t.mlp_grad[step.off_rgb:]), ptr(t.field_ws), s()),
         "grid_bw": lambda: step._grid_bw(mb, 0),
