@@ -102,15 +102,15 @@ int mfnerf_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, 
 /* Fused training compositing for the default loss (no distortion term): mfnerf_composite_train_fw,
  * mfnerf_nerf_loss (target, n_mean, lambda_opacity, bg) and mfnerf_composite_train_bw with
  * dL_ddepth = 0, dL_dws = 0 in one pass (one wave per ray); the same outputs as the three calls,
- * bit-identical.  loss_slots (optional, 64 device f32) ACCUMULATES the loss value spread over 64
- * partial sums (their sum is the loss).  Replaces the chain at rendering.py:121-163 + losses.py:47-60
+ * bit-identical.  loss_partials (optional, ceil(n_rays/4) device f32) is OVERWRITTEN with the loss
+ * value as one partial sum per 4 rays (their sum is the loss; no zeroing needed).  Replaces the chain at rendering.py:121-163 + losses.py:47-60
  * + custom_functions.py:148-159 in one training step. */
 int mfnerf_composite_train_fused(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
                                  const int64_t* rays_a, int64_t n_rays, int64_t n_samples, float T_threshold,
                                  const float* target, int64_t n_mean, float lambda_opacity, float bg_r, float bg_g,
                                  float bg_b, int64_t* total_samples, float* opacity, float* depth, float* rgb,
                                  float* ws, float* dL_drgb, float* dL_dopacity, float* dL_dsigmas, float* dL_drgbs,
-                                 float* loss_slots, mfnerf_stream_t stream);
+                                 float* loss_partials, mfnerf_stream_t stream);
 
 /* vren.composite_test_fw (binding.cpp:176-201, volumerendering.cu:205-285).  sigmas (n_alive,N_samples),
  * rgbs (n_alive,N_samples,3), deltas, ts (n_alive,N_samples); in place on alive_indices, opacity,
@@ -190,6 +190,12 @@ int mfnerf_debug_grid_bw_ablate(int mode, const float* x, int64_t n, const int32
                                 const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
                                 mfnerf_stream_t stream);
 
+/* Debug: the table-gradient scatter with fp16 accumulation (global_atomic_pk_add_f16, values scaled by
+ * gscale) into grad_h2 (n_entries half2); priv_h2: optional private copies of the dense levels. */
+int mfnerf_debug_grid_bw_half(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                              const mfnerf_grid_desc* desc, const float* dL_dout, void* grad_h2, void* priv_h2,
+                              float gscale, mfnerf_stream_t stream);
+
 /* ---------------------------------------------------------------- NGP field head (MFMA) */
 
 /* Weight blob for the two FullyFusedMLPs of NGP (networks.py:50-79) in this library's MFMA
@@ -200,6 +206,10 @@ int64_t mfnerf_field_packed_bytes(int rgb_width);
  * params_rgb: (W*32 + W*W + 16*W) f32.  Writes packed (mfnerf_field_packed_bytes). */
 int mfnerf_field_pack_weights(const float* params_xyz, const float* params_rgb, int rgb_width, void* packed,
                               mfnerf_stream_t stream);
+
+/* The same blob from the fp16 compute copy of the params (what packing the fp32 master gives). */
+int mfnerf_field_pack_weights_f16(const void* params_xyz_f16, const void* params_rgb_f16, int rgb_width, void* packed,
+                                  mfnerf_stream_t stream);
 
 /* NGP.forward (networks.py:134-155) on encoded features:
  *   h = xyz_mlp(feat); sigma = exp(h[0]); rgb = sigmoid(rgb_mlp([SH4((d/|d|+1)/2), h])).
@@ -213,11 +223,15 @@ int mfnerf_field_fw(const void* feat_f16, int64_t feat_plane_stride, const float
  * dL_dfeat (n,32) f32, and ADDS the weight grads into grad_xyz / grad_rgb (tcnn layout f32).
  * grad_scale: power-of-two factor applied to the incoming grads before the fp16 MFMA products
  * and removed from every output (keeps O(1e-6) per-sample grads out of the fp16 subnormals).
- * workspace: mfnerf_field_bw_workspace() bytes (per-workgroup weight-grad slab). */
+ * workspace: mfnerf_field_bw_workspace() bytes (per-workgroup weight-grad slab).
+ * nonfinite (optional device i32): set to 1 when any dL_dfeat or weight gradient is inf/nan (the
+ * table gradient of mfnerf_grid_encode_bw is a weighted sum of dL_dfeat, so this flags the whole
+ * step's gradient without scanning it; feeds mfnerf_adam_step's skip). */
 int64_t mfnerf_field_bw_workspace(int64_t n, int rgb_width);
 int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
                     int rgb_width, const float* dL_dsigma, const float* dL_drgb, float grad_scale, float* dL_dfeat,
-                    float* grad_xyz, float* grad_rgb, void* workspace, mfnerf_stream_t stream);
+                    float* grad_xyz, float* grad_rgb, void* workspace, int32_t* nonfinite,
+                    mfnerf_stream_t stream);
 
 /* Debug: one v_mfma_f32_32x32x16_f16 with A (32x16) and B (16x32) f16 row-major -> D (32x32) f32,
  * through the lane maps the field kernels assume (pins them on the device). */
@@ -268,17 +282,22 @@ int mfnerf_sample_rays(const float* images, const float* poses, const float* dir
 /* Adam (apex FusedAdam semantics, adam_w_mode=False, no weight decay; train.py:136):
  * m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= lr * (m/(1-b1^t)) / (sqrt(v/(1-b2^t)) + eps).
  * g is read as grad*grad_scale.  Optionally mirrors p into p_f16 (the fp16 compute copy).
- * step_dev (optional device i32): step counter incremented by the kernel (graph-replay safe).
+ * step_dev (optional device i32): the number of completed steps; the update uses t = *step_dev+1
+ * and the call then increments it (graph-replay safe).  Without step_dev, t = step.
  * lr_dev (optional device f32): learning rate read on the device (a schedule that does not
  * re-capture the graph); lr is used when it is NULL.
  * skip (optional device i32[2]): when skip[0] != 0 the call changes nothing (params, m, v, p_f16
  * and step_dev untouched) and increments skip[1] -- torch GradScaler's skipped step on a
- * non-finite gradient (PL precision=16, train.py:287); skip[0] is set by mfnerf_check_finite. */
-int mfnerf_adam_step(float* params, const float* grads, float* m, float* v, void* p_f16, int64_t n, float lr,
-                     float beta1, float beta2, float eps, float grad_scale, int step, const int32_t* step_dev,
-                     const float* lr_dev, int32_t* skip, mfnerf_stream_t stream);
+ * non-finite gradient (PL precision=16, train.py:287).  The call clears skip[0] afterwards;
+ * skip[0] is raised by mfnerf_field_bw's nonfinite flag or mfnerf_check_finite.
+ * zero_grads != 0: grads is zeroed by the same pass (also on a skipped step), ready for the next
+ * step's accumulation. */
+int mfnerf_adam_step(float* params, float* grads, float* m, float* v, void* p_f16, int64_t n, float lr,
+                     float beta1, float beta2, float eps, float grad_scale, int step, int32_t* step_dev,
+                     const float* lr_dev, int32_t* skip, int zero_grads, mfnerf_stream_t stream);
 
-/* status[0] (device i32) = 1 if any of x (n f32, 16-byte aligned) is inf/nan, else 0. */
+/* status[0] (device i32) = 1 if any of x (n f32, 16-byte aligned) is inf/nan, else 0 (a full scan;
+ * the training step gets the same flag from mfnerf_field_bw's nonfinite argument instead). */
 int mfnerf_check_finite(const float* x, int64_t n, int32_t* status, mfnerf_stream_t stream);
 
 #ifdef __cplusplus

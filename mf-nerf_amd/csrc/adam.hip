@@ -7,19 +7,28 @@
 
 namespace {
 
-__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+__global__ void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, __half* __restrict__ p16, int64_t n, float lr, float b1, float b2,
                             float eps, float gscale, int step, const int32_t* __restrict__ step_dev,
-                            const float* __restrict__ lr_dev, const int32_t* __restrict__ skip) {
-    if (skip && *skip) return;  // GradScaler: no update on a non-finite gradient
-    const int st = step_dev ? *step_dev : step;
+                            const float* __restrict__ lr_dev, const int32_t* __restrict__ skip, int zero_grads) {
+    const int64_t n4 = n / 4;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (skip && *skip) {  // GradScaler: no update on a non-finite gradient (only the zeroing)
+        if (zero_grads) {
+            for (int64_t i = t0; i < n4; i += stride) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int64_t i = n4 * 4 + t0; i < n; i += stride) g[i] = 0.0f;
+        }
+        return;
+    }
+    // step_dev counts completed steps; this update is number *step_dev + 1 (bump_step_kernel
+    // advances it after the update, so every block reads the same value)
+    const int st = step_dev ? *step_dev + 1 : step;
     if (lr_dev) lr = *lr_dev;
     // apex multi_tensor_adam (ADAM_MODE, decay 0): m/(1-b1^t), v/(1-b2^t), p -= lr*m_hat/(sqrt(v_hat)+eps)
     const float bc1 = 1.0f - powf(b1, (float)st);
     const float bc2 = 1.0f - powf(b2, (float)st);
-    const int64_t n4 = n / 4;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    for (int64_t i = t0; i < n4; i += stride) {
         float4 pp = reinterpret_cast<float4*>(p)[i];
         const float4 gg = reinterpret_cast<const float4*>(g)[i];
         float4 mm = reinterpret_cast<float4*>(m)[i];
@@ -36,6 +45,7 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
         reinterpret_cast<float4*>(p)[i] = pp;
         reinterpret_cast<float4*>(m)[i] = mm;
         reinterpret_cast<float4*>(v)[i] = vv;
+        if (zero_grads) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (p16) {
             __half2 a = __floats2half2_rn(pp.x, pp.y), b = __floats2half2_rn(pp.z, pp.w);
             uint2 u; u.x = *reinterpret_cast<uint32_t*>(&a); u.y = *reinterpret_cast<uint32_t*>(&b);
@@ -43,19 +53,22 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
         }
     }
     // tail
-    for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    for (int64_t i = n4 * 4 + t0; i < n; i += stride) {
         const float gk = g[i] * gscale;
         m[i] = b1 * m[i] + (1.0f - b1) * gk;
         v[i] = b2 * v[i] + (1.0f - b2) * gk * gk;
         const float denom = sqrtf(v[i] / bc2) + eps;
         p[i] = p[i] - lr * ((m[i] / bc1) / denom);
+        if (zero_grads) g[i] = 0.0f;
         if (p16) p16[i] = __float2half_rn(p[i]);
     }
 }
 
+// after the update: count the step (or the skipped step) and clear the non-finite flag for the
+// next step's producers
 __global__ void bump_step_kernel(int32_t* s, int32_t* skip) {
-    if (skip && skip[0]) skip[1] += 1;  // count the skipped step
-    else *s += 1;
+    if (skip && skip[0]) { skip[1] += 1; skip[0] = 0; }
+    else if (s) *s += 1;
 }
 
 // status[0] = 1 if any x is inf/nan (status[0] must be 0 on entry); one atomic per offending wave
@@ -73,9 +86,9 @@ __global__ void finite_kernel(const float* __restrict__ x, int64_t n, int32_t* _
 
 }  // namespace
 
-extern "C" int mfnerf_adam_step(float* params, const float* grads, float* m, float* v, void* p_f16, int64_t n,
+extern "C" int mfnerf_adam_step(float* params, float* grads, float* m, float* v, void* p_f16, int64_t n,
                                 float lr, float beta1, float beta2, float eps, float grad_scale, int step,
-                                const int32_t* step_dev, const float* lr_dev, int32_t* skip,
+                                int32_t* step_dev, const float* lr_dev, int32_t* skip, int zero_grads,
                                 mfnerf_stream_t stream) {
     if (n < 0) { mfn_set_error("adam_step: bad size"); return MFN_ERR_INVALID; }
     if (n == 0) return MFN_OK;
@@ -88,9 +101,9 @@ extern "C" int mfnerf_adam_step(float* params, const float* grads, float* m, flo
     const int threads = 256;
     const int64_t want = mfn::div_up<int64_t>(mfn::div_up<int64_t>(n, 4), threads);
     const unsigned blocks = (unsigned)(want < 4096 ? (want < 1 ? 1 : want) : 4096);
-    if (step_dev) hipLaunchKernelGGL(bump_step_kernel, dim3(1), dim3(1), 0, stream, (int32_t*)step_dev, skip);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(threads), 0, stream, params, grads, m, v, (__half*)p_f16, n, lr,
-                       beta1, beta2, eps, grad_scale, step, step_dev, lr_dev, skip);
+                       beta1, beta2, eps, grad_scale, step, step_dev, lr_dev, skip, zero_grads);
+    if (step_dev || skip) hipLaunchKernelGGL(bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, skip);
     return mfn_check_launch("adam_step");
 }
 

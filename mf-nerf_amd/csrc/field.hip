@@ -64,8 +64,8 @@ __device__ FragSpec frag_spec(int f) {
 }
 
 // weight matrices, row-major (out, in) in the tcnn params vectors
-__device__ __forceinline__ void mat_info(int mat, const float* px, const float* pr, const float** p, int* rows,
-                                         int* cols) {
+template <typename TP>
+__device__ __forceinline__ void mat_info(int mat, const TP* px, const TP* pr, const TP** p, int* rows, int* cols) {
     switch (mat) {
         case 0: *p = px; *rows = 64; *cols = 32; break;
         case 1: *p = px + 64 * 32; *rows = 16; *cols = 64; break;
@@ -78,18 +78,19 @@ __device__ __forceinline__ void mat_info(int mat, const float* px, const float* 
 // k index carried by element j of lane half h (natural B order, or accumulator-as-operand order)
 __device__ __forceinline__ int k_of(int j, int h, int perm) { return perm ? 8 * (j >> 2) + 4 * h + (j & 3) : 8 * h + j; }
 
-__global__ void pack_kernel(const float* __restrict__ px, const float* __restrict__ pr, _Float16* __restrict__ out) {
+template <typename TP>
+__global__ void pack_kernel(const TP* __restrict__ px, const TP* __restrict__ pr, _Float16* __restrict__ out) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= N_FRAGS * FRAG_HALFS) return;
     const int f = t / FRAG_HALFS, lane = (t / 8) & 63, j = t & 7;
     const FragSpec s = frag_spec(f);
     const int r = lane & 31, h = lane >> 5;
     const int m = 32 * s.mtile + r, k = s.kbase + k_of(j, h, s.perm);
-    const float* p; int rows, cols;
+    const TP* p; int rows, cols;
     mat_info(s.mat, px, pr, &p, &rows, &cols);
     float v = 0.0f;
-    if (!s.trans) { if (m < rows && k < cols) v = p[m * cols + k]; }
-    else { if (k < rows && m < cols) v = p[k * cols + m]; }
+    if (!s.trans) { if (m < rows && k < cols) v = (float)p[m * cols + k]; }
+    else { if (k < rows && m < cols) v = (float)p[k * cols + m]; }
     out[t] = (_Float16)v;
 }
 
@@ -366,7 +367,7 @@ __device__ __forceinline__ void dw_add32(float* img, const f32x16& a, int ot, in
 __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
     const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev,
     const _Float16* __restrict__ packed, const float* __restrict__ dL_dsigma, const float* __restrict__ dL_drgb,
-    float grad_scale, float* __restrict__ dL_dfeat, float* __restrict__ slab) {
+    float grad_scale, float* __restrict__ dL_dfeat, float* __restrict__ slab, int32_t* __restrict__ nonfinite) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     _Float16* lds_base = reinterpret_cast<_Float16*>(smem);
     load_frags_bw(lds_base, packed);
@@ -505,13 +506,19 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int q = 0; q < 2; ++q) dx = mfma(lds_frag(lds, B1 + t * 2 + q, lane), dy1p[t][q], dx);
+            bool bad = false;
             if (valid) {
                 float4* dst = reinterpret_cast<float4*>(dL_dfeat + s * 32);
 #pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    dst[2 * g + h] = make_float4(dx[4 * g] * invS, dx[4 * g + 1] * invS, dx[4 * g + 2] * invS,
+                for (int g = 0; g < 4; ++g) {
+                    const float4 o = make_float4(dx[4 * g] * invS, dx[4 * g + 1] * invS, dx[4 * g + 2] * invS,
                                                  dx[4 * g + 3] * invS);
+                    bad |= !(isfinite(o.x) && isfinite(o.y) && isfinite(o.z) && isfinite(o.w));
+                    dst[2 * g + h] = o;
+                }
             }
+            // the table gradient is sum(weight * dL/dfeat): non-finite only if some dL/dfeat is
+            if (nonfinite && __any(bad) && lane == 0) atomicOr(nonfinite, 1);
         }
     }
 
@@ -540,7 +547,8 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
 
 // grad[p] += sum over slab rows (fixed order: deterministic).  64 columns x 4 row groups per block.
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int rows,
-                                                          float* __restrict__ gx, float* __restrict__ gr) {
+                                                          float* __restrict__ gx, float* __restrict__ gr,
+                                                          int32_t* __restrict__ nonfinite) {
     __shared__ float part[4][64];
     const int l = threadIdx.x & 63, rg = threadIdx.x >> 6;
     const int p = blockIdx.x * 64 + l;
@@ -553,6 +561,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
         const float v = (part[0][l] + part[1][l]) + (part[2][l] + part[3][l]);
         if (p < N_XYZ_PARAMS) gx[p] += v;
         else gr[p - N_XYZ_PARAMS] += v;
+        if (nonfinite && !isfinite(v)) atomicOr(nonfinite, 1);
     }
 }
 
@@ -586,9 +595,19 @@ int mfnerf_field_pack_weights(const float* params_xyz, const float* params_rgb, 
     if (rgb_width != RGB_W) { mfn_set_error("field: rgb_width=%d unsupported (this build: %d)", rgb_width, RGB_W); return MFN_ERR_INVALID; }
     if (!params_xyz || !params_rgb || !packed) { mfn_set_error("field_pack_weights: null pointer"); return MFN_ERR_INVALID; }
     const int total = N_FRAGS * FRAG_HALFS;
-    hipLaunchKernelGGL(pack_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, params_xyz, params_rgb,
+    hipLaunchKernelGGL(pack_kernel<float>, dim3((total + 255) / 256), dim3(256), 0, stream, params_xyz, params_rgb,
                        (_Float16*)packed);
     return mfn_check_launch("field_pack_weights");
+}
+
+int mfnerf_field_pack_weights_f16(const void* params_xyz_f16, const void* params_rgb_f16, int rgb_width, void* packed,
+                                  mfnerf_stream_t stream) {
+    if (rgb_width != RGB_W) { mfn_set_error("field: rgb_width=%d unsupported (this build: %d)", rgb_width, RGB_W); return MFN_ERR_INVALID; }
+    if (!params_xyz_f16 || !params_rgb_f16 || !packed) { mfn_set_error("field_pack_weights_f16: null pointer"); return MFN_ERR_INVALID; }
+    const int total = N_FRAGS * FRAG_HALFS;
+    hipLaunchKernelGGL(pack_kernel<_Float16>, dim3((total + 255) / 256), dim3(256), 0, stream,
+                       (const _Float16*)params_xyz_f16, (const _Float16*)params_rgb_f16, (_Float16*)packed);
+    return mfn_check_launch("field_pack_weights_f16");
 }
 
 int mfnerf_field_fw(const void* feat_f16, int64_t feat_plane_stride, const float* dirs, int64_t n,
@@ -623,7 +642,7 @@ int64_t mfnerf_field_bw_workspace(int64_t n, int rgb_width) {
 int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float* dirs, int64_t n,
                     const int32_t* n_dev, const void* packed,
                     int rgb_width, const float* dL_dsigma, const float* dL_drgb, float grad_scale, float* dL_dfeat,
-                    float* grad_xyz, float* grad_rgb, void* workspace, mfnerf_stream_t stream) {
+                    float* grad_xyz, float* grad_rgb, void* workspace, int32_t* nonfinite, mfnerf_stream_t stream) {
     if (rgb_width != RGB_W) { mfn_set_error("field: rgb_width=%d unsupported (this build: %d)", rgb_width, RGB_W); return MFN_ERR_INVALID; }
     if (n < 0 || !(grad_scale > 0.0f) || (feat_plane_stride != 0 && feat_plane_stride < n)) {
         mfn_set_error("field_bw: bad size, plane stride or grad_scale"); return MFN_ERR_INVALID;
@@ -634,9 +653,9 @@ int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float
     }
     hipLaunchKernelGGL(field_bw_kernel, dim3(BW_BLOCKS), dim3(FIELD_BLOCK), BW_LDS, stream, (const _Float16*)feat_f16,
                        feat_plane_stride, dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb, grad_scale, dL_dfeat,
-                       (float*)workspace);
+                       (float*)workspace, nonfinite);
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((N_DW + 63) / 64), dim3(256), 0, stream, (const float*)workspace,
-                       BW_BLOCKS, grad_xyz, grad_rgb);
+                       BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
     return mfn_check_launch("field_bw");
 }
 

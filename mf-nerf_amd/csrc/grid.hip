@@ -283,6 +283,84 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restr
     }
 }
 
+// fp16 variant (experiment / tcnn's grad_t = __half for F = 2): one lane adds BOTH features of a
+// corner with global_atomic_pk_add_f16, lanes = (sample s, x-corner xb, yz-half), so a level takes
+// 2 wave-instructions instead of 4.  Values are multiplied by gscale before rounding to fp16.
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+
+template <int MAXL>
+__global__ __launch_bounds__(ENC_BLOCK) void grid_bw_h2_kernel(const float* __restrict__ X, int64_t n,
+                                                                const int32_t* __restrict__ n_dev, float x_min,
+                                                                float x_range, const mfnerf_grid_desc D,
+                                                                const float* __restrict__ dy, h2v* __restrict__ grad,
+                                                                h2v* __restrict__ priv, int64_t dense_entries,
+                                                                float gscale) {
+    __shared__ float sdy_all[ENC_BLOCK / 64][16 * (2 * MAXL + 1)];
+    const int L_ = D.n_levels;
+    const int lane = threadIdx.x & 63, s = lane & 15, xb = (lane >> 4) & 1, yzh = lane >> 5;
+    const int row = 2 * L_, rs = 2 * L_ + 1, per_chunk = 16 * row;
+    float* sdy = sdy_all[threadIdx.x >> 6];
+    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
+    const int64_t chunks = div_up<int64_t>(nn, 16);
+    const int64_t wave0 = ((int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * ENC_BLOCK) >> 6;
+    const int64_t n_vals = nn * row;
+    float pf[MAXL / 2];
+    float px = 0.0f, py = 0.0f, pz = 0.0f;
+    auto fetch = [&](int64_t ch) {
+        const int64_t base = ch * per_chunk;
+#pragma unroll
+        for (int k = 0; k < MAXL / 2; ++k) {
+            const int idx = lane + 64 * k;
+            pf[k] = (idx < per_chunk && base + idx < n_vals) ? dy[base + idx] : 0.0f;
+        }
+        const int64_t i = ch * 16 + s;
+        if (i < nn) { px = X[3 * i]; py = X[3 * i + 1]; pz = X[3 * i + 2]; }
+    };
+    if (wave0 < chunks) fetch(wave0);
+    for (int64_t chunk = wave0; chunk < chunks; chunk += n_waves) {
+        const int64_t i = chunk * 16 + s;
+        const bool valid = i < nn;
+#pragma unroll
+        for (int k = 0; k < MAXL / 2; ++k) {
+            const int idx = lane + 64 * k;
+            if (idx < per_chunk) sdy[(idx / row) * rs + idx % row] = pf[k];
+        }
+        const float x = valid ? (px - x_min) / x_range : 0.0f;
+        const float y = valid ? (py - x_min) / x_range : 0.0f;
+        const float z = valid ? (pz - x_min) / x_range : 0.0f;
+        if (chunk + n_waves < chunks) fetch(chunk + n_waves);
+        const float* srow = sdy + s * rs;
+        for (int l = 0; l < L_; ++l) {
+            const float g0 = srow[2 * l] * gscale, g1 = srow[2 * l + 1] * gscale;
+            const LevelGeo Lg = level_geo(D.scale[l], x, y, z);
+            const bool spread = priv && (int64_t)D.offset[l] + D.size[l] <= dense_entries;
+            h2v* gt = spread ? priv + ((chunk & (GRAD_COPIES - 1)) * dense_entries + (int64_t)D.offset[l])
+                             : grad + (int64_t)D.offset[l];
+#pragma unroll
+            for (int yp = 0; yp < 2; ++yp) {
+                const int c = xb | ((2 * yzh + yp) << 1);
+                const uint32_t idx =
+                    corner_index(D, l, Lg.g[0] + (c & 1), Lg.g[1] + ((c >> 1) & 1), Lg.g[2] + ((c >> 2) & 1));
+                const int key = valid ? (int)idx : -1;
+                const float w = corner_weight(Lg, c);
+                float v0 = w * g0, v1 = w * g1;
+                const int kn = dpp_i<DPP_ROW_SHL(1)>(key), kp = dpp_i<DPP_ROW_SHR(1)>(key);
+                const bool head = (s == 0) || kp != key;
+                int stop = (s == 15) || kn != key;
+#define H2_STEP(d) { const float a = dpp_f<DPP_ROW_SHL(d)>(v0), b = dpp_f<DPP_ROW_SHL(d)>(v1); \
+                     const int sp = dpp_i<DPP_ROW_SHL(d)>(stop); if (!stop) { v0 += a; v1 += b; stop = sp; } }
+                H2_STEP(1) H2_STEP(2) H2_STEP(4) H2_STEP(8)
+#undef H2_STEP
+                if (head && valid && (v0 != 0.0f || v1 != 0.0f)) {
+                    const h2v hv = {(_Float16)v0, (_Float16)v1};
+                    __builtin_amdgcn_global_atomic_fadd_v2f16((__attribute__((address_space(1))) h2v*)(gt + idx), hv);
+                }
+            }
+        }
+    }
+}
+
 // grad[p] += sum_k priv[k][p]; priv[k][p] = 0 (ready for the next backward)
 __global__ __launch_bounds__(256) void fold_copies_kernel(float* __restrict__ priv, int64_t n, float* __restrict__ grad) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -395,6 +473,19 @@ int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float
                            (float*)workspace, nf, grad_table);
     }
     return mfn_check_launch("grid_encode_bw");
+}
+
+int mfnerf_debug_grid_bw_half(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                              const mfnerf_grid_desc* desc, const float* dL_dout, void* grad_h2, void* priv_h2,
+                              float gscale, mfnerf_stream_t stream) {
+    if (desc->n_levels > 16) { mfn_set_error("grid_bw_half: n_levels <= 16 only"); return MFN_ERR_INVALID; }
+    const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16), ENC_BLOCK / 64);
+    const int64_t cap = grid_bw_block_cap();
+    const int64_t blocks = want < cap ? want : cap;
+    const int64_t dense = priv_h2 ? dense_entries_of(desc) : 0;
+    hipLaunchKernelGGL(grid_bw_h2_kernel<16>, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min,
+                       x_range, *desc, dL_dout, (h2v*)grad_h2, (h2v*)priv_h2, dense, gscale);
+    return mfn_check_launch("grid_bw_half");
 }
 
 // Debug (not part of the training path): the same launch with an ablated kernel body.

@@ -474,8 +474,7 @@ __global__ __launch_bounds__(256) void composite_bw_wave_kernel(
 // stores each sample's post-sample transmittance into dL_dsigmas (as scratch); pass 2 reads w and
 // T back (same lane, same address) instead of re-walking the transmittance chain, so the result is
 // bit-identical to the three separate kernels (the dropped terms are exact zeros).  The loss value
-// goes to 64 partial sums (loss_slots[blockIdx % 64]) to spread the atomics.
-constexpr int LOSS_SLOTS = 64;
+// is written as one partial sum per workgroup of 4 rays (plain stores: no zeroing, no atomics).
 
 __global__ __launch_bounds__(256) void composite_fused_wave_kernel(
     const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
@@ -483,7 +482,7 @@ __global__ __launch_bounds__(256) void composite_fused_wave_kernel(
     const float* __restrict__ target, int64_t n_mean, float lambda_o, float bg0, float bg1, float bg2,
     int64_t* __restrict__ total_samples, float* __restrict__ opacity, float* __restrict__ depth,
     float* __restrict__ rgb, float* __restrict__ ws, float* __restrict__ dL_drgb, float* __restrict__ dL_dop,
-    float* __restrict__ dL_dsigmas, float* __restrict__ dL_drgbs, float* __restrict__ loss_slots) {
+    float* __restrict__ dL_dsigmas, float* __restrict__ dL_drgbs, float* __restrict__ loss_part) {
     __shared__ float lsum[4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t n = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -577,8 +576,7 @@ __global__ __launch_bounds__(256) void composite_fused_wave_kernel(
     }
     if (lane == 0) lsum[wid] = l;
     __syncthreads();
-    if (threadIdx.x == 0 && loss_slots)
-        atomicAdd(loss_slots + (blockIdx.x & (LOSS_SLOTS - 1)), (lsum[0] + lsum[1]) + (lsum[2] + lsum[3]));
+    if (threadIdx.x == 0 && loss_part) loss_part[blockIdx.x] = (lsum[0] + lsum[1]) + (lsum[2] + lsum[3]);
 }
 
 __global__ void composite_test_kernel(const float* __restrict__ sigmas, const float* __restrict__ rgbs,
@@ -824,7 +822,7 @@ int mfnerf_composite_train_fused(const float* sigmas, const float* rgbs, const f
                                  const float* target, int64_t n_mean, float lambda_opacity, float bg_r, float bg_g,
                                  float bg_b, int64_t* total_samples, float* opacity, float* depth, float* rgb,
                                  float* ws, float* dL_drgb, float* dL_dopacity, float* dL_dsigmas, float* dL_drgbs,
-                                 float* loss_slots, mfnerf_stream_t stream) {
+                                 float* loss_partials, mfnerf_stream_t stream) {
     if (n_rays < 0 || n_samples < 0 || n_mean < 0 || (n_mean > 0 && n_mean < n_rays)) {
         mfn_set_error("composite_train_fused: bad sizes"); return MFN_ERR_INVALID;
     }
@@ -836,7 +834,8 @@ int mfnerf_composite_train_fused(const float* sigmas, const float* rgbs, const f
     }
     hipLaunchKernelGGL(composite_fused_wave_kernel, dim3(blocks_for(n_rays, 4)), dim3(256), 0, stream, sigmas, rgbs,
                        deltas, ts, rays_a, n_rays, T_threshold, target, n_mean, lambda_opacity, bg_r, bg_g, bg_b,
-                       total_samples, opacity, depth, rgb, ws, dL_drgb, dL_dopacity, dL_dsigmas, dL_drgbs, loss_slots);
+                       total_samples, opacity, depth, rgb, ws, dL_drgb, dL_dopacity, dL_dsigmas, dL_drgbs,
+                       loss_partials);
     return mfn_check_launch("composite_train_fused");
 }
 

@@ -60,19 +60,21 @@ SIGNATURES = {
     "mfnerf_grid_encode_fw_planar": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _I64, _P]),
     "mfnerf_grid_encode_bw_workspace": (_I64, [ctypes.POINTER(GridDesc)]),
     "mfnerf_grid_encode_bw": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _P]),
+    "mfnerf_debug_grid_bw_half": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _F, _P]),
     "mfnerf_debug_grid_bw_ablate": (_I, [_I, _P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P]),
     "mfnerf_field_packed_bytes": (_I64, [_I]),
+    "mfnerf_field_pack_weights_f16": (_I, [_P, _P, _I, _P, _P]),
     "mfnerf_field_pack_weights": (_I, [_P, _P, _I, _P, _P]),
     "mfnerf_field_fw": (_I, [_P, _I64, _P, _I64, _P, _P, _I, _I, _P, _P, _P]),
     "mfnerf_field_bw_workspace": (_I64, [_I64, _I]),
-    "mfnerf_field_bw": (_I, [_P, _I64, _P, _I64, _P, _P, _I, _P, _P, _F, _P, _P, _P, _P, _P]),
+    "mfnerf_field_bw": (_I, [_P, _I64, _P, _I64, _P, _P, _I, _P, _P, _F, _P, _P, _P, _P, _P, _P]),
     "mfnerf_debug_mfma_probe": (_I, [_P, _P, _P, _P]),
     "mfnerf_occupancy_workspace": (_I64, [_I, _I]),
     "mfnerf_occupancy_points": (_I64, [_I, _I, _I64, _I]),
     "mfnerf_occupancy_cells": (_I, [_P, _I, _I, _F, _I64, _I, _F, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P]),
     "mfnerf_occupancy_update": (_I, [_P, _P, _P, _I64, _I, _I, _F, _P, _F, _P, _P, _P, _P]),
     "mfnerf_sample_rays": (_I, [_P, _P, _P, _I64, _I64, _I64, _I, ctypes.c_uint64, _P, _P, _P, _P, _P]),
-    "mfnerf_adam_step": (_I, [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _P]),
+    "mfnerf_adam_step": (_I, [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _I, _P]),
     "mfnerf_check_finite": (_I, [_P, _I64, _P, _P]),
 }
 

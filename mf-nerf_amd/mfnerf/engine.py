@@ -68,7 +68,7 @@ class _State:
     @property
     def loss_sum(self):
         """The step's loss (device scalar): the sum of the loss partial sums."""
-        return self.loss_slots.sum()
+        return self.loss_parts.sum()
 
 
 def _packed_batch(buf):
@@ -115,7 +115,6 @@ class TrainStep:
         self.m = torch.zeros(self.n_alloc, device=dev)
         self.v = torch.zeros(self.n_alloc, device=dev)
         self.p16 = self.params.half()
-        self._mlp32 = torch.empty(self.off_table, device=dev)  # fp32 view of the fp16 MLP weights (pack)
         self.shard = None  # (rank, lo, hi) once shard_optimizer() is on
         self.finite_status = torch.zeros(2, dtype=torch.int32, device=dev)  # [non-finite flag, skipped steps]
         self.packed = torch.empty(load().mfnerf_field_packed_bytes(c.rgb_width) // 2, dtype=torch.float16,
@@ -139,8 +138,11 @@ class TrainStep:
         self.cap = N * c.max_samples
         self.parts = [self._part_buffers(q) for q in range(c.n_parts)]
         self.mbuf = [self._march_buffers()]  # a second set is added by capture() (pipelined march)
-        # the step's loss as 64 partial sums (spread atomics); loss_sum is their sum
-        self.loss_slots = torch.zeros(64, dtype=torch.float32, device=dev)
+        # the step's loss as partial sums: one per 4 rays of each part (written by the fused
+        # compositing kernel) + 64 accumulated slots (unfused path: NeRFLoss atomics, distortion)
+        self._nb_part = -(-self.Np // 4)
+        self.loss_parts = torch.zeros(c.n_parts * self._nb_part + 64, dtype=torch.float32, device=dev)
+        self._loss_acc = self.loss_parts[c.n_parts * self._nb_part:]
         self.state = _State()
         self._use(self.mbuf[0])
         self.gen = torch.Generator(device=dev)
@@ -218,12 +220,12 @@ class TrainStep:
     def _use(self, mb):
         """state.noise / state.counters / state.loss_sum of the step being run (inspection)."""
         st = self.state
-        st.noise, st.counters, st.loss_slots, st.march = mb.noise, mb.counters, self.loss_slots, mb
+        st.noise, st.counters, st.loss_parts, st.march = mb.noise, mb.counters, self.loss_parts, mb
         st.parts = self.parts
 
     @property
     def loss_sum(self):
-        return self.loss_slots.sum()
+        return self.loss_parts.sum()
 
     def live_samples(self):
         """Device scalar: samples marched by the current step (sum over parts)."""
@@ -267,8 +269,7 @@ class TrainStep:
     def _pack(self):
         """MFMA weight blob from the fp16 compute copy (the fp16 values packing the fp32 master
         would produce), so it works on every rank when the fp32 master is sharded."""
-        self._mlp32.copy_(self.p16[:self.off_table])
-        call("mfnerf_field_pack_weights", ptr(self._mlp32), ptr(self._mlp32[self.off_rgb:]), self.cfg.rgb_width,
+        call("mfnerf_field_pack_weights_f16", ptr(self.p16), ptr(self.p16[self.off_rgb:]), self.cfg.rgb_width,
              ptr(self.packed), stream())
 
     def shard_optimizer(self, rank, world):
@@ -314,8 +315,10 @@ class TrainStep:
         t, m = self.parts[q], mb.part[q]
         Np, cap = self.Np, self.cap_p
         if q == 0:
-            self.grads.zero_()
-            self.loss_slots.zero_()
+            if self.shard is not None:
+                self.grads.zero_()  # unsharded: the previous Adam pass left it zero
+            if c.lambda_distortion > 0:
+                self._loss_acc.zero_()
         else:
             t.mlp_grad.zero_()
         call("mfnerf_grid_encode_fw_planar", ptr(m.xyzs), cap, ptr(m.counter), self.x_min, self.x_range, self.desc,
@@ -331,17 +334,17 @@ class TrainStep:
             call("mfnerf_composite_train_fused", ptr(t.sigma), ptr(t.rgb_s), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a),
                  Np, cap, c.T_threshold, target, c.n_rays, c.lambda_opacity, bg, bg, bg, ptr(t.total),
                  ptr(t.opacity), ptr(t.depth), ptr(t.rgb), ptr(t.ws), ptr(t.dL_drgb), ptr(t.dL_dop), ptr(t.dsig),
-                 ptr(t.drgb_s), ptr(self.loss_slots), s)
+                 ptr(t.drgb_s), ptr(self.loss_parts[q * self._nb_part:]), s)
             mark("composite")
         else:
             call("mfnerf_composite_train_fw", ptr(t.sigma), ptr(t.rgb_s), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a),
                  Np, cap, c.T_threshold, ptr(t.total), ptr(t.opacity), ptr(t.depth), ptr(t.rgb), ptr(t.ws), s)
             call("mfnerf_nerf_loss", ptr(t.rgb), ptr(t.opacity), target, Np, c.n_rays, c.lambda_opacity, bg, bg, bg,
-                 ptr(t.dL_drgb), ptr(t.dL_dop), ptr(self.loss_slots), s)
+                 ptr(t.dL_drgb), ptr(t.dL_dop), ptr(self._loss_acc), s)
             # losses.py:6-37 + 55-58
             call("mfnerf_distortion_loss_fw", ptr(t.ws), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a), Np, cap,
                  ptr(t.dist_loss), ptr(t.ws_incl), ptr(t.wts_incl), s)
-            self.loss_slots[:1].add_(t.dist_loss.sum() * (c.lambda_distortion / c.n_rays))
+            self._loss_acc[1:2].add_(t.dist_loss.sum() * (c.lambda_distortion / c.n_rays))
             call("mfnerf_distortion_loss_bw", ptr(t.dL_ddist), ptr(t.ws_incl), ptr(t.wts_incl), ptr(t.ws),
                  ptr(m.deltas), ptr(m.ts), ptr(m.rays_a), Np, cap, ptr(t.dL_dws), s)
             mark("composite_fw")
@@ -351,7 +354,8 @@ class TrainStep:
             mark("composite_bw")
         call("mfnerf_field_bw", ptr(t.feat), cap, ptr(m.dirs), cap, ptr(m.counter), ptr(self.packed), c.rgb_width,
              ptr(t.dsig), ptr(t.drgb_s), self.grad_scale, ptr(t.dfeat), ptr(t.mlp_grad),
-             ptr(t.mlp_grad[self.off_rgb:]), ptr(t.field_ws), s)
+             ptr(t.mlp_grad[self.off_rgb:]), ptr(t.field_ws),
+             ptr(self.finite_status) if c.skip_nonfinite else None, s)
         mark("field_bw")
 
     def _grid_bw(self, mb, q):
@@ -365,30 +369,24 @@ class TrainStep:
         for t in self.parts[1:]:
             self.grads[:self.off_table].add_(t.mlp_grad)
 
-    def _check(self, grads):
-        """finite_status[0] = any(grads is inf/nan) (when skip_nonfinite)."""
-        if self.cfg.skip_nonfinite:
-            call("mfnerf_check_finite", ptr(grads), grads.numel(), ptr(self.finite_status), stream())
-
-    def _adam(self, grads, lo, hi):
-        """Adam over params[lo:hi] with grads (hi-lo), refreshing p16[lo:hi]; a no-op when the
-        finite check flagged this step."""
+    def _adam(self, grads, lo, hi, zero_grads):
+        """Adam over params[lo:hi] with grads (hi-lo), refreshing p16[lo:hi]; a no-op (but for the
+        zeroing) when the step's non-finite flag is up (raised by field_bw, cleared by the call)."""
         c = self.cfg
         call("mfnerf_adam_step", ptr(self.params[lo:hi]), ptr(grads), ptr(self.m), ptr(self.v), ptr(self.p16[lo:hi]),
              hi - lo, float(c.lr), 0.9, 0.999, c.eps, 1.0, 0, ptr(self.step_dev), ptr(self.lr_dev),
-             ptr(self.finite_status) if c.skip_nonfinite else None, stream())
+             ptr(self.finite_status) if c.skip_nonfinite else None, int(zero_grads), stream())
 
     def _update(self):
-        """Finite check + Adam over the flat params (+ fp16 mirror) + MLP weight repack (unsharded)."""
-        self._check(self.grads)
-        self._adam(self.grads, 0, self.n_alloc)
+        """Adam over the flat params (+ fp16 mirror, + zeroing the gradient for the next step) +
+        MLP weight repack (unsharded)."""
+        self._adam(self.grads, 0, self.n_alloc, True)
         self._pack()
 
-    def _shard_adam(self, check, adam):
-        """Sharded: each rank checks its gradient shard, the flag is max-reduced over ranks (one
-        int, so every rank takes the same decision), then Adam on the shard."""
+    def _shard_adam(self, adam):
+        """Sharded: every rank's flag (its own field_bw's) is max-reduced over ranks -- one int, so
+        every rank takes the same decision -- then Adam on the shard."""
         from . import dp
-        check()
         if self.cfg.skip_nonfinite:
             dp.allreduce_max_(self.finite_status[:1])
         adam()
@@ -415,7 +413,7 @@ class TrainStep:
         if self.shard is not None:
             rank, lo, hi = self.shard
             dp.sharded_update(self.grads, self.g_shard, self.p16, rank,
-                              adam or (lambda g: self._shard_adam(lambda: self._check(g), lambda: self._adam(g, lo, hi))))
+                              adam or (lambda g: self._shard_adam(lambda: self._adam(g, lo, hi, False))))
             (pack or self._pack)()
         else:
             if exchange is not None:
@@ -500,8 +498,7 @@ class TrainStep:
         }
         if self.shard is not None:
             rank, lo, hi = self.shard
-            self.graphs["check"] = cap(lambda: self._check(self.g_shard))
-            self.graphs["adam"] = cap(lambda: self._adam(self.g_shard, lo, hi))
+            self.graphs["adam"] = cap(lambda: self._adam(self.g_shard, lo, hi, False))
             self.graphs["pack"] = cap(self._pack)
         else:
             self.graphs["update"] = cap(self._update)
@@ -579,7 +576,7 @@ class TrainStep:
         if g["reduce"] is not None:
             g["reduce"].replay()
         if self.shard is not None:
-            self._optimize(None, adam=lambda _g: self._shard_adam(g["check"].replay, g["adam"].replay),
+            self._optimize(None, adam=lambda _g: self._shard_adam(g["adam"].replay),
                            pack=g["pack"].replay)
         else:
             self._optimize(exchange, adam=lambda _g: g["update"].replay())

@@ -65,9 +65,10 @@ def field_bw_workspace(n, rgb_width=64, device="cuda"):
 
 
 def field_bw(feat, dirs, n, packed, dL_dsigma, dL_drgb, grad_scale, dL_dfeat, grad_xyz_net, grad_rgb, workspace,
-             rgb_width=64, n_dev=None):
+             rgb_width=64, n_dev=None, nonfinite=None):
     call("mfnerf_field_bw", ptr(feat), 0, ptr(dirs), int(n), ptr(n_dev), ptr(packed), int(rgb_width), ptr(dL_dsigma),
-         ptr(dL_drgb), float(grad_scale), ptr(dL_dfeat), ptr(grad_xyz_net), ptr(grad_rgb), ptr(workspace), stream())
+         ptr(dL_drgb), float(grad_scale), ptr(dL_dfeat), ptr(grad_xyz_net), ptr(grad_rgb), ptr(workspace),
+         ptr(nonfinite), stream())
 
 
 def pow2_grad_scale(max_abs):

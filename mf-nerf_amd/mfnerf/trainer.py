@@ -9,7 +9,7 @@ the step.
 * fp16 loss scaling -- PL precision=16 (train.py:287).  The engine runs the MLP backward in fp16
   with a fixed power-of-two scale and un-scales inside the kernel, so there is no dynamic scale to
   grow; what GradScaler adds beyond that -- skip the optimizer step when a gradient is not finite --
-  is done on the device every step (mfnerf_check_finite feeding mfnerf_adam_step's skip flag; no
+  is done on the device every step (mfnerf_field_bw's non-finite flag feeding mfnerf_adam_step's skip; no
   host synchronisation);
 * metrics -- train loss / PSNR / rm_s (train.py:178-189), test PSNR with the test-time renderer
   (train.py:197-206), both read back only every `log_every` steps;

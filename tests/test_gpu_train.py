@@ -6,7 +6,7 @@ import math
 import pytest
 import torch
 
-from mfnerf import data, engine
+from mfnerf import data, engine, synthetic
 from mfnerf.trainer import HParams, Trainer
 
 pytestmark = pytest.mark.gpu
@@ -53,16 +53,24 @@ def test_sample_rays_batches_are_independent(gpu):
 
 
 def test_nonfinite_gradient_skips_the_step(gpu):
+    """GradScaler semantics (PL precision=16, train.py:287): a step whose gradient holds an inf/nan
+    changes no parameter, no Adam moment and no step count; it is counted as skipped and leaves the
+    gradient zero for the next step.  The NaN enters through the loss target, so the flag is the one
+    the step itself raises (field_bw's dL/dfeat and weight-gradient checks), not a gradient scan."""
     st = engine.TrainStep(engine.StepConfig(n_rays=256, log2_T=14), device=gpu)
+    st.set_occupancy(synthetic.ball_density_grid())
+    bad, good = st.make_batches(2, seed=3)
+    bad.rgb.fill_(float("nan"))
     p0, m0, s0 = st.params.clone(), st.m.clone(), int(st.step_dev)
-    st.grads.normal_()
-    st.grads[12345] = float("nan")
-    st._update()
+    st.run(bad)
+    torch.cuda.synchronize()
     assert torch.equal(st.params, p0) and torch.equal(st.m, m0) and int(st.step_dev) == s0
-    assert st.skipped_steps() == 1
-    st.grads.normal_()
-    st._update()
+    assert st.skipped_steps() == 1 and int(st.finite_status[0]) == 0
+    assert int((st.grads != 0).sum()) == 0  # zeroed for the next step even though skipped
+    st.run(good)
+    torch.cuda.synchronize()
     assert not torch.equal(st.params, p0) and int(st.step_dev) == s0 + 1 and st.skipped_steps() == 1
+    assert torch.isfinite(st.params).all()
 
 
 def _ball_views(n, W=64, seed=0):

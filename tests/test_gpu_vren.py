@@ -272,7 +272,8 @@ def _fused_vs_separate(gpu, oracle, rays_a, sig, rgbs, deltas, ts, seed=0, lam=1
         return dict(total=torch.zeros(n_rays, dtype=torch.int64, device=gpu), op=torch.zeros(n_rays, **f32),
                     de=torch.zeros(n_rays, **f32), rgb=torch.zeros(n_rays, 3, **f32), ws=torch.zeros(n, **f32),
                     g_rgb=torch.zeros(n_rays, 3, **f32), g_op=torch.zeros(n_rays, **f32),
-                    dsig=torch.zeros(n, **f32), drgb=torch.zeros(n, 3, **f32), loss=torch.zeros(64, **f32))
+                    dsig=torch.zeros(n, **f32), drgb=torch.zeros(n, 3, **f32),
+                    loss=torch.zeros(max(64, (n_rays + 3) // 4), **f32))
     a, b = outs(), outs()
     call("mfnerf_composite_train_fused", ptr(S), ptr(C), ptr(Dt), ptr(Tt), ptr(R), n_rays, n, thr, ptr(T), n_rays, lam,
          1.0, 1.0, 1.0, ptr(a["total"]), ptr(a["op"]), ptr(a["de"]), ptr(a["rgb"]), ptr(a["ws"]), ptr(a["g_rgb"]),

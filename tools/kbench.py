@@ -31,6 +31,8 @@ def main():
     zeros_samp = torch.zeros(cap, device=dev)
     planes = torch.empty(c.L, cap, 2, dtype=torch.float16, device=dev)
     rowmajor = torch.empty(cap, 2 * c.L, dtype=torch.float16, device=dev)
+    grad_h2 = torch.zeros(step.layout.n_params, dtype=torch.float16, device=dev)
+    priv_h2 = torch.zeros_like(t.grid_ws)
     s = stream
 
     stages = {
@@ -44,7 +46,7 @@ def main():
                                      ptr(m.ts), ptr(m.rays_a), Np, cap, c.T_threshold, ptr(t.total), ptr(t.opacity),
                                      ptr(t.depth), ptr(t.rgb), ptr(t.ws), s()),
         "loss": lambda: call("mfnerf_nerf_loss", ptr(t.rgb), ptr(t.opacity), ptr(batch.rgb), Np, c.n_rays,
-                             c.lambda_opacity, 1.0, 1.0, 1.0, ptr(t.dL_drgb), ptr(t.dL_dop), ptr(step.loss_slots), s()),
+                             c.lambda_opacity, 1.0, 1.0, 1.0, ptr(t.dL_drgb), ptr(t.dL_dop), ptr(step.loss_parts[-64:]), s()),
         "composite_bw": lambda: call("mfnerf_composite_train_bw", ptr(t.dL_dop), ptr(t.zeros_ray), ptr(t.dL_drgb),
                                      ptr(zeros_samp), ptr(t.sigma), ptr(t.rgb_s), ptr(t.ws), ptr(m.deltas),
                                      ptr(m.ts), ptr(m.rays_a), ptr(t.opacity), ptr(t.depth), ptr(t.rgb), Np, cap,
@@ -52,12 +54,14 @@ def main():
         "composite": lambda: call("mfnerf_composite_train_fused", ptr(t.sigma), ptr(t.rgb_s), ptr(m.deltas), ptr(m.ts),
                                   ptr(m.rays_a), Np, cap, c.T_threshold, ptr(batch.rgb), c.n_rays, c.lambda_opacity,
                                   1.0, 1.0, 1.0, ptr(t.total), ptr(t.opacity), ptr(t.depth), ptr(t.rgb), ptr(t.ws),
-                                  ptr(t.dL_drgb), ptr(t.dL_dop), ptr(t.dsig), ptr(t.drgb_s), ptr(step.loss_slots), s()),
+                                  ptr(t.dL_drgb), ptr(t.dL_dop), ptr(t.dsig), ptr(t.drgb_s), ptr(step.loss_parts), s()),
         "field_bw": lambda: call("mfnerf_field_bw", ptr(t.feat), cap, ptr(m.dirs), cap, ptr(m.counter), ptr(step.packed),
                                  c.rgb_width, ptr(t.dsig), ptr(t.drgb_s), step.grad_scale, ptr(t.dfeat),
-                                 ptr(t.mlp_grad), ptr(t.mlp_grad[step.off_rgb:]), ptr(t.field_ws), s()),
+                                 ptr(t.mlp_grad), ptr(t.mlp_grad[step.off_rgb:]), ptr(t.field_ws), None, s()),
         "grid_bw": lambda: step._grid_bw(mb, 0),
-        "check": lambda: step._check(step.grads),
+        "grid_bw_half": lambda: call("mfnerf_debug_grid_bw_half", ptr(m.xyzs), cap, ptr(m.counter), step.x_min,
+                                     step.x_range, step.desc, ptr(t.dfeat), ptr(grad_h2), ptr(priv_h2), 2048.0, s()),
+        "check": lambda: call("mfnerf_check_finite", ptr(step.grads), step.grads.numel(), ptr(step.finite_status), s()),
         "adam": lambda: step._adam(step.grads, 0, step.n_alloc),
         "pack": step._pack,
         "march": lambda: step._march(batch, mb, lambda _n: None),
