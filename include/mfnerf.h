@@ -300,6 +300,13 @@ int mfnerf_adam_step(float* params, float* grads, float* m, float* v, void* p_f1
  * the training step gets the same flag from mfnerf_field_bw's nonfinite argument instead). */
 int mfnerf_check_finite(const float* x, int64_t n, int32_t* status, mfnerf_stream_t stream);
 
+/* Sharded data parallel (mfnerf.dp.sharded_update): the step's non-finite flag rides the gradient
+ * reduce-scatter.  mfnerf_flag_to_shards: if flag[0], grads[r*shard_len] = NaN for r < world (call
+ * before the reduce-scatter); mfnerf_flag_from_shard: flag[0] = !isfinite(g_shard[0]) (after it).
+ * Every rank then skips or updates together, with no extra collective. */
+int mfnerf_flag_to_shards(float* grads, int64_t world, int64_t shard_len, const int32_t* flag, mfnerf_stream_t stream);
+int mfnerf_flag_from_shard(const float* g_shard, int32_t* flag, mfnerf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -84,7 +84,33 @@ __global__ void finite_kernel(const float* __restrict__ x, int64_t n, int32_t* _
 }
 
 
+// Sharded data parallel: carry every rank's non-finite flag through the gradient reduce-scatter
+// itself instead of a separate all-reduce.  Before: a flagged rank writes NaN into the first
+// element of every shard; after: a shard whose first element is not finite flags the step (a NaN
+// survives the sum), so all ranks take the same decision without another collective.
+__global__ void flag_to_shards_kernel(float* g, int64_t world, int64_t shard_len, const int32_t* flag) {
+    if (*flag && (int64_t)threadIdx.x < world) g[(int64_t)threadIdx.x * shard_len] = __int_as_float(0x7fc00000);
+}
+__global__ void flag_from_shard_kernel(const float* g_shard, int32_t* flag) {
+    *flag = isfinite(g_shard[0]) ? 0 : 1;
+}
+
 }  // namespace
+
+extern "C" int mfnerf_flag_to_shards(float* grads, int64_t world, int64_t shard_len, const int32_t* flag,
+                                     mfnerf_stream_t stream) {
+    if (!grads || !flag || world < 1 || world > 1024 || shard_len < 1) {
+        mfn_set_error("flag_to_shards: bad arguments"); return MFN_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(flag_to_shards_kernel, dim3(1), dim3(1024), 0, stream, grads, world, shard_len, flag);
+    return mfn_check_launch("flag_to_shards");
+}
+
+extern "C" int mfnerf_flag_from_shard(const float* g_shard, int32_t* flag, mfnerf_stream_t stream) {
+    if (!g_shard || !flag) { mfn_set_error("flag_from_shard: null pointer"); return MFN_ERR_INVALID; }
+    hipLaunchKernelGGL(flag_from_shard_kernel, dim3(1), dim3(1), 0, stream, g_shard, flag);
+    return mfn_check_launch("flag_from_shard");
+}
 
 extern "C" int mfnerf_adam_step(float* params, float* grads, float* m, float* v, void* p_f16, int64_t n,
                                 float lr, float beta1, float beta2, float eps, float grad_scale, int step,

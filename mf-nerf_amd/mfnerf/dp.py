@@ -77,11 +77,20 @@ def all_gather_(full, rank):
     return full
 
 
-def sharded_update(grads, g_shard, p16, rank, adam_shard):
+def sharded_update(grads, g_shard, p16, rank, adam_shard, flag=None):
     """One ZeRO-1 optimizer step: reduce-scatter(mean) grads into g_shard, adam_shard(g_shard)
     updates this rank's fp32 master / m / v shard and writes its fp16 slice of p16, then the fp16
-    slices are all-gathered so every rank holds the full updated compute copy."""
+    slices are all-gathered so every rank holds the full updated compute copy.
+    flag (optional device i32[1], this rank's non-finite flag): carried through the reduce-scatter
+    (NaN in every shard's first element when set; read back from this rank's shard), so every rank
+    sees the union of the flags without another collective."""
+    from ._lib import call, ptr, stream
+    w = _world()
+    if flag is not None and w > 1:
+        call("mfnerf_flag_to_shards", ptr(grads), w, g_shard.numel(), ptr(flag), stream())
     reduce_scatter_mean_(g_shard, grads)
+    if flag is not None and w > 1:
+        call("mfnerf_flag_from_shard", ptr(g_shard), ptr(flag), stream())
     adam_shard(g_shard)
     all_gather_(p16, rank)
 

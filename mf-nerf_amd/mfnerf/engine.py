@@ -384,11 +384,8 @@ class TrainStep:
         self._pack()
 
     def _shard_adam(self, adam):
-        """Sharded: every rank's flag (its own field_bw's) is max-reduced over ranks -- one int, so
-        every rank takes the same decision -- then Adam on the shard."""
-        from . import dp
-        if self.cfg.skip_nonfinite:
-            dp.allreduce_max_(self.finite_status[:1])
+        """Sharded: the flag already holds the union over ranks (carried through the
+        reduce-scatter, dp.sharded_update), so every rank takes the same decision."""
         adam()
 
     def full_params(self):
@@ -413,11 +410,18 @@ class TrainStep:
         if self.shard is not None:
             rank, lo, hi = self.shard
             dp.sharded_update(self.grads, self.g_shard, self.p16, rank,
-                              adam or (lambda g: self._shard_adam(lambda: self._adam(g, lo, hi, False))))
+                              adam or (lambda g: self._shard_adam(lambda: self._adam(g, lo, hi, False))),
+                              flag=self.finite_status[:1] if self.cfg.skip_nonfinite else None)
             (pack or self._pack)()
         else:
             if exchange is not None:
+                # the non-finite flag rides the all-reduce: NaN in element 0 when set, read back
+                flag = self.finite_status[:1] if self.cfg.skip_nonfinite else None
+                if flag is not None:
+                    call("mfnerf_flag_to_shards", ptr(self.grads), 1, self.n_alloc, ptr(flag), stream())
                 exchange(self.grads)
+                if flag is not None:
+                    call("mfnerf_flag_from_shard", ptr(self.grads), ptr(flag), stream())
             if adam is not None:
                 adam(None)
                 (pack or (lambda: None))()
