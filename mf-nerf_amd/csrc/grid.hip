@@ -203,12 +203,26 @@ __device__ __forceinline__ int dpp_i(int v) {
 
 // ABLATE: 0 = product; debug builds: 1 plain stores, 2 levels 0-5 only, 3 levels 10-15 only.
 // MAXL: level-count bound (16 or 32) sizing the LDS tile and the prefetch registers.
-template <int ABLATE, int MAXL>
+// FIX: fixed-point accumulation -- per level l, each (run-merged) contribution v is added as the
+// int32 rint(v * scale_l) with global_atomic_add (integer atomics run ~28% faster than float ones
+// at the memory side, tools/atomic_probe3.hip), scale_l = fixed_scale(level_l1[l]); the buffers
+// then hold int32 bit patterns until fold_convert_kernel turns them back into floats.
+__device__ __forceinline__ float fixed_scale(float l1) {
+    // |entry sum| <= sum over samples of |dL/dy| of the level = l1 < 2^e, so scale 2^(30-e) keeps
+    // every entry (and every private copy of one) within 2^30: no int32 overflow is possible
+    if (!(l1 > 0.0f)) return 0.0f;
+    int e;
+    frexpf(l1, &e);
+    return ldexpf(1.0f, 30 - e);
+}
+
+template <int ABLATE, int MAXL, bool FIX>
 __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restrict__ X, int64_t n,
                                                              const int32_t* __restrict__ n_dev, float x_min,
                                                              float x_range, const mfnerf_grid_desc D,
                                                              const float* __restrict__ dy, float* __restrict__ grad,
-                                                             float* __restrict__ priv, int64_t dense_entries) {
+                                                             float* __restrict__ priv, int64_t dense_entries,
+                                                             const float* __restrict__ level_l1) {
     // dL/dy of the wave's chunk (16 samples x 2L floats) is staged in LDS (rows padded by one
     // float: conflict-free column reads) and the NEXT chunk is prefetched into registers before
     // this chunk's atomics are issued.  On gfx9 no-return atomics count in vmcnt, so a global load
@@ -255,6 +269,7 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restr
             if (ABLATE == 2 && l > 5) continue;
             if (ABLATE == 3 && l < 10) continue;
             const float g = srow[2 * l];
+            const float fs = FIX ? fixed_scale(level_l1[l]) : 0.0f;
             const LevelGeo Lg = level_geo(D.scale[l], x, y, z);
             const bool spread = priv && (int64_t)D.offset[l] + D.size[l] <= dense_entries;
             float* gt = spread ? priv + 2 * ((chunk & (GRAD_COPIES - 1)) * dense_entries + (int64_t)D.offset[l])
@@ -274,7 +289,12 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restr
                 { const float vp = dpp_f<DPP_ROW_SHL(2)>(v); const int sp = dpp_i<DPP_ROW_SHL(2)>(stop); if (!stop) { v += vp; stop = sp; } }
                 { const float vp = dpp_f<DPP_ROW_SHL(4)>(v); const int sp = dpp_i<DPP_ROW_SHL(4)>(stop); if (!stop) { v += vp; stop = sp; } }
                 { const float vp = dpp_f<DPP_ROW_SHL(8)>(v); const int sp = dpp_i<DPP_ROW_SHL(8)>(stop); if (!stop) { v += vp; stop = sp; } }
-                if (head && valid && v != 0.0f) {
+                if (FIX) {
+                    const int q = (int)rintf(v * fs);
+                    if (head && valid && q != 0)
+                        __hip_atomic_fetch_add(reinterpret_cast<int*>(gt) + 2 * idx + f, q, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                } else if (head && valid && v != 0.0f) {
                     if (ABLATE == 1) gt[2 * idx + f] = v;
                     else __hip_atomic_fetch_add(gt + 2 * idx + f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
@@ -377,6 +397,46 @@ __global__ __launch_bounds__(256) void fold_copies_kernel(float* __restrict__ pr
     }
 }
 
+// Fixed-point path: grad[p] (float) = sum_k priv[k][p] / scale for the dense prefix (copies zeroed),
+// grad[p] = int(grad[p]) / scale for the rest; scale per level from the same level_l1 as grid_bw.
+__global__ __launch_bounds__(256) void fold_convert_kernel(float* __restrict__ grad, int* __restrict__ priv,
+                                                           int64_t dense_vals, int64_t total_vals,
+                                                           const mfnerf_grid_desc D,
+                                                           const float* __restrict__ level_l1) {
+    __shared__ float inv_s[MFN_MAX_LEVELS];
+    __shared__ int64_t lo_v[MFN_MAX_LEVELS + 1];
+    if (threadIdx.x < D.n_levels) {
+        const float sc = fixed_scale(level_l1[threadIdx.x]);
+        inv_s[threadIdx.x] = sc > 0.0f ? 1.0f / sc : 0.0f;
+        lo_v[threadIdx.x] = 2 * (int64_t)D.offset[threadIdx.x];
+    }
+    if (threadIdx.x == 0) lo_v[D.n_levels] = total_vals;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int l = 0;  // level of value i (i increases per thread: walk forward)
+    for (int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; 4 * i4 < total_vals; i4 += stride) {
+        const int64_t i = 4 * i4;  // level boundaries are multiples of 16 values
+        while (l + 1 < D.n_levels && i >= lo_v[l + 1]) ++l;
+        const float is = inv_s[l];
+        int4 acc;
+        if (i < dense_vals) {
+            acc = make_int4(0, 0, 0, 0);
+#pragma unroll
+            for (int k = 0; k < GRAD_COPIES; ++k) {
+                int4* q = reinterpret_cast<int4*>(priv + k * dense_vals + i);
+                const int4 v = *q;
+                acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+                *q = make_int4(0, 0, 0, 0);
+            }
+            // the dense prefix's own entries in grad received no contributions (all went to copies)
+        } else {
+            acc = *reinterpret_cast<const int4*>(grad + i);
+        }
+        *reinterpret_cast<float4*>(grad + i) =
+            make_float4((float)acc.x * is, (float)acc.y * is, (float)acc.z * is, (float)acc.w * is);
+    }
+}
+
 int64_t dense_entries_of(const mfnerf_grid_desc* d) {
     int64_t e = 0;  // dense own-table levels are laid out first (res grows with the level)
     for (int l = 0; l < d->n_levels; ++l) {
@@ -453,7 +513,7 @@ int64_t mfnerf_grid_encode_bw_workspace(const mfnerf_grid_desc* desc) {
 
 int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                           const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table, void* workspace,
-                          mfnerf_stream_t stream) {
+                          const float* level_l1, mfnerf_stream_t stream) {
     int st = check_desc(desc, "grid_encode_bw");
     if (st) return st;
     if (n < 0) { mfn_set_error("grid_encode_bw: bad size"); return MFN_ERR_INVALID; }
@@ -463,9 +523,24 @@ int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float
     const int64_t cap = grid_bw_block_cap();
     const int64_t blocks = want < cap ? want : cap;
     const int64_t dense = workspace ? dense_entries_of(desc) : 0;
-    auto kern = desc->n_levels <= 16 ? grid_bw_kernel<0, 16> : grid_bw_kernel<0, MFN_MAX_LEVELS>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0,
-                       stream, x, n, n_dev, x_min, x_range, *desc, dL_dout, grad_table, (float*)workspace, dense);
+    const bool big = desc->n_levels > 16;
+    if (level_l1) {
+        auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, true> : grid_bw_kernel<0, 16, true>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range,
+                           *desc, dL_dout, grad_table, (float*)workspace, dense, level_l1);
+        int64_t total = 0;
+        for (int l = 0; l < desc->n_levels; ++l) {
+            const int64_t e = 2 * ((int64_t)desc->offset[l] + desc->size[l]);
+            total = e > total ? e : total;
+        }
+        const int64_t fb = div_up<int64_t>(total / 4, 256);
+        hipLaunchKernelGGL(fold_convert_kernel, dim3((unsigned)(fb < 4096 ? fb : 4096)), dim3(256), 0, stream,
+                           grad_table, (int*)workspace, 2 * dense, total, *desc, level_l1);
+        return mfn_check_launch("grid_encode_bw");
+    }
+    auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, false> : grid_bw_kernel<0, 16, false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc,
+                       dL_dout, grad_table, (float*)workspace, dense, (const float*)nullptr);
     if (dense > 0) {
         const int64_t nf = 2 * dense;  // multiple of 16 (level sizes are multiples of 8)
         const int64_t fb = div_up<int64_t>(nf / 4, 256);
@@ -473,6 +548,31 @@ int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float
                            (float*)workspace, nf, grad_table);
     }
     return mfn_check_launch("grid_encode_bw");
+}
+
+// Per-level L1 norm of dL/dout (n, L*F) f32: out[l] += sum_i |dy[i][2l]| + |dy[i][2l+1]| (the bound
+// the fixed-point backward sizes its scales with, when the producer does not supply it).
+__global__ __launch_bounds__(256) void level_l1_kernel(const float* __restrict__ dy, int64_t n,
+                                                       const int32_t* __restrict__ n_dev, int L,
+                                                       float* __restrict__ out) {
+    __shared__ float part[MFN_MAX_LEVELS];
+    if (threadIdx.x < L) part[threadIdx.x] = 0.0f;
+    __syncthreads();
+    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
+    const int row = 2 * L;
+    // thread t handles column pair (level) l = t % L of rows t / L, t / L + stride/L, ...
+    const int l = threadIdx.x % L;
+    const int64_t r0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / L;
+    const int64_t rstride = ((int64_t)gridDim.x * blockDim.x) / L;
+    float acc = 0.0f;
+    if ((int)threadIdx.x < (int)(blockDim.x / L) * L)
+        for (int64_t r = r0; r < nn; r += rstride) {
+            const float2 v = *reinterpret_cast<const float2*>(dy + r * row + 2 * l);
+            acc += fabsf(v.x) + fabsf(v.y);
+        }
+    atomicAdd(&part[l], acc);
+    __syncthreads();
+    if (threadIdx.x < L) atomicAdd(out + threadIdx.x, part[threadIdx.x]);
 }
 
 int mfnerf_debug_grid_bw_half(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
@@ -488,6 +588,18 @@ int mfnerf_debug_grid_bw_half(const float* x, int64_t n, const int32_t* n_dev, f
     return mfn_check_launch("grid_bw_half");
 }
 
+int mfnerf_grid_level_l1(const float* dL_dout, int64_t n, const int32_t* n_dev, int n_levels, float* out,
+                         mfnerf_stream_t stream) {
+    if (n < 0 || n_levels <= 0 || n_levels > MFN_MAX_LEVELS || !out || (n > 0 && !dL_dout)) {
+        mfn_set_error("grid_level_l1: bad arguments"); return MFN_ERR_INVALID;
+    }
+    if (n == 0) return MFN_OK;
+    const int64_t want = div_up<int64_t>(n * n_levels, 256);
+    hipLaunchKernelGGL(level_l1_kernel, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(256), 0, stream, dL_dout, n,
+                       n_dev, n_levels, out);
+    return mfn_check_launch("grid_level_l1");
+}
+
 // Debug (not part of the training path): the same launch with an ablated kernel body.
 int mfnerf_debug_grid_bw_ablate(int mode, const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                                 const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
@@ -495,12 +607,12 @@ int mfnerf_debug_grid_bw_ablate(int mode, const float* x, int64_t n, const int32
     const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16), ENC_BLOCK / 64);
     const int64_t blocks = want < 4096 ? want : 4096;
     if (desc->n_levels > 16) { mfn_set_error("grid_bw_ablate: n_levels <= 16 only"); return MFN_ERR_INVALID; }
-    auto k = mode == 1   ? grid_bw_kernel<1, 16>
-             : mode == 2 ? grid_bw_kernel<2, 16>
-             : mode == 3 ? grid_bw_kernel<3, 16>
-                         : grid_bw_kernel<0, 16>;
+    auto k = mode == 1   ? grid_bw_kernel<1, 16, false>
+             : mode == 2 ? grid_bw_kernel<2, 16, false>
+             : mode == 3 ? grid_bw_kernel<3, 16, false>
+                         : grid_bw_kernel<0, 16, false>;
     hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc,
-                       dL_dout, grad_table, nullptr, (int64_t)0);
+                       dL_dout, grad_table, nullptr, (int64_t)0, (const float*)nullptr);
     return mfn_check_launch("grid_bw_ablate");
 }
 

@@ -59,7 +59,8 @@ SIGNATURES = {
     "mfnerf_grid_encode_fw": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P]),
     "mfnerf_grid_encode_fw_planar": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _I64, _P]),
     "mfnerf_grid_encode_bw_workspace": (_I64, [ctypes.POINTER(GridDesc)]),
-    "mfnerf_grid_encode_bw": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _P]),
+    "mfnerf_grid_encode_bw": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _P, _P]),
+    "mfnerf_grid_level_l1": (_I, [_P, _I64, _P, _I, _P, _P]),
     "mfnerf_debug_grid_bw_half": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _F, _P]),
     "mfnerf_debug_grid_bw_ablate": (_I, [_I, _P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P]),
     "mfnerf_field_packed_bytes": (_I64, [_I]),

@@ -55,6 +55,7 @@ class StepConfig:
     max_samples: int = MAX_SAMPLES
     n_parts: int = 1
     skip_nonfinite: bool = True  # GradScaler semantics: no optimizer step on an inf/nan gradient
+    fixed_point_grid: bool = True  # table gradient by int32 fixed-point atomics (n_parts == 1)
 
 
 @dataclass
@@ -141,6 +142,7 @@ class TrainStep:
         # the step's loss as partial sums: one per 4 rays of each part (written by the fused
         # compositing kernel) + 64 accumulated slots (unfused path: NeRFLoss atomics, distortion)
         self._nb_part = -(-self.Np // 4)
+        self._level_l1 = torch.zeros(c.L, dtype=torch.float32, device=dev)
         self.loss_parts = torch.zeros(c.n_parts * self._nb_part + 64, dtype=torch.float32, device=dev)
         self._loss_acc = self.loss_parts[c.n_parts * self._nb_part:]
         self.state = _State()
@@ -359,10 +361,18 @@ class TrainStep:
         mark("field_bw")
 
     def _grid_bw(self, mb, q):
-        """Part q's hash-table gradient scatter (the dominant kernel)."""
-        t, m = self.parts[q], mb.part[q]
+        """Part q's hash-table gradient scatter (the dominant kernel).  One part: int32 fixed-point
+        atomics (per-level scales bounded by the L1 norm of dL/dfeat, so no overflow; the table
+        gradient starts at zero because Adam zeroed it); several parts share the gradient, so they
+        accumulate with float atomics."""
+        t, m, s = self.parts[q], mb.part[q], stream()
+        l1 = None
+        if self.n_parts == 1 and self.cfg.fixed_point_grid:
+            l1 = self._level_l1
+            l1.zero_()
+            call("mfnerf_grid_level_l1", ptr(t.dfeat), self.cap_p, ptr(m.counter), self.cfg.L, ptr(l1), s)
         call("mfnerf_grid_encode_bw", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min, self.x_range, self.desc,
-             ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws), stream())
+             ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws), ptr(l1), s)
 
     def _reduce_parts(self):
         """Fold parts 1.. MLP weight grads into grads (the table part is already shared)."""

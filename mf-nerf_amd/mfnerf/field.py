@@ -33,9 +33,16 @@ def grid_bw_workspace(desc, device):
     return torch.zeros(max(nb, 16) // 4, dtype=torch.float32, device=device)
 
 
-def grid_encode_bw(x, n, dL_dfeat, grad_table, layout, desc, x_min=0.0, x_range=1.0, n_dev=None, workspace=None):
+def grid_encode_bw(x, n, dL_dfeat, grad_table, layout, desc, x_min=0.0, x_range=1.0, n_dev=None, workspace=None,
+                   fixed_point=False):
+    """Accumulates into grad_table (float atomics); fixed_point=True: int32 fixed-point atomics with
+    per-level scales from the L1 norm of dL_dfeat (grad_table must be zero; it is overwritten)."""
+    l1 = None
+    if fixed_point:
+        l1 = torch.zeros(layout.L, dtype=torch.float32, device=x.device)
+        call("mfnerf_grid_level_l1", ptr(dL_dfeat), int(n), ptr(n_dev), layout.L, ptr(l1), stream())
     call("mfnerf_grid_encode_bw", ptr(x), int(n), ptr(n_dev), float(x_min), float(x_range), desc, ptr(dL_dfeat),
-         ptr(grad_table), ptr(workspace), stream())
+         ptr(grad_table), ptr(workspace), ptr(l1), stream())
 
 
 def pack_field_weights(params_xyz_net, params_rgb, rgb_width=64, out=None):

@@ -65,14 +65,26 @@ def test_grid_encode_fw_bw(gpu, name, args):
         assert torch.allclose(gt.cpu(), 2 * gref, rtol=1e-4, atol=2e-4 * float(gref.abs().max()))
         if ws is not None:
             assert int((ws != 0).sum()) == 0
+    # fixed-point path (int32 atomics, per-level scale from the L1 norm of dy): same sums to the
+    # level resolution, and bit-reproducible (integer atomics are order-independent)
+    fx = []
+    for ws in (FLD.grid_bw_workspace(desc, gpu), None, FLD.grid_bw_workspace(desc, gpu)):
+        gt = torch.zeros(lay.n_params, device=gpu)
+        FLD.grid_encode_bw(xg, N, dyg, gt, lay, desc, workspace=ws, fixed_point=True)
+        assert torch.allclose(gt.cpu(), gref, rtol=1e-4, atol=1e-4 * float(gref.abs().max()))
+        if ws is not None:
+            assert int((ws != 0).sum()) == 0
+        fx.append(gt)
+    assert torch.equal(fx[0], fx[1]) and torch.equal(fx[0], fx[2])
     m = 4099  # not a multiple of the 16-sample chunk: the live count comes from the device
     tp = table.clone().requires_grad_(True)
     (FO.grid_encode(x[:m], tp, olay) * dy[:m]).sum().backward()
     n_dev = torch.tensor([m], dtype=torch.int32, device=gpu)
     for ws in (FLD.grid_bw_workspace(desc, gpu), None):
-        gt = torch.zeros(lay.n_params, device=gpu)
-        FLD.grid_encode_bw(xg, N, dyg, gt, lay, desc, n_dev=n_dev, workspace=ws)
-        assert torch.allclose(gt.cpu(), tp.grad, rtol=1e-4, atol=1e-4 * float(tp.grad.abs().max()))
+        for fixed in (False, True):
+            gt = torch.zeros(lay.n_params, device=gpu)
+            FLD.grid_encode_bw(xg, N, dyg, gt, lay, desc, n_dev=n_dev, workspace=ws, fixed_point=fixed)
+            assert torch.allclose(gt.cpu(), tp.grad, rtol=1e-4, atol=1e-4 * float(tp.grad.abs().max()))
 
 
 def test_grid_encode_bw_along_rays(gpu):
@@ -92,9 +104,52 @@ def test_grid_encode_bw_along_rays(gpu):
     (FO.grid_encode(x, table, olay) * dy).sum().backward()
     gref = table.grad
     desc = lay.desc()
+    for fixed in (False, True):
+        gt = torch.zeros(lay.n_params, device=gpu)
+        FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=FLD.grid_bw_workspace(desc, gpu),
+                           fixed_point=fixed)
+        assert torch.allclose(gt.cpu(), gref, rtol=1e-4, atol=1e-4 * float(gref.abs().max()))
+    # the training regime: per-sample gradients ~1e-7 of very different size per level; the
+    # fixed-point resolution (2^-30 of each level's L1) stays far below fp32's relative error
+    dys = dy * torch.logspace(-9, -5, 32).view(1, 32)
+    tp = torch.zeros(lay.n_params).requires_grad_(True)
+    (FO.grid_encode(x, tp, olay).double() * dys.double()).sum().backward()
+    gref = tp.grad.double()
     gt = torch.zeros(lay.n_params, device=gpu)
-    FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=FLD.grid_bw_workspace(desc, gpu))
-    assert torch.allclose(gt.cpu(), gref, rtol=1e-4, atol=1e-4 * float(gref.abs().max()))
+    FLD.grid_encode_bw(x.to(gpu), N, dys.to(gpu), gt, lay, desc, workspace=FLD.grid_bw_workspace(desc, gpu),
+                       fixed_point=True)
+    got = gt.cpu().double()
+    for l in range(16):
+        a, b = lay.offsets[l] * 2, lay.offsets[l + 1] * 2 if l + 1 < 16 else lay.n_params
+        scale = float(gref[a:b].abs().max())
+        if scale > 0:
+            err = float((got[a:b] - gref[a:b]).abs().max()) / scale
+            assert err < 1e-4, (l, err)
+
+
+def test_grid_encode_bw_fixed_point_extreme_range(gpu):
+    """No int32 overflow whatever the gradient magnitude (the scale follows the L1 bound), and an
+    all-zero gradient leaves the table gradient zero."""
+    lay = GridLayout(16, 2, 14, 16, LEGO_B)
+    olay = FO.GridLayout(16, 2, 14, 16, LEGO_B)
+    g = torch.Generator().manual_seed(9)
+    N = 3000
+    x = torch.rand(N, 3, generator=g)
+    desc = lay.desc()
+    for mag in (1e-30, 1e-3, 1e12, 1e30):
+        dy = torch.randn(N, 32, generator=g) * mag
+        tp = torch.zeros(lay.n_params).requires_grad_(True)
+        (FO.grid_encode(x, tp, olay).double() * dy.double()).sum().backward()
+        gref = tp.grad.double()
+        gt = torch.zeros(lay.n_params, device=gpu)
+        FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=FLD.grid_bw_workspace(desc, gpu),
+                           fixed_point=True)
+        got = gt.cpu().double()
+        assert torch.isfinite(got).all()
+        assert float((got - gref).abs().max()) <= 1e-4 * float(gref.abs().max()), mag
+    gt = torch.ones(lay.n_params, device=gpu) * 0
+    FLD.grid_encode_bw(x.to(gpu), N, torch.zeros(N, 32, device=gpu), gt, lay, desc, fixed_point=True)
+    assert int((gt != 0).sum()) == 0
 
 
 def test_grid_encode_world_coords_normalisation(gpu):
