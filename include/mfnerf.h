@@ -188,6 +188,15 @@ int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float
                           const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table, void* workspace,
                           const float* level_l1, mfnerf_stream_t stream);
 
+/* mfnerf_grid_encode_bw in two calls (the scatter, then the fold of the private copies /
+ * fixed-point conversion), so the scatter can be timed on its own and the finish scheduled later
+ * (anything reading grad_table must come after the finish). */
+int mfnerf_grid_encode_bw_scatter(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                                  const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
+                                  void* workspace, const float* level_l1, mfnerf_stream_t stream);
+int mfnerf_grid_encode_bw_finish(const mfnerf_grid_desc* desc, float* grad_table, void* workspace,
+                                 const float* level_l1, mfnerf_stream_t stream);
+
 /* out[l] += sum over rows i < n (or *n_dev) of |dL_dout[i][2l]| + |dL_dout[i][2l+1]| (f32). */
 int mfnerf_grid_level_l1(const float* dL_dout, int64_t n, const int32_t* n_dev, int n_levels, float* out,
                          mfnerf_stream_t stream);
@@ -234,11 +243,13 @@ int mfnerf_field_fw(const void* feat_f16, int64_t feat_plane_stride, const float
  * workspace: mfnerf_field_bw_workspace() bytes (per-workgroup weight-grad slab).
  * nonfinite (optional device i32): set to 1 when any dL_dfeat or weight gradient is inf/nan (the
  * table gradient of mfnerf_grid_encode_bw is a weighted sum of dL_dfeat, so this flags the whole
- * step's gradient without scanning it; feeds mfnerf_adam_step's skip). */
+ * step's gradient without scanning it; feeds mfnerf_adam_step's skip).
+ * level_l1 (optional device f32[16], ACCUMULATED): the per-level L1 norm of dL_dfeat, i.e. what
+ * mfnerf_grid_level_l1 computes, for free (the fixed-point scales of mfnerf_grid_encode_bw). */
 int64_t mfnerf_field_bw_workspace(int64_t n, int rgb_width);
 int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
                     int rgb_width, const float* dL_dsigma, const float* dL_drgb, float grad_scale, float* dL_dfeat,
-                    float* grad_xyz, float* grad_rgb, void* workspace, int32_t* nonfinite,
+                    float* grad_xyz, float* grad_rgb, void* workspace, int32_t* nonfinite, float* level_l1,
                     mfnerf_stream_t stream);
 
 /* Debug: one v_mfma_f32_32x32x16_f16 with A (32x16) and B (16x32) f16 row-major -> D (32x32) f32,

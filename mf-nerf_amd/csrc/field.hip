@@ -367,7 +367,8 @@ __device__ __forceinline__ void dw_add32(float* img, const f32x16& a, int ot, in
 __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
     const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev,
     const _Float16* __restrict__ packed, const float* __restrict__ dL_dsigma, const float* __restrict__ dL_drgb,
-    float grad_scale, float* __restrict__ dL_dfeat, float* __restrict__ slab, int32_t* __restrict__ nonfinite) {
+    float grad_scale, float* __restrict__ dL_dfeat, float* __restrict__ slab, int32_t* __restrict__ nonfinite,
+    float* __restrict__ level_l1) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     _Float16* lds_base = reinterpret_cast<_Float16*>(smem);
     load_frags_bw(lds_base, packed);
@@ -400,6 +401,9 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
     };
     const int64_t tile0 = (int64_t)blockIdx.x * 4 + wid;
     if (tile0 < tiles) fetch(tile0);
+    // per-level L1 of dL/dfeat (the fixed-point table-gradient scales): this lane's 8 levels are
+    // 4g + 2h (features 8g+4h, +1) and 4g + 2h + 1 (features 8g+4h+2, +3), g = 0..3
+    float l1a[4] = {0.f, 0.f, 0.f, 0.f}, l1b[4] = {0.f, 0.f, 0.f, 0.f};
     for (int64_t tile = tile0; tile < tiles; tile += stride) {
         // the fragment reads are loop-invariant; an opaque base keeps the compiler from hoisting
         // all 48 of them (192 registers) out of the loop
@@ -515,6 +519,8 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
                                                  dx[4 * g + 3] * invS);
                     bad |= !(isfinite(o.x) && isfinite(o.y) && isfinite(o.z) && isfinite(o.w));
                     dst[2 * g + h] = o;
+                    l1a[g] += fabsf(o.x) + fabsf(o.y);
+                    l1b[g] += fabsf(o.z) + fabsf(o.w);
                 }
             }
             // the table gradient is sum(weight * dL/dfeat): non-finite only if some dL/dfeat is
@@ -526,7 +532,18 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
     __syncthreads();
     float* img = reinterpret_cast<float*>(smem);  // reuses the fragment area (N_DW*4 <= fragments)
     for (int i = threadIdx.x; i < N_DW; i += blockDim.x) img[i] = 0.0f;
+    float* l1_part = img + N_DW;                  // 16 floats after the image
+    if (threadIdx.x < 16) l1_part[threadIdx.x] = 0.0f;
     __syncthreads();
+    if (level_l1) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            float a = l1a[g], b = l1b[g];
+#pragma unroll
+            for (int off = 16; off > 0; off >>= 1) { a += __shfl_xor(a, off, 64); b += __shfl_xor(b, off, 64); }
+            if (r == 0) { atomicAdd(l1_part + 4 * g + 2 * h, a); atomicAdd(l1_part + 4 * g + 2 * h + 1, b); }
+        }
+    }
     float* ix = img;
     float* ir = img + N_XYZ_PARAMS;
     float* ir2 = ir + RGB_W * 32;
@@ -543,6 +560,7 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
     __syncthreads();
     float* row = slab + (int64_t)blockIdx.x * N_DW;
     for (int i = threadIdx.x; i < N_DW; i += blockDim.x) row[i] = img[i] * invS;
+    if (level_l1 && threadIdx.x < 16) atomicAdd(level_l1 + threadIdx.x, l1_part[threadIdx.x]);
 }
 
 // grad[p] += sum over slab rows (fixed order: deterministic).  64 columns x 4 row groups per block.
@@ -567,7 +585,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 
 constexpr int BW_BLOCKS = 256;
 constexpr size_t BW_LDS = (size_t)N_FRAGS_BW * FRAG_HALFS * 2;
-static_assert((size_t)N_DW * 4 <= BW_LDS, "reduction image must fit the bw LDS");
+static_assert((size_t)N_DW * 4 + 64 <= BW_LDS, "reduction image must fit the bw LDS");
 
 // debug: one MFMA with A (32x16) and B (16x32) f16 row-major -> D (32x32) f32, to pin the lane maps
 __global__ void mfma_probe_kernel(const _Float16* A, const _Float16* B, float* D) {
@@ -642,7 +660,8 @@ int64_t mfnerf_field_bw_workspace(int64_t n, int rgb_width) {
 int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float* dirs, int64_t n,
                     const int32_t* n_dev, const void* packed,
                     int rgb_width, const float* dL_dsigma, const float* dL_drgb, float grad_scale, float* dL_dfeat,
-                    float* grad_xyz, float* grad_rgb, void* workspace, int32_t* nonfinite, mfnerf_stream_t stream) {
+                    float* grad_xyz, float* grad_rgb, void* workspace, int32_t* nonfinite, float* level_l1,
+                    mfnerf_stream_t stream) {
     if (rgb_width != RGB_W) { mfn_set_error("field: rgb_width=%d unsupported (this build: %d)", rgb_width, RGB_W); return MFN_ERR_INVALID; }
     if (n < 0 || !(grad_scale > 0.0f) || (feat_plane_stride != 0 && feat_plane_stride < n)) {
         mfn_set_error("field_bw: bad size, plane stride or grad_scale"); return MFN_ERR_INVALID;
@@ -653,7 +672,7 @@ int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float
     }
     hipLaunchKernelGGL(field_bw_kernel, dim3(BW_BLOCKS), dim3(FIELD_BLOCK), BW_LDS, stream, (const _Float16*)feat_f16,
                        feat_plane_stride, dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb, grad_scale, dL_dfeat,
-                       (float*)workspace, nonfinite);
+                       (float*)workspace, nonfinite, level_l1);
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((N_DW + 63) / 64), dim3(256), 0, stream, (const float*)workspace,
                        BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
     return mfn_check_launch("field_bw");

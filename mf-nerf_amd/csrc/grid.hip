@@ -511,9 +511,9 @@ int64_t mfnerf_grid_encode_bw_workspace(const mfnerf_grid_desc* desc) {
     return (int64_t)GRAD_COPIES * dense_entries_of(desc) * 2 * (int64_t)sizeof(float);
 }
 
-int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
-                          const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table, void* workspace,
-                          const float* level_l1, mfnerf_stream_t stream) {
+int mfnerf_grid_encode_bw_scatter(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                                  const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
+                                  void* workspace, const float* level_l1, mfnerf_stream_t stream) {
     int st = check_desc(desc, "grid_encode_bw");
     if (st) return st;
     if (n < 0) { mfn_set_error("grid_encode_bw: bad size"); return MFN_ERR_INVALID; }
@@ -528,6 +528,21 @@ int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float
         auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, true> : grid_bw_kernel<0, 16, true>;
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range,
                            *desc, dL_dout, grad_table, (float*)workspace, dense, level_l1);
+    } else {
+        auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, false> : grid_bw_kernel<0, 16, false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range,
+                           *desc, dL_dout, grad_table, (float*)workspace, dense, (const float*)nullptr);
+    }
+    return mfn_check_launch("grid_encode_bw_scatter");
+}
+
+int mfnerf_grid_encode_bw_finish(const mfnerf_grid_desc* desc, float* grad_table, void* workspace,
+                                 const float* level_l1, mfnerf_stream_t stream) {
+    int st = check_desc(desc, "grid_encode_bw_finish");
+    if (st) return st;
+    if (!grad_table) { mfn_set_error("grid_encode_bw_finish: null pointer"); return MFN_ERR_INVALID; }
+    const int64_t dense = workspace ? dense_entries_of(desc) : 0;
+    if (level_l1) {
         int64_t total = 0;
         for (int l = 0; l < desc->n_levels; ++l) {
             const int64_t e = 2 * ((int64_t)desc->offset[l] + desc->size[l]);
@@ -536,18 +551,23 @@ int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float
         const int64_t fb = div_up<int64_t>(total / 4, 256);
         hipLaunchKernelGGL(fold_convert_kernel, dim3((unsigned)(fb < 4096 ? fb : 4096)), dim3(256), 0, stream,
                            grad_table, (int*)workspace, 2 * dense, total, *desc, level_l1);
-        return mfn_check_launch("grid_encode_bw");
-    }
-    auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, false> : grid_bw_kernel<0, 16, false>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc,
-                       dL_dout, grad_table, (float*)workspace, dense, (const float*)nullptr);
-    if (dense > 0) {
+    } else if (dense > 0) {
         const int64_t nf = 2 * dense;  // multiple of 16 (level sizes are multiples of 8)
         const int64_t fb = div_up<int64_t>(nf / 4, 256);
         hipLaunchKernelGGL(fold_copies_kernel, dim3((unsigned)(fb < 2048 ? fb : 2048)), dim3(256), 0, stream,
                            (float*)workspace, nf, grad_table);
     }
-    return mfn_check_launch("grid_encode_bw");
+    return mfn_check_launch("grid_encode_bw_finish");
+}
+
+int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                          const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table, void* workspace,
+                          const float* level_l1, mfnerf_stream_t stream) {
+    if (n == 0 && n >= 0) return MFN_OK;
+    int st = mfnerf_grid_encode_bw_scatter(x, n, n_dev, x_min, x_range, desc, dL_dout, grad_table, workspace,
+                                           level_l1, stream);
+    if (st) return st;
+    return mfnerf_grid_encode_bw_finish(desc, grad_table, workspace, level_l1, stream);
 }
 
 // Per-level L1 norm of dL/dout (n, L*F) f32: out[l] += sum_i |dy[i][2l]| + |dy[i][2l+1]| (the bound
@@ -570,7 +590,9 @@ __global__ __launch_bounds__(256) void level_l1_kernel(const float* __restrict__
             const float2 v = *reinterpret_cast<const float2*>(dy + r * row + 2 * l);
             acc += fabsf(v.x) + fabsf(v.y);
         }
-    atomicAdd(&part[l], acc);
+    // reduce the 256/L lanes of each level inside the wave first (lanes l, l+L, ... share a level)
+    for (int off = 32; off >= L; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if ((threadIdx.x & 63) < L) atomicAdd(&part[l], acc);
     __syncthreads();
     if (threadIdx.x < L) atomicAdd(out + threadIdx.x, part[threadIdx.x]);
 }
@@ -594,9 +616,11 @@ int mfnerf_grid_level_l1(const float* dL_dout, int64_t n, const int32_t* n_dev, 
         mfn_set_error("grid_level_l1: bad arguments"); return MFN_ERR_INVALID;
     }
     if (n == 0) return MFN_OK;
-    const int64_t want = div_up<int64_t>(n * n_levels, 256);
-    hipLaunchKernelGGL(level_l1_kernel, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(256), 0, stream, dL_dout, n,
-                       n_dev, n_levels, out);
+    // one workgroup per CU at most: the 16 per-level sums are atomics on 16 addresses, which
+    // serialise at the memory side -- 2048 workgroups made this 36 us, most of it in that tail
+    const int64_t want = div_up<int64_t>(n * n_levels, 256 * 16);
+    hipLaunchKernelGGL(level_l1_kernel, dim3((unsigned)(want < 256 ? (want < 1 ? 1 : want) : 256)), dim3(256), 0,
+                       stream, dL_dout, n, n_dev, n_levels, out);
     return mfn_check_launch("grid_level_l1");
 }
 

@@ -60,6 +60,8 @@ SIGNATURES = {
     "mfnerf_grid_encode_fw_planar": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _I64, _P]),
     "mfnerf_grid_encode_bw_workspace": (_I64, [ctypes.POINTER(GridDesc)]),
     "mfnerf_grid_encode_bw": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _P, _P]),
+    "mfnerf_grid_encode_bw_scatter": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _P, _P]),
+    "mfnerf_grid_encode_bw_finish": (_I, [ctypes.POINTER(GridDesc), _P, _P, _P, _P]),
     "mfnerf_grid_level_l1": (_I, [_P, _I64, _P, _I, _P, _P]),
     "mfnerf_debug_grid_bw_half": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _F, _P]),
     "mfnerf_debug_grid_bw_ablate": (_I, [_I, _P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P]),
@@ -68,7 +70,7 @@ SIGNATURES = {
     "mfnerf_field_pack_weights": (_I, [_P, _P, _I, _P, _P]),
     "mfnerf_field_fw": (_I, [_P, _I64, _P, _I64, _P, _P, _I, _I, _P, _P, _P]),
     "mfnerf_field_bw_workspace": (_I64, [_I64, _I]),
-    "mfnerf_field_bw": (_I, [_P, _I64, _P, _I64, _P, _P, _I, _P, _P, _F, _P, _P, _P, _P, _P, _P]),
+    "mfnerf_field_bw": (_I, [_P, _I64, _P, _I64, _P, _P, _I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P]),
     "mfnerf_debug_mfma_probe": (_I, [_P, _P, _P, _P]),
     "mfnerf_occupancy_workspace": (_I64, [_I, _I]),
     "mfnerf_occupancy_points": (_I64, [_I, _I, _I64, _I]),

@@ -317,6 +317,8 @@ class TrainStep:
         t, m = self.parts[q], mb.part[q]
         Np, cap = self.Np, self.cap_p
         if q == 0:
+            if self._fixed():
+                self._level_l1.zero_()  # accumulated by field_bw
             if self.shard is not None:
                 self.grads.zero_()  # unsharded: the previous Adam pass left it zero
             if c.lambda_distortion > 0:
@@ -357,22 +359,28 @@ class TrainStep:
         call("mfnerf_field_bw", ptr(t.feat), cap, ptr(m.dirs), cap, ptr(m.counter), ptr(self.packed), c.rgb_width,
              ptr(t.dsig), ptr(t.drgb_s), self.grad_scale, ptr(t.dfeat), ptr(t.mlp_grad),
              ptr(t.mlp_grad[self.off_rgb:]), ptr(t.field_ws),
-             ptr(self.finite_status) if c.skip_nonfinite else None, s)
+             ptr(self.finite_status) if c.skip_nonfinite else None,
+             ptr(self._level_l1) if self._fixed() else None, s)
         mark("field_bw")
 
+    def _fixed(self):
+        """One part: the table gradient is accumulated by int32 fixed-point atomics (per-level scales
+        bounded by the L1 norm of dL/dfeat, which field_bw accumulates, so no overflow; the table
+        gradient starts at zero because Adam zeroed it); several parts share the gradient and use
+        float atomics."""
+        return self.n_parts == 1 and self.cfg.fixed_point_grid
+
     def _grid_bw(self, mb, q):
-        """Part q's hash-table gradient scatter (the dominant kernel).  One part: int32 fixed-point
-        atomics (per-level scales bounded by the L1 norm of dL/dfeat, so no overflow; the table
-        gradient starts at zero because Adam zeroed it); several parts share the gradient, so they
-        accumulate with float atomics."""
-        t, m, s = self.parts[q], mb.part[q], stream()
-        l1 = None
-        if self.n_parts == 1 and self.cfg.fixed_point_grid:
-            l1 = self._level_l1
-            l1.zero_()
-            call("mfnerf_grid_level_l1", ptr(t.dfeat), self.cap_p, ptr(m.counter), self.cfg.L, ptr(l1), s)
-        call("mfnerf_grid_encode_bw", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min, self.x_range, self.desc,
-             ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws), ptr(l1), s)
+        """Part q's hash-table gradient scatter (the dominant kernel, alone so it can be timed)."""
+        t, m = self.parts[q], mb.part[q]
+        call("mfnerf_grid_encode_bw_scatter", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min, self.x_range,
+             self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws),
+             ptr(self._level_l1) if self._fixed() else None, stream())
+
+    def _grid_finish(self, q):
+        """Fold part q's private copies of the coarse levels / convert the fixed-point sums."""
+        call("mfnerf_grid_encode_bw_finish", self.desc, ptr(self.grads[self.off_table:]), ptr(self.parts[q].grid_ws),
+             ptr(self._level_l1) if self._fixed() else None, stream())
 
     def _reduce_parts(self):
         """Fold parts 1.. MLP weight grads into grads (the table part is already shared)."""
@@ -455,6 +463,8 @@ class TrainStep:
             self._chain(batch, mb, q, mark)
             self._grid_bw(mb, q)
             mark("grid_bw")
+            self._grid_finish(q)
+            mark("grid_finish")
         self._reduce_parts()
         self._optimize(exchange)
         mark("update")
@@ -508,6 +518,7 @@ class TrainStep:
             "chain": [[cap(lambda j=j, q=q: self._chain(self._static[j], self.mbuf[j], q, nomark)) for q in range(P)]
                       for j in range(2)],
             "grid_bw": [[cap(lambda j=j, q=q: self._grid_bw(self.mbuf[j], q)) for q in range(P)] for j in range(2)],
+            "finish": [cap(lambda q=q: self._grid_finish(q)) for q in range(P)],
             "reduce": cap(self._reduce_parts) if P > 1 else None,
         }
         if self.shard is not None:
@@ -584,6 +595,9 @@ class TrainStep:
                 g["grid_bw"][j][q].replay()
                 if grid_bw_events is not None:
                     grid_bw_events[1][q].record(sq)
+                if q > 0:  # the folds read-modify-write the shared gradient: one part at a time
+                    sq.wait_event(self._ev_part[q - 1])
+                g["finish"][q].replay()
                 self._ev_part[q].record(sq)
         for q in range(1, P):
             main.wait_event(self._ev_part[q])

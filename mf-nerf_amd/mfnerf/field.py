@@ -75,7 +75,7 @@ def field_bw(feat, dirs, n, packed, dL_dsigma, dL_drgb, grad_scale, dL_dfeat, gr
              rgb_width=64, n_dev=None, nonfinite=None):
     call("mfnerf_field_bw", ptr(feat), 0, ptr(dirs), int(n), ptr(n_dev), ptr(packed), int(rgb_width), ptr(dL_dsigma),
          ptr(dL_drgb), float(grad_scale), ptr(dL_dfeat), ptr(grad_xyz_net), ptr(grad_rgb), ptr(workspace),
-         ptr(nonfinite), stream())
+         ptr(nonfinite), None, stream())
 
 
 def pow2_grad_scale(max_abs):

@@ -268,7 +268,7 @@ def test_planar_encode_and_field_match_row_major(gpu, name, args):
         gx, gr = torch.zeros(3072, device=gpu), torch.zeros(7168, device=gpu)
         ws = FLD.field_bw_workspace(N, 64, gpu)
         call("mfnerf_field_bw", ptr(feat), stride, ptr(dg), N, None, ptr(packed), 64, ptr(dsig), ptr(drgb), 4096.0,
-             ptr(dfeat), ptr(gx), ptr(gr), ptr(ws), None, st)
+             ptr(dfeat), ptr(gx), ptr(gr), ptr(ws), None, None, st)
         torch.cuda.synchronize()
         outs.append((dfeat, gx, gr))
     assert torch.equal(outs[0][0], outs[1][0])

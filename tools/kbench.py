@@ -57,8 +57,9 @@ def main():
                                   ptr(t.dL_drgb), ptr(t.dL_dop), ptr(t.dsig), ptr(t.drgb_s), ptr(step.loss_parts), s()),
         "field_bw": lambda: call("mfnerf_field_bw", ptr(t.feat), cap, ptr(m.dirs), cap, ptr(m.counter), ptr(step.packed),
                                  c.rgb_width, ptr(t.dsig), ptr(t.drgb_s), step.grad_scale, ptr(t.dfeat),
-                                 ptr(t.mlp_grad), ptr(t.mlp_grad[step.off_rgb:]), ptr(t.field_ws), None, s()),
+                                 ptr(t.mlp_grad), ptr(t.mlp_grad[step.off_rgb:]), ptr(t.field_ws), None, None, s()),
         "grid_bw": lambda: step._grid_bw(mb, 0),
+        "grid_finish": lambda: step._grid_finish(0),
         "grid_bw_half": lambda: call("mfnerf_debug_grid_bw_half", ptr(m.xyzs), cap, ptr(m.counter), step.x_min,
                                      step.x_range, step.desc, ptr(t.dfeat), ptr(grad_h2), ptr(priv_h2), 2048.0, s()),
         "check": lambda: call("mfnerf_check_finite", ptr(step.grads), step.grads.numel(), ptr(step.finite_status), s()),
