@@ -1,7 +1,8 @@
 // field.hip -- NGP field head on gfx950 MFMA: the two tiny-cuda-nn FullyFusedMLPs of
-// models/networks.py:36-79 (xyz: 32->64->16, rgb: [SH4(16) | h(16)] -> 64 -> 64 -> 3, ReLU,
-// bias-free, fp16 operands / fp32 accumulation), TruncExp on h[0] and the SH4 direction
-// encoding, forward and backward.
+// models/networks.py:36-79 (xyz: 32->64->16; rgb: [SH4(16) | h(16)] -> W -> W -> 3 with
+// W = rgb_channels in {64, 128} (opt.py:87; the MF benchmark scripts use 128), ReLU, bias-free,
+// fp16 operands / fp32 accumulation), TruncExp on h[0] and the SH4 direction encoding, forward
+// and backward.
 //
 // Layout (one wave = one tile of 32 samples, v_mfma_f32_32x32x16_f16):
 //   activations are kept TRANSPOSED -- channel on the MFMA row, sample on the lane (col = lane&31)
@@ -9,11 +10,9 @@
 //   LDS round trip (cdna_hip_programming.md section 3, "An accumulator tile as the next MFMA's
 //   operand").  The weights are the A operands, pre-permuted once per optimizer step by
 //   mfnerf_field_pack_weights into 1-KiB lane-linear fragments (ds_read_b128, conflict-free).
-//   Backward-data products (dX = W^T dY) chain the same way; only the weight gradients
-//   (a reduction over samples = over lanes) go through a per-wave LDS transpose.  Weight
-//   gradients accumulate in registers across all tiles a wave processes (persistent grid),
-//   then one LDS block reduction and one slab row per workgroup, summed by a second kernel
-//   (deterministic, no float atomics).
+//   Backward: see the comment above field_bw_kernel.
+#include <cstdlib>
+
 #include "common.hpp"
 #include "../../include/mfnerf.h"
 
@@ -21,73 +20,103 @@ using namespace mfn;
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-constexpr int RGB_W = 64;        // rgb_channels supported by this build of the fused head
 constexpr int N_XYZ_PARAMS = 64 * 32 + 16 * 64;
-constexpr int N_RGB_PARAMS = RGB_W * 32 + RGB_W * RGB_W + 16 * RGB_W;
-constexpr int N_FRAGS = 44;
-constexpr int FRAG_HALFS = 64 * 8;  // one A fragment: 64 lanes x 8 f16
-constexpr int FIELD_BLOCK = 256;    // 4 waves
+constexpr int FRAG_HALFS = 64 * 8;  // one A fragment: 64 lanes x 8 f16 (1 KiB)
+constexpr int FIELD_BLOCK = 256;    // forward: 4 waves
 
-// fragment ids (see frag_spec)
-enum : int {
-    F1 = 0,   // W1  (64x32)  [mt*2+q]     natural, kbase 16q
-    F2 = 4,   // W2  (16x64)  [t*2+q]      perm,    kbase 32t+16q
-    F3 = 8,   // Wr1 (64x32)  [mt*2+q]     q=0 natural kbase 0 (SH); q=1 perm kbase 16 (h)
-    F4 = 12,  // Wr2 (64x64)  [mt*4+t*2+q] perm
-    F5 = 20,  // Wr3 (16x64)  [t*2+q]      perm
-    B5 = 24,  // Wr3^T (64x16) [mt]        perm kbase 0
-    B4 = 26,  // Wr2^T         [mt*4+t*2+q]
-    B3 = 34,  // Wr1^T (32x64) [t*2+q]
-    B2 = 38,  // W2^T  (64x16) [mt]        perm kbase 0
-    B1 = 40,  // W1^T  (32x64) [t*2+q]
+// Fragment table for rgb width W: MT = W/32 row tiles, KC = W/16 K chunks of a W-wide input.
+template <int W>
+struct Geo {
+    static constexpr int MT = W / 32, KC = W / 16;
+    static constexpr int F1 = 0;             // W1  (64x32)  [mt*2+q]  natural, kbase 16q
+    static constexpr int F2 = 4;             // W2  (16x64)  [t*2+q]   perm, kbase 32t+16q
+    static constexpr int F3 = 8;             // Wr1 (Wx32)   [mt*2+q]  q=0 natural kbase 0 (SH); q=1 perm kbase 16 (h)
+    static constexpr int F4 = F3 + 2 * MT;   // Wr2 (WxW)    [mt*KC+c] perm, kbase 16c
+    static constexpr int F5 = F4 + MT * KC;  // Wr3 (16xW)   [c]       perm
+    static constexpr int B5 = F5 + KC;       // Wr3^T (Wx16) [mt]      perm kbase 0
+    static constexpr int B4 = B5 + MT;       // Wr2^T        [mt*KC+c]
+    static constexpr int B3 = B4 + MT * KC;  // Wr1^T (32xW) [c]
+    static constexpr int B2 = B3 + KC;       // W2^T  (64x16) [mt]     perm kbase 0
+    static constexpr int B1 = B2 + 2;        // W1^T  (32x64) [t*2+q]
+    static constexpr int N = B1 + 4;         // 44 (W = 64), 106 (W = 128)
+    static constexpr int N_FW = B5;          // the forward's fragments
+    static constexpr int N_RGB = W * 32 + W * W + 16 * W;
+    static constexpr int N_DW = N_XYZ_PARAMS + N_RGB;  // weight-gradient floats (one slab row)
+};
+
+// Backward variants (NW = waves per workgroup; one workgroup per CU):
+//   W = 64,  NW = 4: all 12 weight-gradient tiles accumulate in registers (192 of the 512 a lone
+//                    wave per SIMD can hold);
+//   W = 64,  NW = 8: all of them accumulate in an LDS image (ds_add_f32 per sample tile), so a wave
+//                    fits in 256 registers and two waves share each SIMD;
+//   W = 128, NW = 4: the rgb-net tiles (dWr1, dWr2, dWr3: 24) in the LDS image -- in registers
+//                    they spill -- the xyz-net ones in registers; Wr2^T (B4, 32 KiB) is read from
+//                    global memory (L2-resident) to leave LDS room for the image (159.5 KiB in all).
+template <int W, int NW>
+struct BwCfg {
+    using G = Geo<W>;
+    static constexpr bool XYZ_LDS = (NW == 8);            // dW1, dW2
+    static constexpr bool RGB_LDS = XYZ_LDS || W == 128;  // dWr1, dWr2, dWr3
+    static constexpr bool B4_GLOBAL = (W == 128);
+    static constexpr int SKIP = B4_GLOBAL ? G::MT * G::KC : 0;
+    static constexpr int LDS_FRAGS = G::N - SKIP + 4;  // + 4 identity fragments
+    static constexpr int ID_BASE = LDS_FRAGS - 4;
+    static constexpr size_t IMG_OFF = (size_t)LDS_FRAGS * FRAG_HALFS * 2;
+    // image: the slab row (+16 level-L1 partials) when everything is in LDS; else the rgb part
+    // [dWr1 | dWr2 | dWr3 rows 0..2] (dWr3's other rows are zero: dL/dout has 3 channels)
+    static constexpr int RGB_IMG = W * 32 + W * W + 3 * W;
+    static constexpr int IMG_FLOATS = XYZ_LDS ? G::N_DW + 16 : (RGB_LDS ? RGB_IMG : 0);
+    static constexpr size_t LDS = IMG_OFF + (size_t)IMG_FLOATS * 4;
+    static_assert(LDS <= 160 * 1024, "the backward's LDS must fit one CU");
 };
 
 struct FragSpec { int mat, trans, mtile, kbase, perm; };
 
+template <int W>
 __device__ FragSpec frag_spec(int f) {
+    using G = Geo<W>;
     FragSpec s{0, 0, 0, 0, 1};
-    if (f < 4) { s.mat = 0; s.mtile = f >> 1; s.kbase = 16 * (f & 1); s.perm = 0; }
-    else if (f < 8) { int i = f - 4; s.mat = 1; s.kbase = 32 * (i >> 1) + 16 * (i & 1); }
-    else if (f < 12) { int i = f - 8; s.mat = 2; s.mtile = i >> 1; s.kbase = 16 * (i & 1); s.perm = i & 1; }
-    else if (f < 20) { int i = f - 12; s.mat = 3; s.mtile = i >> 2; s.kbase = 16 * (i & 3); }
-    else if (f < 24) { int i = f - 20; s.mat = 4; s.kbase = 16 * i; }
-    else if (f < 26) { s.mat = 4; s.trans = 1; s.mtile = f - 24; s.kbase = 0; }
-    else if (f < 34) { int i = f - 26; s.mat = 3; s.trans = 1; s.mtile = i >> 2; s.kbase = 16 * (i & 3); }
-    else if (f < 38) { int i = f - 34; s.mat = 2; s.trans = 1; s.kbase = 16 * i; }
-    else if (f < 40) { s.mat = 1; s.trans = 1; s.mtile = f - 38; s.kbase = 0; }
-    else { int i = f - 40; s.mat = 0; s.trans = 1; s.kbase = 16 * i; }
+    if (f < G::F2) { s.mat = 0; s.mtile = f >> 1; s.kbase = 16 * (f & 1); s.perm = 0; }
+    else if (f < G::F3) { int i = f - G::F2; s.mat = 1; s.kbase = 32 * (i >> 1) + 16 * (i & 1); }
+    else if (f < G::F4) { int i = f - G::F3; s.mat = 2; s.mtile = i >> 1; s.kbase = 16 * (i & 1); s.perm = i & 1; }
+    else if (f < G::F5) { int i = f - G::F4; s.mat = 3; s.mtile = i / G::KC; s.kbase = 16 * (i % G::KC); }
+    else if (f < G::B5) { int i = f - G::F5; s.mat = 4; s.kbase = 16 * i; }
+    else if (f < G::B4) { s.mat = 4; s.trans = 1; s.mtile = f - G::B5; s.kbase = 0; }
+    else if (f < G::B3) { int i = f - G::B4; s.mat = 3; s.trans = 1; s.mtile = i / G::KC; s.kbase = 16 * (i % G::KC); }
+    else if (f < G::B2) { int i = f - G::B3; s.mat = 2; s.trans = 1; s.kbase = 16 * i; }
+    else if (f < G::B1) { s.mat = 1; s.trans = 1; s.mtile = f - G::B2; s.kbase = 0; }
+    else { int i = f - G::B1; s.mat = 0; s.trans = 1; s.kbase = 16 * i; }
     return s;
 }
 
 // weight matrices, row-major (out, in) in the tcnn params vectors
-template <typename TP>
+template <int W, typename TP>
 __device__ __forceinline__ void mat_info(int mat, const TP* px, const TP* pr, const TP** p, int* rows, int* cols) {
     switch (mat) {
         case 0: *p = px; *rows = 64; *cols = 32; break;
         case 1: *p = px + 64 * 32; *rows = 16; *cols = 64; break;
-        case 2: *p = pr; *rows = RGB_W; *cols = 32; break;
-        case 3: *p = pr + RGB_W * 32; *rows = RGB_W; *cols = RGB_W; break;
-        default: *p = pr + RGB_W * 32 + RGB_W * RGB_W; *rows = 16; *cols = RGB_W; break;
+        case 2: *p = pr; *rows = W; *cols = 32; break;
+        case 3: *p = pr + W * 32; *rows = W; *cols = W; break;
+        default: *p = pr + W * 32 + W * W; *rows = 16; *cols = W; break;
     }
 }
 
 // k index carried by element j of lane half h (natural B order, or accumulator-as-operand order)
 __device__ __forceinline__ int k_of(int j, int h, int perm) { return perm ? 8 * (j >> 2) + 4 * h + (j & 3) : 8 * h + j; }
 
-template <typename TP>
+template <typename TP, int W>
 __global__ void pack_kernel(const TP* __restrict__ px, const TP* __restrict__ pr, _Float16* __restrict__ out) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= N_FRAGS * FRAG_HALFS) return;
+    if (t >= Geo<W>::N * FRAG_HALFS) return;
     const int f = t / FRAG_HALFS, lane = (t / 8) & 63, j = t & 7;
-    const FragSpec s = frag_spec(f);
+    const FragSpec s = frag_spec<W>(f);
     const int r = lane & 31, h = lane >> 5;
     const int m = 32 * s.mtile + r, k = s.kbase + k_of(j, h, s.perm);
     const TP* p; int rows, cols;
-    mat_info(s.mat, px, pr, &p, &rows, &cols);
+    mat_info<W>(s.mat, px, pr, &p, &rows, &cols);
     float v = 0.0f;
     if (!s.trans) { if (m < rows && k < cols) v = (float)p[m * cols + k]; }
     else { if (k < rows && m < cols) v = (float)p[k * cols + m]; }
@@ -148,15 +177,16 @@ __device__ __forceinline__ void sh4(float dx, float dy, float dz, float* o) {
 }
 
 // Forward state of one tile that the backward needs again.
+template <int W>
 struct FwdTile {
-    half8 x[2];      // B operands of layer 1 (natural order, features 16q+8h+j)
-    half8 y1[2][2];  // relu(Y1) as B operands [t][q]
-    half8 hb;        // h (16 features, perm order) = rgb-input k-step 1
-    half8 sh;        // SH (natural order 8h+j)    = rgb-input k-step 0
-    half8 r1[2][2];
-    half8 r2[2][2];
-    float h0;        // h[0] (f16-rounded) on lanes h==0
-    float rgb[3];    // sigmoid outputs on lanes h==0 (fp32)
+    half8 x[2];             // B operands of layer 1 (natural order, features 16q+8h+j)
+    half8 y1[2][2];         // relu(Y1) as B operands [t][q]
+    half8 hb;               // h (16 features, perm order) = rgb-input k-step 1
+    half8 sh;               // SH (natural order 8h+j)    = rgb-input k-step 0
+    half8 r1[W / 32][2];
+    half8 r2[W / 32][2];
+    float h0;               // h[0] (f16-rounded) on lanes h==0
+    float rgb[3];           // sigmoid outputs on lanes h==0 (fp32)
 };
 
 // Loads of one tile's inputs (feature row halves for this lane, direction), used directly or as
@@ -195,24 +225,27 @@ __device__ __forceinline__ void load_tile_in(const _Float16* __restrict__ feat, 
     }
 }
 
-template <bool DENSITY_ONLY>
-__device__ __forceinline__ void forward_tile(const _Float16* lds, int lane, const TileIn& I, bool valid, FwdTile& T) {
+template <int W, bool DENSITY_ONLY>
+__device__ __forceinline__ void forward_tile(const _Float16* lds, int lane, const TileIn& I, bool valid,
+                                             FwdTile<W>& T) {
+    using G = Geo<W>;
+    constexpr int MT = G::MT;
     const int h = lane >> 5;
     const f32x16 z = {};
     T.x[0] = I.x[0];
     T.x[1] = I.x[1];
     // xyz layer 1: Y1^T = W1 X^T
-    f32x16 y1a = mfma(lds_frag(lds, F1 + 0, lane), T.x[0], z);
-    y1a = mfma(lds_frag(lds, F1 + 1, lane), T.x[1], y1a);
-    f32x16 y1b = mfma(lds_frag(lds, F1 + 2, lane), T.x[0], z);
-    y1b = mfma(lds_frag(lds, F1 + 3, lane), T.x[1], y1b);
+    f32x16 y1a = mfma(lds_frag(lds, G::F1 + 0, lane), T.x[0], z);
+    y1a = mfma(lds_frag(lds, G::F1 + 1, lane), T.x[1], y1a);
+    f32x16 y1b = mfma(lds_frag(lds, G::F1 + 2, lane), T.x[0], z);
+    y1b = mfma(lds_frag(lds, G::F1 + 3, lane), T.x[1], y1b);
     T.y1[0][0] = pack8<0, true>(y1a); T.y1[0][1] = pack8<8, true>(y1a);
     T.y1[1][0] = pack8<0, true>(y1b); T.y1[1][1] = pack8<8, true>(y1b);
     // xyz layer 2: H^T = W2 relu(Y1)^T (rows 0..15 valid)
-    f32x16 ha = mfma(lds_frag(lds, F2 + 0, lane), T.y1[0][0], z);
-    ha = mfma(lds_frag(lds, F2 + 1, lane), T.y1[0][1], ha);
-    ha = mfma(lds_frag(lds, F2 + 2, lane), T.y1[1][0], ha);
-    ha = mfma(lds_frag(lds, F2 + 3, lane), T.y1[1][1], ha);
+    f32x16 ha = mfma(lds_frag(lds, G::F2 + 0, lane), T.y1[0][0], z);
+    ha = mfma(lds_frag(lds, G::F2 + 1, lane), T.y1[0][1], ha);
+    ha = mfma(lds_frag(lds, G::F2 + 2, lane), T.y1[1][0], ha);
+    ha = mfma(lds_frag(lds, G::F2 + 3, lane), T.y1[1][1], ha);
     T.hb = pack8<0, false>(ha);   // the fp16 network output of tcnn
     T.h0 = (float)T.hb[0];        // row 0 on lanes h==0
     if (DENSITY_ONLY) return;
@@ -225,29 +258,28 @@ __device__ __forceinline__ void forward_tile(const _Float16* lds, int lane, cons
 #pragma unroll
     for (int j = 0; j < 8; ++j) T.sh[j] = (_Float16)(h ? shv[8 + j] : shv[j]);
     // rgb layer 1
-    f32x16 r1a = mfma(lds_frag(lds, F3 + 0, lane), T.sh, z);
-    r1a = mfma(lds_frag(lds, F3 + 1, lane), T.hb, r1a);
-    f32x16 r1b = mfma(lds_frag(lds, F3 + 2, lane), T.sh, z);
-    r1b = mfma(lds_frag(lds, F3 + 3, lane), T.hb, r1b);
-    T.r1[0][0] = pack8<0, true>(r1a); T.r1[0][1] = pack8<8, true>(r1a);
-    T.r1[1][0] = pack8<0, true>(r1b); T.r1[1][1] = pack8<8, true>(r1b);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        f32x16 a = mfma(lds_frag(lds, G::F3 + 2 * mt, lane), T.sh, z);
+        a = mfma(lds_frag(lds, G::F3 + 2 * mt + 1, lane), T.hb, a);
+        T.r1[mt][0] = pack8<0, true>(a); T.r1[mt][1] = pack8<8, true>(a);
+    }
     // rgb layer 2
-    f32x16 r2a = z, r2b = z;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int mt = 0; mt < MT; ++mt) {
+        f32x16 a = z;
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            r2a = mfma(lds_frag(lds, F4 + 0 * 4 + t * 2 + q, lane), T.r1[t][q], r2a);
-            r2b = mfma(lds_frag(lds, F4 + 1 * 4 + t * 2 + q, lane), T.r1[t][q], r2b);
-        }
-    T.r2[0][0] = pack8<0, true>(r2a); T.r2[0][1] = pack8<8, true>(r2a);
-    T.r2[1][0] = pack8<0, true>(r2b); T.r2[1][1] = pack8<8, true>(r2b);
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) a = mfma(lds_frag(lds, G::F4 + mt * G::KC + t * 2 + q, lane), T.r1[t][q], a);
+        T.r2[mt][0] = pack8<0, true>(a); T.r2[mt][1] = pack8<8, true>(a);
+    }
     // rgb layer 3 (rows 0..2 = rgb logits on lanes h==0)
     f32x16 o = z;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < MT; ++t)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) o = mfma(lds_frag(lds, F5 + t * 2 + q, lane), T.r2[t][q], o);
+        for (int q = 0; q < 2; ++q) o = mfma(lds_frag(lds, G::F5 + t * 2 + q, lane), T.r2[t][q], o);
 #pragma unroll
     for (int c = 0; c < 3; ++c) T.rgb[c] = 1.0f / (1.0f + __expf(-o[c]));
 }
@@ -259,7 +291,7 @@ __device__ __forceinline__ void load_frags(_Float16* lds, const _Float16* __rest
     __syncthreads();
 }
 
-template <bool DENSITY_ONLY>
+template <int W, bool DENSITY_ONLY>
 __global__ __launch_bounds__(FIELD_BLOCK) void field_fw_kernel(const _Float16* __restrict__ feat,
                                                                 int64_t plane_stride,
                                                                 const float* __restrict__ dirs, int64_t n,
@@ -268,7 +300,7 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_fw_kernel(const _Float16* _
                                                                 float* __restrict__ sigma, float* __restrict__ rgb) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     _Float16* lds = reinterpret_cast<_Float16*>(smem);
-    load_frags(lds, packed, DENSITY_ONLY ? 8 : 24);
+    load_frags(lds, packed, DENSITY_ONLY ? 8 : Geo<W>::N_FW);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
@@ -278,8 +310,8 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_fw_kernel(const _Float16* _
         const bool valid = s < nn;
         TileIn I;
         load_tile_in(feat, plane_stride, dirs, s, valid, h, !DENSITY_ONLY, I);
-        FwdTile T;
-        forward_tile<DENSITY_ONLY>(lds, lane, I, valid, T);
+        FwdTile<W> T;
+        forward_tile<W, DENSITY_ONLY>(lds, lane, I, valid, T);
         if (valid && h == 0) {
             sigma[s] = __expf(T.h0);  // TruncExp forward (custom_functions.py:166)
             if (!DENSITY_ONLY) {
@@ -302,16 +334,21 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_fw_kernel(const _Float16* _
 // accumulator packed to f16 IS an operand with K = samples.  Exact (products with 1.0, one
 // non-zero term per output), no LDS round trip, no wave-level synchronisation.
 //   dW[out][in] (32x32 tile) += S(dY)[out-tile] x S(X)[in-tile], K = the tile's 32 samples (2 MFMAs)
+// The dW tiles accumulate across all sample tiles a wave processes (persistent grid) in registers
+// or in the workgroup's LDS image (BwCfg), then one slab row per workgroup, summed in a fixed order
+// by slab_reduce_kernel.
 
-// identity B fragments, appended after the weight fragments in LDS: ID_BASE + 2*perm + (off/16)
-constexpr int ID_BASE = N_FRAGS;
-constexpr int ID_N0 = ID_BASE, ID_N16 = ID_BASE + 1, ID_P0 = ID_BASE + 2, ID_P16 = ID_BASE + 3;
-constexpr int N_FRAGS_BW = N_FRAGS + 4;
-
+template <int W, int NW>
 __device__ __forceinline__ void load_frags_bw(_Float16* lds, const _Float16* __restrict__ packed) {
+    using G = Geo<W>;
+    using C = BwCfg<W, NW>;
     const uint4* src = reinterpret_cast<const uint4*>(packed);
     uint4* dst = reinterpret_cast<uint4*>(lds);
-    for (int i = threadIdx.x; i < N_FRAGS * 64; i += blockDim.x) dst[i] = src[i];
+    for (int i = threadIdx.x; i < (G::N - C::SKIP) * 64; i += blockDim.x) {
+        const int f = i >> 6;
+        const int gf = f < G::B4 ? f : f + C::SKIP;  // B4 stays in global memory when SKIP > 0
+        dst[i] = src[gf * 64 + (i & 63)];
+    }
     // identity: lane (n = lane&31, h), element j = 1 iff off + k_of(j, h, perm) == n
     for (int i = threadIdx.x; i < 4 * 64; i += blockDim.x) {
         const int fi = i >> 6, ln = i & 63, nn = ln & 31, hh = ln >> 5;
@@ -319,9 +356,21 @@ __device__ __forceinline__ void load_frags_bw(_Float16* lds, const _Float16* __r
         half8 v;
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (_Float16)((off + k_of(j, hh, perm) == nn) ? 1.0f : 0.0f);
-        *reinterpret_cast<half8*>(lds + ((ID_BASE + fi) * 64 + ln) * 8) = v;
+        *reinterpret_cast<half8*>(lds + ((C::ID_BASE + fi) * 64 + ln) * 8) = v;
     }
     __syncthreads();
+}
+
+// a backward fragment (index in the packed blob): from LDS, except B4 when it stays in global memory
+template <int W, int NW>
+__device__ __forceinline__ half8 bw_frag(const _Float16* lds, const _Float16* __restrict__ packed, int f, int lane) {
+    using G = Geo<W>;
+    using C = BwCfg<W, NW>;
+    if constexpr (C::SKIP > 0) {
+        if (f >= G::B4 && f < G::B3) return *reinterpret_cast<const half8*>(packed + (f * 64 + lane) * 8);
+        if (f >= G::B3) return lds_frag(lds, f - C::SKIP, lane);
+    }
+    return lds_frag(lds, f, lane);
 }
 
 // S operands (K = samples 0..15 / 16..31 of the tile) of one 32-channel tile given as two T chunks
@@ -351,10 +400,9 @@ __device__ __forceinline__ void dw_acc(f32x16& acc, const SOp& dy, const SOp& x)
     acc = mfma(dy.k[1], x.k[1], acc);
 }
 
-constexpr int N_DW = N_XYZ_PARAMS + N_RGB_PARAMS;  // 10240 floats per slab row
-
 // add one 32x32 dW tile (row = out 32*ot + (i&3)+8(i>>2)+4h, col = in 32*it + lane&31) into a
-// row-major fp32 LDS image of a (rows x cols) matrix
+// row-major fp32 LDS image of a (rows x cols) matrix; rows/cols are compile-time at every call, so
+// the register rows that can never be in range are dropped statically
 __device__ __forceinline__ void dw_add32(float* img, const f32x16& a, int ot, int it, int rows, int cols, int lane) {
     const int col = 32 * it + (lane & 31), h = lane >> 5;
 #pragma unroll
@@ -364,28 +412,61 @@ __device__ __forceinline__ void dw_add32(float* img, const f32x16& a, int ot, in
     }
 }
 
-__global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
-    const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev,
-    const _Float16* __restrict__ packed, const float* __restrict__ dL_dsigma, const float* __restrict__ dL_drgb,
-    float grad_scale, float* __restrict__ dL_dfeat, float* __restrict__ slab, int32_t* __restrict__ nonfinite,
-    float* __restrict__ level_l1) {
+// one dW tile += dY x X: into its register accumulator, or (IN_LDS) into the workgroup's image
+template <bool IN_LDS>
+__device__ __forceinline__ void acc_tile(f32x16& reg, float* img, int rows, int cols, const SOp& dy, const SOp& x,
+                                         int ot, int it, int lane) {
+    if constexpr (IN_LDS) {
+        f32x16 a = {};
+        dw_acc(a, dy, x);
+        dw_add32(img, a, ot, it, rows, cols, lane);
+    } else {
+        dw_acc(reg, dy, x);
+    }
+}
+
+template <int W, int NW>
+__global__ __launch_bounds__(64 * NW) void field_bw_kernel(
+    const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n,
+    const int32_t* __restrict__ n_dev, const _Float16* __restrict__ packed, const float* __restrict__ dL_dsigma,
+    const float* __restrict__ dL_drgb, float grad_scale, float* __restrict__ dL_dfeat, float* __restrict__ slab,
+    int32_t* __restrict__ nonfinite, float* __restrict__ level_l1) {
+    using G = Geo<W>;
+    using C = BwCfg<W, NW>;
+    constexpr int MT = G::MT;
+    constexpr bool XL = C::XYZ_LDS, RL = C::RGB_LDS;
+    constexpr int ID_N0 = C::ID_BASE, ID_N16 = C::ID_BASE + 1, ID_P0 = C::ID_BASE + 2, ID_P16 = C::ID_BASE + 3;
+    constexpr int oR1 = N_XYZ_PARAMS, oR2 = oR1 + W * 32, oR3 = oR2 + W * W;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     _Float16* lds_base = reinterpret_cast<_Float16*>(smem);
-    load_frags_bw(lds_base, packed);
+    // LDS-resident accumulators (BwCfg): the slab row, or its rgb part
+    float* limg = reinterpret_cast<float*>(smem + C::IMG_OFF);
+    for (int i = threadIdx.x; i < C::IMG_FLOATS; i += blockDim.x) limg[i] = 0.0f;
+    load_frags_bw<W, NW>(lds_base, packed);
+    float* i_w1 = limg;
+    float* i_w2 = limg + 64 * 32;
+    float* i_r1 = limg + (XL ? oR1 : 0);
+    float* i_r2 = i_r1 + W * 32;
+    float* i_r3 = i_r2 + W * W;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
     const float S = grad_scale, invS = 1.0f / grad_scale;
     const f32x16 z = {};
-    // persistent weight-gradient accumulators, 32x32 tiles [out-tile][in-tile] (192 registers)
-    f32x16 dw1[2], dw2[2], dwr1[2], dwr2[2][2], dwr3[2];
+    // register accumulators, 32x32 tiles [out-tile][in-tile] (192 registers at W = 64, NW = 4)
+    constexpr int R2 = RL ? 1 : MT;
+    f32x16 dw1[XL ? 1 : 2], dw2[XL ? 1 : 2], dwr1[RL ? 1 : MT], dwr3[RL ? 1 : MT], dwr2[R2][R2];
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-        dw1[a] = z; dw2[a] = z; dwr1[a] = z; dwr3[a] = z; dwr2[a][0] = z; dwr2[a][1] = z;
-    }
+    for (int a = 0; a < (XL ? 1 : 2); ++a) { dw1[a] = z; dw2[a] = z; }
+#pragma unroll
+    for (int a = 0; a < (RL ? 1 : MT); ++a) { dwr1[a] = z; dwr3[a] = z; }
+#pragma unroll
+    for (int a = 0; a < R2; ++a)
+#pragma unroll
+        for (int b = 0; b < R2; ++b) dwr2[a][b] = z;
 
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     const int64_t tiles = div_up<int64_t>(nn, 32);
-    const int64_t stride = (int64_t)gridDim.x * 4;
+    const int64_t stride = (int64_t)gridDim.x * NW;
     // the next tile's inputs are loaded while this tile computes
     TileIn nI;
     float ngs = 0.f, ng0 = 0.f, ng1 = 0.f, ng2 = 0.f;
@@ -399,24 +480,25 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
             ng0 = dL_drgb[3 * s]; ng1 = dL_drgb[3 * s + 1]; ng2 = dL_drgb[3 * s + 2];
         }
     };
-    const int64_t tile0 = (int64_t)blockIdx.x * 4 + wid;
+    const int64_t tile0 = (int64_t)blockIdx.x * NW + wid;
     if (tile0 < tiles) fetch(tile0);
     // per-level L1 of dL/dfeat (the fixed-point table-gradient scales): this lane's 8 levels are
     // 4g + 2h (features 8g+4h, +1) and 4g + 2h + 1 (features 8g+4h+2, +3), g = 0..3
     float l1a[4] = {0.f, 0.f, 0.f, 0.f}, l1b[4] = {0.f, 0.f, 0.f, 0.f};
     for (int64_t tile = tile0; tile < tiles; tile += stride) {
         // the fragment reads are loop-invariant; an opaque base keeps the compiler from hoisting
-        // all 48 of them (192 registers) out of the loop
+        // all of them (4 registers each) out of the loop
         int opaque = 0;
         asm volatile("" : "+s"(opaque));
         const _Float16* lds = lds_base + opaque;
+        const _Float16* pk = packed + opaque;  // B4 from global memory (W = 128): not hoisted either
         const int64_t s = tile * 32 + r;
         const bool valid = s < nn;
         const TileIn I = nI;
         const float gs = ngs, g0 = ng0, g1 = ng1, g2 = ng2;
         if (tile + stride < tiles) fetch(tile + stride);
-        FwdTile T;
-        forward_tile<false>(lds, lane, I, valid, T);
+        FwdTile<W> T;
+        forward_tile<W, false>(lds, lane, I, valid, T);
         // -- rgb layer 3: dO (rows 0..2 on lanes h==0) = dL/drgb * sigmoid'
         f32x16 dO = z;
         if (h == 0) {
@@ -425,60 +507,62 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
             dO[2] = g2 * S * T.rgb[2] * (1.0f - T.rgb[2]);
         }
         const half8 dOb = pack8<0, false>(dO);
-        {   // dWr3 (16 x W) += dO^T R2
+        {   // dWr3 (16 x W, rows 0..2 non-zero) += dO^T R2
             const SOp d = to_s16(lds, lane, dOb, ID_P0);
 #pragma unroll
-            for (int t = 0; t < 2; ++t) dw_acc(dwr3[t], d, to_s(lds, lane, T.r2[t][0], ID_P0, T.r2[t][1], ID_P16));
+            for (int t = 0; t < MT; ++t)
+                acc_tile<RL>(dwr3[RL ? 0 : t], i_r3, 3, W, d, to_s(lds, lane, T.r2[t][0], ID_P0, T.r2[t][1], ID_P16),
+                             0, t, lane);
         }
         //    dR2 = Wr3^T dO, masked by R2 > 0
-        half8 dr2p[2][2];
-        {
-            f32x16 a0 = mfma(lds_frag(lds, B5 + 0, lane), dOb, z);
-            f32x16 a1 = mfma(lds_frag(lds, B5 + 1, lane), dOb, z);
-            relu_mask<0>(a0, T.r2[0][0]); relu_mask<8>(a0, T.r2[0][1]);
-            relu_mask<0>(a1, T.r2[1][0]); relu_mask<8>(a1, T.r2[1][1]);
-            dr2p[0][0] = pack8<0, false>(a0); dr2p[0][1] = pack8<8, false>(a0);
-            dr2p[1][0] = pack8<0, false>(a1); dr2p[1][1] = pack8<8, false>(a1);
+        half8 dr2p[MT][2];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            f32x16 a = mfma(bw_frag<W, NW>(lds, pk, G::B5 + mt, lane), dOb, z);
+            relu_mask<0>(a, T.r2[mt][0]); relu_mask<8>(a, T.r2[mt][1]);
+            dr2p[mt][0] = pack8<0, false>(a); dr2p[mt][1] = pack8<8, false>(a);
         }
         {   // -- rgb layer 2: dWr2 (WxW) += dR2^T R1
-            const SOp x0 = to_s(lds, lane, T.r1[0][0], ID_P0, T.r1[0][1], ID_P16);
-            const SOp x1 = to_s(lds, lane, T.r1[1][0], ID_P0, T.r1[1][1], ID_P16);
+            SOp x[MT];
 #pragma unroll
-            for (int o = 0; o < 2; ++o) {
+            for (int i = 0; i < MT; ++i) x[i] = to_s(lds, lane, T.r1[i][0], ID_P0, T.r1[i][1], ID_P16);
+#pragma unroll
+            for (int o = 0; o < MT; ++o) {
                 const SOp d = to_s(lds, lane, dr2p[o][0], ID_P0, dr2p[o][1], ID_P16);
-                dw_acc(dwr2[o][0], d, x0);
-                dw_acc(dwr2[o][1], d, x1);
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+                    acc_tile<RL>(dwr2[RL ? 0 : o][RL ? 0 : i], i_r2, W, W, d, x[i], o, i, lane);
             }
         }
         //    dR1 = Wr2^T dR2, masked by R1 > 0
-        half8 dr1p[2][2];
-        {
-            f32x16 a0 = z, a1 = z;
+        half8 dr1p[MT][2];
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
+        for (int mt = 0; mt < MT; ++mt) {
+            f32x16 a = z;
 #pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    a0 = mfma(lds_frag(lds, B4 + 0 * 4 + t * 2 + q, lane), dr2p[t][q], a0);
-                    a1 = mfma(lds_frag(lds, B4 + 1 * 4 + t * 2 + q, lane), dr2p[t][q], a1);
-                }
-            relu_mask<0>(a0, T.r1[0][0]); relu_mask<8>(a0, T.r1[0][1]);
-            relu_mask<0>(a1, T.r1[1][0]); relu_mask<8>(a1, T.r1[1][1]);
-            dr1p[0][0] = pack8<0, false>(a0); dr1p[0][1] = pack8<8, false>(a0);
-            dr1p[1][0] = pack8<0, false>(a1); dr1p[1][1] = pack8<8, false>(a1);
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    a = mfma(bw_frag<W, NW>(lds, pk, G::B4 + mt * G::KC + t * 2 + q, lane), dr2p[t][q], a);
+            relu_mask<0>(a, T.r1[mt][0]); relu_mask<8>(a, T.r1[mt][1]);
+            dr1p[mt][0] = pack8<0, false>(a); dr1p[mt][1] = pack8<8, false>(a);
         }
         {   // -- rgb layer 1: dWr1 (Wx32) += dR1^T [SH;h]   (SH natural order, h perm order)
             const SOp x = to_s(lds, lane, T.sh, ID_N0, T.hb, ID_P16);
 #pragma unroll
-            for (int o = 0; o < 2; ++o) dw_acc(dwr1[o], to_s(lds, lane, dr1p[o][0], ID_P0, dr1p[o][1], ID_P16), x);
+            for (int o = 0; o < MT; ++o)
+                acc_tile<RL>(dwr1[RL ? 0 : o], i_r1, W, 32, to_s(lds, lane, dr1p[o][0], ID_P0, dr1p[o][1], ID_P16), x,
+                             o, 0, lane);
         }
         //    d[SH;h] = Wr1^T dR1 (rows 16..31 = dh) + TruncExp backward into h[0]
         half8 dhb;
         {
             f32x16 dsh = z;
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
+            for (int t = 0; t < MT; ++t)
 #pragma unroll
-                for (int q = 0; q < 2; ++q) dsh = mfma(lds_frag(lds, B3 + t * 2 + q, lane), dr1p[t][q], dsh);
+                for (int q = 0; q < 2; ++q)
+                    dsh = mfma(bw_frag<W, NW>(lds, pk, G::B3 + t * 2 + q, lane), dr1p[t][q], dsh);
             // row 16 = reg 8 on lanes h==0: g * exp(clamp(h0,-15,15)) (custom_functions.py:170-173)
             if (h == 0) dsh[8] += gs * S * __expf(fminf(fmaxf(T.h0, -15.0f), 15.0f));
             dhb = pack8<8, false>(dsh);
@@ -486,13 +570,15 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
         {   // -- xyz layer 2: dW2 (16x64) += dh^T Y1
             const SOp d = to_s16(lds, lane, dhb, ID_P0);
 #pragma unroll
-            for (int t = 0; t < 2; ++t) dw_acc(dw2[t], d, to_s(lds, lane, T.y1[t][0], ID_P0, T.y1[t][1], ID_P16));
+            for (int t = 0; t < 2; ++t)
+                acc_tile<XL>(dw2[XL ? 0 : t], i_w2, 16, 64, d, to_s(lds, lane, T.y1[t][0], ID_P0, T.y1[t][1], ID_P16),
+                             0, t, lane);
         }
         //    dY1 = W2^T dh, masked by Y1 > 0
         half8 dy1p[2][2];
         {
-            f32x16 a0 = mfma(lds_frag(lds, B2 + 0, lane), dhb, z);
-            f32x16 a1 = mfma(lds_frag(lds, B2 + 1, lane), dhb, z);
+            f32x16 a0 = mfma(bw_frag<W, NW>(lds, pk, G::B2 + 0, lane), dhb, z);
+            f32x16 a1 = mfma(bw_frag<W, NW>(lds, pk, G::B2 + 1, lane), dhb, z);
             relu_mask<0>(a0, T.y1[0][0]); relu_mask<8>(a0, T.y1[0][1]);
             relu_mask<0>(a1, T.y1[1][0]); relu_mask<8>(a1, T.y1[1][1]);
             dy1p[0][0] = pack8<0, false>(a0); dy1p[0][1] = pack8<8, false>(a0);
@@ -501,7 +587,9 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
         {   // -- xyz layer 1: dW1 (64x32) += dY1^T X   (X natural order)
             const SOp x = to_s(lds, lane, T.x[0], ID_N0, T.x[1], ID_N16);
 #pragma unroll
-            for (int o = 0; o < 2; ++o) dw_acc(dw1[o], to_s(lds, lane, dy1p[o][0], ID_P0, dy1p[o][1], ID_P16), x);
+            for (int o = 0; o < 2; ++o)
+                acc_tile<XL>(dw1[XL ? 0 : o], i_w1, 64, 32, to_s(lds, lane, dy1p[o][0], ID_P0, dy1p[o][1], ID_P16), x,
+                             o, 0, lane);
         }
         //    dX = W1^T dY1 -> global fp32 (features (i&3)+8(i>>2)+4h)
         {
@@ -509,7 +597,8 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int q = 0; q < 2; ++q) dx = mfma(lds_frag(lds, B1 + t * 2 + q, lane), dy1p[t][q], dx);
+                for (int q = 0; q < 2; ++q)
+                    dx = mfma(bw_frag<W, NW>(lds, pk, G::B1 + t * 2 + q, lane), dy1p[t][q], dx);
             bool bad = false;
             if (valid) {
                 float4* dst = reinterpret_cast<float4*>(dL_dfeat + s * 32);
@@ -528,45 +617,77 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_kernel(
         }
     }
 
-    // ---- block reduction of the per-wave dW partials into an fp32 LDS image, then one slab row
-    __syncthreads();
-    float* img = reinterpret_cast<float*>(smem);  // reuses the fragment area (N_DW*4 <= fragments)
-    for (int i = threadIdx.x; i < N_DW; i += blockDim.x) img[i] = 0.0f;
-    float* l1_part = img + N_DW;                  // 16 floats after the image
-    if (threadIdx.x < 16) l1_part[threadIdx.x] = 0.0f;
-    __syncthreads();
-    if (level_l1) {
+    // ---- epilogue: the workgroup's dW (and the level L1 partials) -> one slab row
+    float* row = slab + (int64_t)blockIdx.x * G::N_DW;
+    if constexpr (XL) {
+        float* l1_part = limg + G::N_DW;  // zeroed with the image
+        __syncthreads();
+        if (level_l1) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            float a = l1a[g], b = l1b[g];
+            for (int g = 0; g < 4; ++g) {
+                float a = l1a[g], b = l1b[g];
 #pragma unroll
-            for (int off = 16; off > 0; off >>= 1) { a += __shfl_xor(a, off, 64); b += __shfl_xor(b, off, 64); }
-            if (r == 0) { atomicAdd(l1_part + 4 * g + 2 * h, a); atomicAdd(l1_part + 4 * g + 2 * h + 1, b); }
+                for (int off = 16; off > 0; off >>= 1) { a += __shfl_xor(a, off, 64); b += __shfl_xor(b, off, 64); }
+                if (r == 0) { atomicAdd(l1_part + 4 * g + 2 * h, a); atomicAdd(l1_part + 4 * g + 2 * h + 1, b); }
+            }
         }
-    }
-    float* ix = img;
-    float* ir = img + N_XYZ_PARAMS;
-    float* ir2 = ir + RGB_W * 32;
-    float* ir3 = ir2 + RGB_W * RGB_W;
+        __syncthreads();
+        for (int i = threadIdx.x; i < G::N_DW; i += blockDim.x) row[i] = limg[i] * invS;
+        if (level_l1 && threadIdx.x < 16) atomicAdd(level_l1 + threadIdx.x, l1_part[threadIdx.x]);
+    } else {
+        // register partials -> an fp32 image over the fragment area (the xyz part only when the
+        // rgb part already is in limg)
+        constexpr int N_IMG = RL ? N_XYZ_PARAMS : G::N_DW;
+        static_assert((size_t)N_IMG * 4 + 64 <= C::IMG_OFF, "reduction image must fit the fragment area");
+        __syncthreads();
+        float* img = reinterpret_cast<float*>(smem);
+        for (int i = threadIdx.x; i < N_IMG; i += blockDim.x) img[i] = 0.0f;
+        float* l1_part = img + N_IMG;  // 16 floats after the image
+        if (threadIdx.x < 16) l1_part[threadIdx.x] = 0.0f;
+        __syncthreads();
+        if (level_l1) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-        dw_add32(ix, dw1[a], a, 0, 64, 32, lane);
-        dw_add32(ix + 64 * 32, dw2[a], 0, a, 16, 64, lane);
-        dw_add32(ir, dwr1[a], a, 0, RGB_W, 32, lane);
-        dw_add32(ir2, dwr2[a][0], a, 0, RGB_W, RGB_W, lane);
-        dw_add32(ir2, dwr2[a][1], a, 1, RGB_W, RGB_W, lane);
-        dw_add32(ir3, dwr3[a], 0, a, 16, RGB_W, lane);
+            for (int g = 0; g < 4; ++g) {
+                float a = l1a[g], b = l1b[g];
+#pragma unroll
+                for (int off = 16; off > 0; off >>= 1) { a += __shfl_xor(a, off, 64); b += __shfl_xor(b, off, 64); }
+                if (r == 0) { atomicAdd(l1_part + 4 * g + 2 * h, a); atomicAdd(l1_part + 4 * g + 2 * h + 1, b); }
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            dw_add32(img, dw1[a], a, 0, 64, 32, lane);
+            dw_add32(img + 64 * 32, dw2[a], 0, a, 16, 64, lane);
+        }
+        if constexpr (!RL) {
+#pragma unroll
+            for (int a = 0; a < MT; ++a) {
+                dw_add32(img + oR1, dwr1[a], a, 0, W, 32, lane);
+                dw_add32(img + oR3, dwr3[a], 0, a, 16, W, lane);
+            }
+#pragma unroll
+            for (int o = 0; o < R2; ++o)
+#pragma unroll
+                for (int i = 0; i < R2; ++i) dw_add32(img + oR2, dwr2[o][i], o, i, W, W, lane);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < G::N_DW; i += blockDim.x) {
+            float v;
+            if (!RL || i < oR1) v = img[i];
+            else if (i < oR3 + 3 * W) v = limg[i - oR1];
+            else v = 0.0f;  // dWr3 rows 3..15
+            row[i] = v * invS;
+        }
+        if (level_l1 && threadIdx.x < 16) atomicAdd(level_l1 + threadIdx.x, l1_part[threadIdx.x]);
     }
-    __syncthreads();
-    float* row = slab + (int64_t)blockIdx.x * N_DW;
-    for (int i = threadIdx.x; i < N_DW; i += blockDim.x) row[i] = img[i] * invS;
-    if (level_l1 && threadIdx.x < 16) atomicAdd(level_l1 + threadIdx.x, l1_part[threadIdx.x]);
 }
 
 // grad[p] += sum over slab rows (fixed order: deterministic).  64 columns x 4 row groups per block.
+template <int W>
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int rows,
                                                           float* __restrict__ gx, float* __restrict__ gr,
                                                           int32_t* __restrict__ nonfinite) {
+    constexpr int N_DW = Geo<W>::N_DW;
     __shared__ float part[4][64];
     const int l = threadIdx.x & 63, rg = threadIdx.x >> 6;
     const int p = blockIdx.x * 64 + l;
@@ -583,9 +704,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
     }
 }
 
-constexpr int BW_BLOCKS = 256;
-constexpr size_t BW_LDS = (size_t)N_FRAGS_BW * FRAG_HALFS * 2;
-static_assert((size_t)N_DW * 4 + 64 <= BW_LDS, "reduction image must fit the bw LDS");
+constexpr int BW_BLOCKS = 256;  // one workgroup per CU (persistent)
 
 // debug: one MFMA with A (32x16) and B (16x32) f16 row-major -> D (32x32) f32, to pin the lane maps
 __global__ void mfma_probe_kernel(const _Float16* A, const _Float16* B, float* D) {
@@ -599,62 +718,115 @@ __global__ void mfma_probe_kernel(const _Float16* A, const _Float16* B, float* D
     for (int i = 0; i < 16; ++i) D[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = c[i];
 }
 
+bool width_ok(int w) { return w == 64 || w == 128; }
+
+int bad_width(int w) {
+    mfn_set_error("field: rgb_width=%d unsupported (this build: 64 or 128)", w);
+    return MFN_ERR_INVALID;
+}
+
+// W = 64 backward variant: 4 waves per workgroup (register accumulators) or 8 (LDS accumulators);
+// MFNERF_FIELD_BW_WAVES=4|8 selects it (read once), for A/B measurements
+int bw_waves_w64() {
+    static const int w = [] {
+        const char* e = getenv("MFNERF_FIELD_BW_WAVES");
+        return (e && atoi(e) == 8) ? 8 : 4;
+    }();
+    return w;
+}
+
+template <typename TP, int W>
+void launch_pack(const TP* px, const TP* pr, void* packed, mfnerf_stream_t stream) {
+    const int total = Geo<W>::N * FRAG_HALFS;
+    hipLaunchKernelGGL((pack_kernel<TP, W>), dim3((total + 255) / 256), dim3(256), 0, stream, px, pr,
+                       (_Float16*)packed);
+}
+
+template <int W>
+void launch_fw(const void* feat, int64_t ps, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
+               int density_only, float* sigma, float* rgb, mfnerf_stream_t stream) {
+    const int64_t tiles = div_up<int64_t>(n, 32);
+    const int64_t want = div_up<int64_t>(tiles, 4);
+    const unsigned blocks = (unsigned)(want < 2048 ? want : 2048);
+    if (density_only)
+        hipLaunchKernelGGL((field_fw_kernel<W, true>), dim3(blocks), dim3(FIELD_BLOCK), 8 * FRAG_HALFS * 2, stream,
+                           (const _Float16*)feat, ps, dirs, n, n_dev, (const _Float16*)packed, sigma, rgb);
+    else
+        hipLaunchKernelGGL((field_fw_kernel<W, false>), dim3(blocks), dim3(FIELD_BLOCK),
+                           (size_t)Geo<W>::N_FW * FRAG_HALFS * 2, stream, (const _Float16*)feat, ps, dirs, n, n_dev,
+                           (const _Float16*)packed, sigma, rgb);
+}
+
+template <int W, int NW>
+int launch_bw(const void* feat, int64_t ps, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
+              const float* dL_dsigma, const float* dL_drgb, float grad_scale, float* dL_dfeat, float* grad_xyz,
+              float* grad_rgb, void* workspace, int32_t* nonfinite, float* level_l1, mfnerf_stream_t stream) {
+    using C = BwCfg<W, NW>;
+    if constexpr (C::LDS > 65536) {  // more than the default dynamic-LDS limit
+        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_kernel<W, NW>),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
+        if (attr != hipSuccess) {
+            mfn_set_error("field_bw: cannot raise the LDS limit to %d bytes", (int)C::LDS);
+            return MFN_ERR_INVALID;
+        }
+    }
+    hipLaunchKernelGGL((field_bw_kernel<W, NW>), dim3(BW_BLOCKS), dim3(64 * NW), C::LDS, stream,
+                       (const _Float16*)feat, ps, dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb,
+                       grad_scale, dL_dfeat, (float*)workspace, nonfinite, level_l1);
+    hipLaunchKernelGGL(slab_reduce_kernel<W>, dim3((Geo<W>::N_DW + 63) / 64), dim3(256), 0, stream,
+                       (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
+    return MFN_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 int64_t mfnerf_field_packed_bytes(int rgb_width) {
-    if (rgb_width != RGB_W) return -1;
-    return (int64_t)N_FRAGS * FRAG_HALFS * 2;
+    if (rgb_width == 64) return (int64_t)Geo<64>::N * FRAG_HALFS * 2;
+    if (rgb_width == 128) return (int64_t)Geo<128>::N * FRAG_HALFS * 2;
+    return -1;
 }
 
 int mfnerf_field_pack_weights(const float* params_xyz, const float* params_rgb, int rgb_width, void* packed,
                               mfnerf_stream_t stream) {
-    if (rgb_width != RGB_W) { mfn_set_error("field: rgb_width=%d unsupported (this build: %d)", rgb_width, RGB_W); return MFN_ERR_INVALID; }
+    if (!width_ok(rgb_width)) return bad_width(rgb_width);
     if (!params_xyz || !params_rgb || !packed) { mfn_set_error("field_pack_weights: null pointer"); return MFN_ERR_INVALID; }
-    const int total = N_FRAGS * FRAG_HALFS;
-    hipLaunchKernelGGL(pack_kernel<float>, dim3((total + 255) / 256), dim3(256), 0, stream, params_xyz, params_rgb,
-                       (_Float16*)packed);
+    if (rgb_width == 64) launch_pack<float, 64>(params_xyz, params_rgb, packed, stream);
+    else launch_pack<float, 128>(params_xyz, params_rgb, packed, stream);
     return mfn_check_launch("field_pack_weights");
 }
 
 int mfnerf_field_pack_weights_f16(const void* params_xyz_f16, const void* params_rgb_f16, int rgb_width, void* packed,
                                   mfnerf_stream_t stream) {
-    if (rgb_width != RGB_W) { mfn_set_error("field: rgb_width=%d unsupported (this build: %d)", rgb_width, RGB_W); return MFN_ERR_INVALID; }
+    if (!width_ok(rgb_width)) return bad_width(rgb_width);
     if (!params_xyz_f16 || !params_rgb_f16 || !packed) { mfn_set_error("field_pack_weights_f16: null pointer"); return MFN_ERR_INVALID; }
-    const int total = N_FRAGS * FRAG_HALFS;
-    hipLaunchKernelGGL(pack_kernel<_Float16>, dim3((total + 255) / 256), dim3(256), 0, stream,
-                       (const _Float16*)params_xyz_f16, (const _Float16*)params_rgb_f16, (_Float16*)packed);
+    const _Float16* px = (const _Float16*)params_xyz_f16;
+    const _Float16* pr = (const _Float16*)params_rgb_f16;
+    if (rgb_width == 64) launch_pack<_Float16, 64>(px, pr, packed, stream);
+    else launch_pack<_Float16, 128>(px, pr, packed, stream);
     return mfn_check_launch("field_pack_weights_f16");
 }
 
 int mfnerf_field_fw(const void* feat_f16, int64_t feat_plane_stride, const float* dirs, int64_t n,
                     const int32_t* n_dev, const void* packed,
                     int rgb_width, int density_only, float* sigma, float* rgb, mfnerf_stream_t stream) {
-    if (rgb_width != RGB_W) { mfn_set_error("field: rgb_width=%d unsupported (this build: %d)", rgb_width, RGB_W); return MFN_ERR_INVALID; }
+    if (!width_ok(rgb_width)) return bad_width(rgb_width);
     if (n < 0 || (feat_plane_stride != 0 && feat_plane_stride < n)) { mfn_set_error("field_fw: bad size"); return MFN_ERR_INVALID; }
     if (n == 0) return MFN_OK;
     if (!feat_f16 || !packed || !sigma || (!density_only && (!dirs || !rgb))) {
         mfn_set_error("field_fw: null pointer"); return MFN_ERR_INVALID;
     }
-    const int64_t tiles = div_up<int64_t>(n, 32);
-    const int64_t want = div_up<int64_t>(tiles, 4);
-    const unsigned blocks = (unsigned)(want < 2048 ? want : 2048);
-    if (density_only)
-        hipLaunchKernelGGL(field_fw_kernel<true>, dim3(blocks), dim3(FIELD_BLOCK), 8 * FRAG_HALFS * 2, stream,
-                           (const _Float16*)feat_f16, feat_plane_stride, dirs, n, n_dev, (const _Float16*)packed,
-                           sigma, rgb);
-    else
-        hipLaunchKernelGGL(field_fw_kernel<false>, dim3(blocks), dim3(FIELD_BLOCK), 24 * FRAG_HALFS * 2, stream,
-                           (const _Float16*)feat_f16, feat_plane_stride, dirs, n, n_dev, (const _Float16*)packed,
-                           sigma, rgb);
+    if (rgb_width == 64) launch_fw<64>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, density_only, sigma, rgb, stream);
+    else launch_fw<128>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, density_only, sigma, rgb, stream);
     return mfn_check_launch("field_fw");
 }
 
 int64_t mfnerf_field_bw_workspace(int64_t n, int rgb_width) {
     (void)n;
-    if (rgb_width != RGB_W) return -1;
-    return (int64_t)BW_BLOCKS * N_DW * 4;
+    if (rgb_width == 64) return (int64_t)BW_BLOCKS * Geo<64>::N_DW * 4;
+    if (rgb_width == 128) return (int64_t)BW_BLOCKS * Geo<128>::N_DW * 4;
+    return -1;
 }
 
 int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float* dirs, int64_t n,
@@ -662,7 +834,7 @@ int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float
                     int rgb_width, const float* dL_dsigma, const float* dL_drgb, float grad_scale, float* dL_dfeat,
                     float* grad_xyz, float* grad_rgb, void* workspace, int32_t* nonfinite, float* level_l1,
                     mfnerf_stream_t stream) {
-    if (rgb_width != RGB_W) { mfn_set_error("field: rgb_width=%d unsupported (this build: %d)", rgb_width, RGB_W); return MFN_ERR_INVALID; }
+    if (!width_ok(rgb_width)) return bad_width(rgb_width);
     if (n < 0 || !(grad_scale > 0.0f) || (feat_plane_stride != 0 && feat_plane_stride < n)) {
         mfn_set_error("field_bw: bad size, plane stride or grad_scale"); return MFN_ERR_INVALID;
     }
@@ -670,11 +842,17 @@ int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float
     if (!feat_f16 || !dirs || !packed || !dL_dsigma || !dL_drgb || !dL_dfeat || !grad_xyz || !grad_rgb || !workspace) {
         mfn_set_error("field_bw: null pointer"); return MFN_ERR_INVALID;
     }
-    hipLaunchKernelGGL(field_bw_kernel, dim3(BW_BLOCKS), dim3(FIELD_BLOCK), BW_LDS, stream, (const _Float16*)feat_f16,
-                       feat_plane_stride, dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb, grad_scale, dL_dfeat,
-                       (float*)workspace, nonfinite, level_l1);
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3((N_DW + 63) / 64), dim3(256), 0, stream, (const float*)workspace,
-                       BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
+    int st;
+    if (rgb_width == 128)
+        st = launch_bw<128, 4>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, dL_dsigma, dL_drgb, grad_scale,
+                               dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
+    else if (bw_waves_w64() == 8)
+        st = launch_bw<64, 8>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, dL_dsigma, dL_drgb, grad_scale,
+                              dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
+    else
+        st = launch_bw<64, 4>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, dL_dsigma, dL_drgb, grad_scale,
+                              dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
+    if (st != MFN_OK) return st;
     return mfn_check_launch("field_bw");
 }
 

@@ -132,8 +132,10 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_fw_planar_kernel(const float* 
         const float x = (X[3 * i] - x_min) / x_range;
         const float y = (X[3 * i + 1] - x_min) / x_range;
         const float z = (X[3 * i + 2] - x_min) / x_range;
-        for (int l = 0; l < D.n_levels; ++l) {
-            if (level_group(l) != grp) continue;
+        // this group's levels, visited directly: 16m + grp and 16m + 15 - grp
+        for (int j = 0; j < 2 * ((D.n_levels + 15) >> 4); ++j) {
+            const int l = 16 * (j >> 1) + ((j & 1) ? 15 - grp : grp);
+            if (l >= D.n_levels) continue;
             const LevelGeo L = level_geo(D.scale[l], x, y, z);
             const __half2* tab = table + D.offset[l];
             const uint32_t size = D.size[l], res = D.res[l];
@@ -216,6 +218,17 @@ __device__ __forceinline__ float fixed_scale(float l1) {
     return ldexpf(1.0f, 30 - e);
 }
 
+// The scale of the table level l adds into.  A MixedFeature table shared by several levels takes
+// the sum of their L1 bounds, so every level adding into it uses the table's one scale and the
+// bound still holds for each entry.
+__device__ __forceinline__ float table_fixed_scale(const mfnerf_grid_desc& D, const float* __restrict__ level_l1,
+                                                   int l) {
+    float l1 = 0.0f;
+    for (int k = 0; k < D.n_levels; ++k)
+        if (D.offset[k] == D.offset[l]) l1 += level_l1[k];
+    return fixed_scale(l1);
+}
+
 template <int ABLATE, int MAXL, bool FIX>
 __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restrict__ X, int64_t n,
                                                              const int32_t* __restrict__ n_dev, float x_min,
@@ -233,6 +246,11 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restr
     const int lane = threadIdx.x & 63, s = lane & 15, f = (lane >> 4) & 1, xb = lane >> 5;
     const int row = 2 * L_, rs = 2 * L_ + 1, per_chunk = 16 * row;
     float* sdy = sdy_all[threadIdx.x >> 6];
+    __shared__ float fs_s[MAXL];  // fixed-point scale per level (its table's)
+    if (FIX) {
+        if ((int)threadIdx.x < L_) fs_s[threadIdx.x] = table_fixed_scale(D, level_l1, threadIdx.x);
+        __syncthreads();
+    }
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     const int64_t chunks = div_up<int64_t>(nn, 16);
     const int64_t wave0 = ((int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x) >> 6;
@@ -269,7 +287,7 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restr
             if (ABLATE == 2 && l > 5) continue;
             if (ABLATE == 3 && l < 10) continue;
             const float g = srow[2 * l];
-            const float fs = FIX ? fixed_scale(level_l1[l]) : 0.0f;
+            const float fs = FIX ? fs_s[l] : 0.0f;
             const LevelGeo Lg = level_geo(D.scale[l], x, y, z);
             const bool spread = priv && (int64_t)D.offset[l] + D.size[l] <= dense_entries;
             float* gt = spread ? priv + 2 * ((chunk & (GRAD_COPIES - 1)) * dense_entries + (int64_t)D.offset[l])
@@ -403,20 +421,34 @@ __global__ __launch_bounds__(256) void fold_convert_kernel(float* __restrict__ g
                                                            int64_t dense_vals, int64_t total_vals,
                                                            const mfnerf_grid_desc D,
                                                            const float* __restrict__ level_l1) {
-    __shared__ float inv_s[MFN_MAX_LEVELS];
+    // table regions in address order -- a level's own table, or a shared MixedFeature table counted
+    // once (the levels sharing it have its offset) -- each with its table's scale
+    __shared__ float lvl_inv[MFN_MAX_LEVELS], inv_s[MFN_MAX_LEVELS];
     __shared__ int64_t lo_v[MFN_MAX_LEVELS + 1];
+    __shared__ int n_reg;
     if (threadIdx.x < D.n_levels) {
-        const float sc = fixed_scale(level_l1[threadIdx.x]);
-        inv_s[threadIdx.x] = sc > 0.0f ? 1.0f / sc : 0.0f;
-        lo_v[threadIdx.x] = 2 * (int64_t)D.offset[threadIdx.x];
+        const float sc = table_fixed_scale(D, level_l1, threadIdx.x);
+        lvl_inv[threadIdx.x] = sc > 0.0f ? 1.0f / sc : 0.0f;
     }
-    if (threadIdx.x == 0) lo_v[D.n_levels] = total_vals;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int nr = 0;
+        int64_t last = -1;
+        for (int k = 0; k < D.n_levels; ++k) {
+            if ((int64_t)D.offset[k] <= last) continue;
+            last = D.offset[k];
+            inv_s[nr] = lvl_inv[k];
+            lo_v[nr++] = 2 * (int64_t)D.offset[k];
+        }
+        lo_v[nr] = total_vals;
+        n_reg = nr;
+    }
     __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    int l = 0;  // level of value i (i increases per thread: walk forward)
+    int l = 0;  // region of value i (i increases per thread: walk forward)
     for (int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; 4 * i4 < total_vals; i4 += stride) {
-        const int64_t i = 4 * i4;  // level boundaries are multiples of 16 values
-        while (l + 1 < D.n_levels && i >= lo_v[l + 1]) ++l;
+        const int64_t i = 4 * i4;  // region boundaries are multiples of 16 values
+        while (l + 1 < n_reg && i >= lo_v[l + 1]) ++l;
         const float is = inv_s[l];
         int4 acc;
         if (i < dense_vals) {

@@ -333,17 +333,25 @@ __global__ void march_test_kernel(MarchParams p, float* __restrict__ hits_t, con
 // evaluated in the reference's sequential order by a uniform loop over the lanes (bit-identical
 // T, hence identical termination and total_samples); the rgb/depth/opacity sums and the backward's
 // prefix sums are wave reductions/scans (fp32 reassociation only, ~1e-7 relative).
-__device__ __forceinline__ float wave_sum(float v) {
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+// Wave scans and sums on the DPP network: row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast:15 / row_bcast:31 carry the row totals -- a few cycles per step, where each __shfl step
+// is an LDS-routed ds_bpermute with ~100 cycles of latency (this path runs one wave per ray).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_src(float v) {
+    // lanes outside ROW_MASK, or without a source lane, read 0
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
 }
 __device__ __forceinline__ float wave_incl_scan(float v, int lane) {
-    for (int off = 1; off < 64; off <<= 1) {
-        const float u = __shfl_up(v, off, 64);
-        if (lane >= off) v += u;
-    }
+    (void)lane;
+    v += dpp_src<0x111, 0xF>(v);  // row_shr:1
+    v += dpp_src<0x112, 0xF>(v);  // row_shr:2
+    v += dpp_src<0x114, 0xF>(v);  // row_shr:4
+    v += dpp_src<0x118, 0xF>(v);  // row_shr:8
+    v += dpp_src<0x142, 0xA>(v);  // row_bcast:15 -> rows 1 and 3
+    v += dpp_src<0x143, 0xC>(v);  // row_bcast:31 -> rows 2 and 3
     return v;
 }
+__device__ __forceinline__ float wave_sum(float v) { return readlane_f(wave_incl_scan(v, 0), 63); }
 
 // Sequential T over the chunk: returns this lane's T before its sample; T_run is advanced; *stop is
 // the first lane whose post-update T <= thr (64 if none).
@@ -490,6 +498,7 @@ __global__ __launch_bounds__(256) void composite_fused_wave_kernel(
     if (n < n_rays) {
         const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
         const int N = (int)rays_a[3 * n + 2];
+        const float tg[3] = {target[3 * ray], target[3 * ray + 1], target[3 * ray + 2]};
         // ---- pass 1: forward (composite_fw_wave_kernel)
         float T = 1.0f, R = 0.f, G = 0.f, B = 0.f, D = 0.f, O = 0.f;
         int total = N;
@@ -500,14 +509,20 @@ __global__ __launch_bounds__(256) void composite_fused_wave_kernel(
             const bool valid = lane < nv;
             float w = 0.0f, tn = 0.0f;
             if (!ended) {
-                const float a = valid ? 1.0f - fast_exp(-sigmas[s] * deltas[s]) : 0.0f;
+                // the chunk's loads are all issued before the serial chain, which hides them
+                float sg = 0.f, dl = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f, tv = 0.f;
+                if (valid) {
+                    sg = sigmas[s]; dl = deltas[s]; tv = ts[s];
+                    c0 = rgbs[3 * s]; c1 = rgbs[3 * s + 1]; c2 = rgbs[3 * s + 2];
+                }
+                const float a = valid ? 1.0f - fast_exp(-sg * dl) : 0.0f;
                 int stop;
                 const float myT = t_chain(a, T, T_thr, lane, nv, &stop);
                 if (valid && lane <= stop) {
                     w = a * myT;
                     tn = myT * (1.0f - a);
-                    R = fmaf(w, rgbs[3 * s], R); G = fmaf(w, rgbs[3 * s + 1], G); B = fmaf(w, rgbs[3 * s + 2], B);
-                    D = fmaf(w, ts[s], D);
+                    R = fmaf(w, c0, R); G = fmaf(w, c1, G); B = fmaf(w, c2, B);
+                    D = fmaf(w, tv, D);
                     O += w;
                 }
                 if (stop < 64) { ended = true; total = k0 + stop; }
@@ -521,7 +536,7 @@ __global__ __launch_bounds__(256) void composite_fused_wave_kernel(
         float gcol[3], dop = 0.0f;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const float e = col[c] + bg[c] * (1.0f - O) - target[3 * ray + c];
+            const float e = col[c] + bg[c] * (1.0f - O) - tg[c];
             l += e * e * inv3n;
             gcol[c] = 2.0f * e * inv3n;
             dop -= bg[c] * gcol[c];

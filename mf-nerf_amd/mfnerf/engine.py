@@ -446,10 +446,12 @@ class TrainStep:
             else:
                 self._update()
 
-    def run(self, batch: Batch = None, mark=None, exchange=None):
+    def run(self, batch: Batch = None, mark=None, exchange=None, optimize=True):
         """One training step, eagerly on the current stream, parts in sequence, march buffer set 0.
         mark(name) is called after each stage (bench timing); exchange(grads) runs between backward
-        and Adam (the data-parallel all-reduce).  batch=None: drawn from the attached dataset."""
+        and Adam (the data-parallel all-reduce).  batch=None: drawn from the attached dataset.
+        optimize=False stops after the backward and leaves the step's gradient in self.grads (no
+        Adam step, no repack; for inspection)."""
         mark = mark or (lambda name: None)
         if batch is None:
             batch = self._sampled
@@ -466,7 +468,8 @@ class TrainStep:
             self._grid_finish(q)
             mark("grid_finish")
         self._reduce_parts()
-        self._optimize(exchange)
+        if optimize:
+            self._optimize(exchange)
         mark("update")
 
     def optimizer(self, lr=None, exchange=None):

@@ -11,8 +11,8 @@ from mfnerf import engine, synthetic
 pytestmark = pytest.mark.gpu
 
 
-def _make(gpu, parts=2):
-    st = engine.TrainStep(engine.StepConfig(n_rays=1024, log2_T=16, n_parts=parts), device=gpu, seed=0)
+def _make(gpu, parts=2, **kw):
+    st = engine.TrainStep(engine.StepConfig(n_rays=1024, log2_T=16, n_parts=parts, **kw), device=gpu, seed=0)
     st.set_occupancy(synthetic.ball_density_grid())
     return st
 
@@ -63,21 +63,27 @@ def test_pipelined_replay_matches_eager(gpu, oracle, parts):
     assert torch.equal(got[k]["xyzs"].cpu(), xyzs_o[:n_o])
 
 
-def test_parts_sum_to_the_whole_batch(gpu):
-    """n_parts only changes the schedule: the loss and the gradient of one eager step are the same
-    for 1, 2 and 4 parts (up to float summation order)."""
+@pytest.mark.parametrize("kw", [{}, {"grid": "MixedFeature", "N_tables": 8, "rgb_width": 128}],
+                         ids=["hash-rgb64", "mixedfeature-rgb128"])
+def test_parts_sum_to_the_whole_batch(gpu, kw):
+    """n_parts only changes the schedule: the loss and the gradient of one step (before Adam) are
+    the same for 1 part (int32 fixed-point table gradient) and 2 / 4 parts (float atomics), up to
+    summation order and the fixed-point resolution -- per parameter block (MLPs, table)."""
     out = []
     for parts in (1, 2, 4):
-        st = _make(gpu, parts)
+        st = _make(gpu, parts, **kw)
         batch = st.make_batches(1, seed=9)[0]
-        st.run(batch)
+        st.run(batch, optimize=False)
         torch.cuda.synchronize()
         out.append((float(st.loss_sum), st.grads.clone(), st.gather_march()[0]))
+    blocks = [(0, st.off_rgb), (st.off_rgb, st.off_table), (st.off_table, st.n_params)]
     for loss, g, ra in out[1:]:
         assert torch.equal(ra, out[0][2])
         assert abs(loss - out[0][0]) <= 1e-5 * abs(out[0][0])
-        tol = 1e-4 * float(out[0][1].abs().max())
-        assert torch.allclose(g, out[0][1], rtol=1e-3, atol=tol)
+        for a, b in blocks:
+            ref = out[0][1][a:b]
+            assert float(ref.abs().max()) > 0
+            assert torch.allclose(g[a:b], ref, rtol=1e-3, atol=1e-4 * float(ref.abs().max())), (a, b)
 
 
 def test_distortion_loss_in_the_fused_step(gpu, oracle):

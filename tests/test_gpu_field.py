@@ -164,34 +164,42 @@ def test_grid_encode_world_coords_normalisation(gpu):
     assert torch.allclose(out.float().cpu(), ref, atol=1e-3, rtol=0)
 
 
-def _field_inputs(N, seed=4, wscale=3.0):
+def _field_inputs(N, seed=4, wscale=3.0, width=64):
     g = torch.Generator().manual_seed(seed)
     feat = (torch.rand(N, 32, generator=g) - 0.5).half()
     dirs = torch.randn(N, 3, generator=g)
     px = FO.xavier_uniform_(torch.empty(3072), FO.mlp_shapes(32, 16, 64, 1), g) * wscale
-    pr = FO.xavier_uniform_(torch.empty(7168), FO.mlp_shapes(32, 3, 64, 2), g) * wscale
+    pr = FO.xavier_uniform_(torch.empty(FLD.rgb_net_params(width)), FO.mlp_shapes(32, 3, width, 2), g) * wscale
     return feat, dirs, px, pr
 
 
-@pytest.mark.parametrize("N", [1, 31, 33, 5000])
-def test_field_fw(gpu, N):
-    feat, dirs, px, pr = _field_inputs(N)
-    s_ref, c_ref, _ = FO.ngp_field_fw16(feat, dirs, px, pr)
-    packed = FLD.pack_field_weights(px.to(gpu), pr.to(gpu))
-    s, c = FLD.field_fw(feat.to(gpu), dirs.to(gpu), N, packed)
+@pytest.mark.parametrize("N,width", [(1, 64), (31, 64), (33, 64), (5000, 64), (1, 128), (33, 128), (5000, 128)])
+def test_field_fw(gpu, N, width):
+    # width 128 at 3x Xavier: activations in the hundreds, where an fp16 rounding flip of one hidden
+    # unit (accumulation order) moves a logit by ~0.1 -- keep the Xavier scale there
+    feat, dirs, px, pr = _field_inputs(N, width=width, wscale=3.0 if width == 64 else 1.0)
+    s_ref, c_ref, _ = FO.ngp_field_fw16(feat, dirs, px, pr, width)
+    packed = FLD.pack_field_weights(px.to(gpu), pr.to(gpu), width)
+    s, c = FLD.field_fw(feat.to(gpu), dirs.to(gpu), N, packed, width)
     # h0 is one fp16 value on both sides; sigma = exp(h0): fp16-accumulation-order noise only
     assert torch.allclose(s.cpu(), s_ref, rtol=4e-3, atol=1e-6)
     assert torch.allclose(c.cpu(), c_ref, atol=2e-3, rtol=0)
-    sd, _ = FLD.field_fw(feat.to(gpu), None, N, packed, density_only=True)
+    sd, _ = FLD.field_fw(feat.to(gpu), None, N, packed, width, density_only=True)
     assert torch.equal(sd.cpu(), s.cpu())
 
 
-def _fp32_autograd(feat, dirs, px, pr, dsig, drgb):
+def test_field_width_unsupported(gpu):
+    with pytest.raises(RuntimeError):
+        FLD.pack_field_weights(torch.zeros(3072, device=gpu), torch.zeros(FLD.rgb_net_params(96), device=gpu), 96)
+
+
+def _fp32_autograd(feat, dirs, px, pr, dsig, drgb, width=64):
     f32 = feat.float().requires_grad_(True)
     a = px.half().float().requires_grad_(True)
     b = pr.half().float().requires_grad_(True)
+    W = width
     W1 = a[:2048].view(64, 32); W2 = a[2048:3072].view(16, 64)
-    R1 = b[:2048].view(64, 32); R2 = b[2048:6144].view(64, 64); R3 = b[6144:].view(16, 64)
+    R1 = b[:W * 32].view(W, 32); R2 = b[W * 32:W * 32 + W * W].view(W, W); R3 = b[W * 32 + W * W:].view(16, W)
     y1 = torch.relu(f32 @ W1.t()); h = y1 @ W2.t()
     sigma = torch.exp(h[:, 0])
     dn = dirs / torch.norm(dirs, dim=1, keepdim=True)
@@ -201,23 +209,24 @@ def _fp32_autograd(feat, dirs, px, pr, dsig, drgb):
     return f32.grad, a.grad, b.grad
 
 
-@pytest.mark.parametrize("wscale,sig_on", [(1.0, 0.0), (1.0, 1.0), (3.0, 1.0)])
-def test_field_bw(gpu, wscale, sig_on):
+@pytest.mark.parametrize("wscale,sig_on,width", [(1.0, 0.0, 64), (1.0, 1.0, 64), (3.0, 1.0, 64), (1.0, 1.0, 128),
+                                                 (3.0, 1.0, 128)])
+def test_field_bw(gpu, wscale, sig_on, width):
     N = 3000
-    feat, dirs, px, pr = _field_inputs(N, seed=5, wscale=wscale)
+    feat, dirs, px, pr = _field_inputs(N, seed=5, wscale=wscale, width=width)
     g = torch.Generator().manual_seed(6)
     dsig = torch.randn(N, generator=g) * 1e-6 * sig_on
     drgb = torch.randn(N, 3, generator=g) * 1e-5
     S = 16384.0
-    sig, _, acts = FO.ngp_field_fw16(feat, dirs, px, pr)
+    sig, _, acts = FO.ngp_field_fw16(feat, dirs, px, pr, width)
     ref16 = FO.ngp_field_bw16(acts, dsig, drgb, S)
-    ref32 = _fp32_autograd(feat, dirs, px, pr, dsig, drgb)
-    packed = FLD.pack_field_weights(px.to(gpu), pr.to(gpu))
+    ref32 = _fp32_autograd(feat, dirs, px, pr, dsig, drgb, width)
+    packed = FLD.pack_field_weights(px.to(gpu), pr.to(gpu), width)
     dfeat = torch.empty(N, 32, device=gpu)
     gx = torch.zeros(3072, device=gpu)
-    gr = torch.zeros(7168, device=gpu)
-    ws = FLD.field_bw_workspace(N, 64, gpu)
-    FLD.field_bw(feat.to(gpu), dirs.to(gpu), N, packed, dsig.to(gpu), drgb.to(gpu), S, dfeat, gx, gr, ws)
+    gr = torch.zeros(FLD.rgb_net_params(width), device=gpu)
+    ws = FLD.field_bw_workspace(N, width, gpu)
+    FLD.field_bw(feat.to(gpu), dirs.to(gpu), N, packed, dsig.to(gpu), drgb.to(gpu), S, dfeat, gx, gr, ws, width)
     for got, r16, r32 in zip((dfeat.cpu(), gx.cpu(), gr.cpu()), ref16, ref32):
         # vs the fp16-point emulation: only fp32 summation-order differences remain
         err = float((got - r16).abs().max() / r16.abs().max())
@@ -274,3 +283,31 @@ def test_planar_encode_and_field_match_row_major(gpu, name, args):
     assert torch.equal(outs[0][0], outs[1][0])
     for a, b in zip(outs[0][1:], outs[1][1:]):
         assert torch.allclose(a, b, rtol=1e-5, atol=1e-6 * float(b.abs().max()))
+
+
+def test_grid_encode_bw_fixed_point_shared_tables(gpu):
+    """MixedFeature levels share tables: with per-level gradient magnitudes six decades apart, every
+    level adding into a shared table must use that table's scale (the sum of its levels' L1 bounds),
+    and the conversion back must use it too -- checked per table region against the oracle."""
+    args = _layouts()[2][1]
+    lay, olay = GridLayout(*args), FO.GridLayout(*args)
+    g = torch.Generator().manual_seed(13)
+    N = 4000
+    x = torch.rand(N, 3, generator=g)
+    dy = torch.randn(N, 32, generator=g) * torch.logspace(-9, -3, 16).repeat_interleave(2).view(1, 32)
+    tp = torch.zeros(lay.n_params).requires_grad_(True)
+    (FO.grid_encode(x, tp, olay).double() * dy.double()).sum().backward()
+    gref = tp.grad.double()
+    desc = lay.desc()
+    gt = torch.zeros(lay.n_params, device=gpu)
+    FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=FLD.grid_bw_workspace(desc, gpu),
+                       fixed_point=True)
+    got = gt.cpu().double()
+    regions = sorted(set((lay.offsets[l], lay.sizes[l]) for l in range(lay.L)))
+    assert len(regions) < lay.L  # some tables are shared
+    for off, size in regions:
+        a, b = 2 * off, 2 * (off + size)
+        scale = float(gref[a:b].abs().max())
+        if scale > 0:
+            err = float((got[a:b] - gref[a:b]).abs().max()) / scale
+            assert err < 1e-4, (off, err)

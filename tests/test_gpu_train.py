@@ -106,3 +106,21 @@ def test_trainer_learns_a_scene_and_checkpoints(gpu, tmp_path):
     m = NGP(0.5, hp)
     m.load_state_dict({k[6:]: v for k, v in sd.items() if k.startswith("model.")}, strict=False)
     assert torch.equal(m.rgb_net.params.detach(), tr.step.params[tr.step.off_rgb:tr.step.off_table].cpu())
+
+
+def test_trainer_mixedfeature_rgb128_learns_a_scene(gpu):
+    """The MF benchmark configuration's field (benchmark_synthetic_mf.sh: --grid MixedFeature
+    --N_tables 8 --rgb_channels 128) through the whole fused step: shared-table fixed-point table
+    gradient, width-128 MFMA head, pipelined graphs."""
+    imgs, poses, dirs, K = _ball_views(100)
+    t_imgs, t_poses, _, _ = _ball_views(4, seed=7)
+    ds = data.DeviceDataset(imgs, poses, dirs, K=K, img_wh=(64, 64), device=gpu, seed=5)
+    hp = HParams(batch_size=4096, T=16, num_epochs=1, steps_per_epoch=800, grid="MixedFeature", N_tables=8,
+                 rgb_channels=128, lr=2e-2)
+    tr = Trainer(hp, ds, device=gpu)
+    hist = tr.fit(log_every=400)
+    psnr, _ = tr.evaluate(t_imgs, t_poses, dirs)
+    white = sum(float(-10 * torch.log10(((1 - im) ** 2).mean())) for im in t_imgs) / len(t_imgs)
+    print("\nMF128 TRAIN", [(h["step"], round(h["psnr"], 2)) for h in hist], "TEST psnr", round(psnr, 2),
+          "white", round(white, 2))
+    assert psnr > white + 6.0 and hist[-1]["skipped"] == 0

@@ -18,7 +18,10 @@ from mfnerf._lib import call, ptr, stream  # noqa: E402
 
 def main():
     dev = torch.device("cuda:0")
-    step = engine.TrainStep(engine.StepConfig(), device=dev)
+    # MFNERF_KBENCH_PRESET=mf128: config 3's field (MixedFeature, 8 tables, T 2^20, rgb 128, 16384 rays)
+    preset = os.environ.get("MFNERF_KBENCH_PRESET", "lego")
+    kw = {} if preset == "lego" else dict(n_rays=16384, log2_T=20, grid="MixedFeature", N_tables=8, rgb_width=128)
+    step = engine.TrainStep(engine.StepConfig(**kw), device=dev)
     step.set_occupancy(synthetic.ball_density_grid())
     b = step.make_batches(2, seed=100)
     for i in range(6):
@@ -63,7 +66,7 @@ def main():
         "grid_bw_half": lambda: call("mfnerf_debug_grid_bw_half", ptr(m.xyzs), cap, ptr(m.counter), step.x_min,
                                      step.x_range, step.desc, ptr(t.dfeat), ptr(grad_h2), ptr(priv_h2), 2048.0, s()),
         "check": lambda: call("mfnerf_check_finite", ptr(step.grads), step.grads.numel(), ptr(step.finite_status), s()),
-        "adam": lambda: step._adam(step.grads, 0, step.n_alloc),
+        "adam": lambda: step._adam(step.grads, 0, step.n_alloc, False),
         "pack": step._pack,
         "march": lambda: step._march(batch, mb, lambda _n: None),
     }
