@@ -52,15 +52,17 @@ struct Geo {
 //                    wave per SIMD can hold);
 //   W = 64,  NW = 8: all of them accumulate in an LDS image (ds_add_f32 per sample tile), so a wave
 //                    fits in 256 registers and two waves share each SIMD;
-//   W = 128, NW = 4: the rgb-net tiles (dWr1, dWr2, dWr3: 24) in the LDS image -- in registers
-//                    they spill -- the xyz-net ones in registers; Wr2^T (B4, 32 KiB) is read from
-//                    global memory (L2-resident) to leave LDS room for the image (159.5 KiB in all).
+//   W = 128, NW = 4: dW1, dW2, dWr1, dWr3 (12 tiles) in registers as at W = 64; dWr2's 16 tiles do
+//                    not fit beside them, so a second pass (field_bw_wr2_kernel: forward + dR2 only,
+//                    256 accumulator registers) computes dWr2 -- LDS atomics for it measured 19x
+//                    slower than the register path (an LDS-image variant ran 3.4 ms per 983k samples).
 template <int W, int NW>
 struct BwCfg {
     using G = Geo<W>;
     static constexpr bool XYZ_LDS = (NW == 8);            // dW1, dW2
-    static constexpr bool RGB_LDS = XYZ_LDS || W == 128;  // dWr1, dWr2, dWr3
-    static constexpr bool B4_GLOBAL = (W == 128);
+    static constexpr bool RGB_LDS = XYZ_LDS;              // dWr1, dWr2, dWr3
+    static constexpr bool R2_SPLIT = (W == 128);          // dWr2 by field_bw_wr2_kernel
+    static constexpr bool B4_GLOBAL = false;              // Wr2^T from global memory (unused variant)
     static constexpr int SKIP = B4_GLOBAL ? G::MT * G::KC : 0;
     static constexpr int LDS_FRAGS = G::N - SKIP + 4;  // + 4 identity fragments
     static constexpr int ID_BASE = LDS_FRAGS - 4;
@@ -522,7 +524,7 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
             relu_mask<0>(a, T.r2[mt][0]); relu_mask<8>(a, T.r2[mt][1]);
             dr2p[mt][0] = pack8<0, false>(a); dr2p[mt][1] = pack8<8, false>(a);
         }
-        {   // -- rgb layer 2: dWr2 (WxW) += dR2^T R1
+        if constexpr (!C::R2_SPLIT) {   // -- rgb layer 2: dWr2 (WxW) += dR2^T R1
             SOp x[MT];
 #pragma unroll
             for (int i = 0; i < MT; ++i) x[i] = to_s(lds, lane, T.r1[i][0], ID_P0, T.r1[i][1], ID_P16);
@@ -668,10 +670,12 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
 #pragma unroll
             for (int o = 0; o < R2; ++o)
 #pragma unroll
-                for (int i = 0; i < R2; ++i) dw_add32(img + oR2, dwr2[o][i], o, i, W, W, lane);
+                for (int i = 0; i < R2; ++i)
+                    if constexpr (!C::R2_SPLIT) dw_add32(img + oR2, dwr2[o][i], o, i, W, W, lane);
         }
         __syncthreads();
         for (int i = threadIdx.x; i < G::N_DW; i += blockDim.x) {
+            if (C::R2_SPLIT && i >= oR2 && i < oR3) continue;  // written by field_bw_wr2_kernel
             float v;
             if (!RL || i < oR1) v = img[i];
             else if (i < oR3 + 3 * W) v = limg[i - oR1];
@@ -680,6 +684,101 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
         }
         if (level_l1 && threadIdx.x < 16) atomicAdd(level_l1 + threadIdx.x, l1_part[threadIdx.x]);
     }
+}
+
+// Second backward pass at W = 128: dWr2 (W x W) = sum over samples of dR2^T R1, with all 16 tiles in
+// registers.  Recomputes the forward and dR2 = relu'(R2) * Wr3^T dO (what field_bw_kernel does before
+// it), and writes the dWr2 segment of the same slab rows.
+template <int W>
+__global__ __launch_bounds__(FIELD_BLOCK) void field_bw_wr2_kernel(
+    const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n,
+    const int32_t* __restrict__ n_dev, const _Float16* __restrict__ packed, const float* __restrict__ dL_drgb,
+    float grad_scale, float* __restrict__ slab) {
+    using G = Geo<W>;
+    constexpr int MT = G::MT;
+    constexpr int NF = G::B4;  // forward fragments + Wr3^T (B5)
+    constexpr int ID_P0 = NF + 2, ID_P16 = NF + 3;
+    constexpr int oR2 = N_XYZ_PARAMS + W * 32;
+    static_assert((size_t)W * W * 4 <= (size_t)(NF + 4) * FRAG_HALFS * 2, "dWr2 image must fit the fragment area");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    _Float16* lds_base = reinterpret_cast<_Float16*>(smem);
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(packed);
+        uint4* dst = reinterpret_cast<uint4*>(lds_base);
+        for (int i = threadIdx.x; i < NF * 64; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < 4 * 64; i += blockDim.x) {
+            const int fi = i >> 6, ln = i & 63, nn = ln & 31, hh = ln >> 5;
+            const int perm = fi >> 1, off = 16 * (fi & 1);
+            half8 v;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = (_Float16)((off + k_of(j, hh, perm) == nn) ? 1.0f : 0.0f);
+            *reinterpret_cast<half8*>(lds_base + ((NF + fi) * 64 + ln) * 8) = v;
+        }
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const float S = grad_scale, invS = 1.0f / grad_scale;
+    const f32x16 z = {};
+    f32x16 acc[MT][MT];
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < MT; ++b) acc[a][b] = z;
+    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
+    const int64_t tiles = div_up<int64_t>(nn, 32);
+    const int64_t stride = (int64_t)gridDim.x * 4;
+    TileIn nI;
+    float ng0 = 0.f, ng1 = 0.f, ng2 = 0.f;
+    auto fetch = [&](int64_t tile) {
+        const int64_t s = tile * 32 + r;
+        const bool v = s < nn;
+        load_tile_in(feat, plane_stride, dirs, s, v, h, true, nI);
+        ng0 = ng1 = ng2 = 0.0f;
+        if (v && h == 0) { ng0 = dL_drgb[3 * s]; ng1 = dL_drgb[3 * s + 1]; ng2 = dL_drgb[3 * s + 2]; }
+    };
+    const int64_t tile0 = (int64_t)blockIdx.x * 4 + wid;
+    if (tile0 < tiles) fetch(tile0);
+    for (int64_t tile = tile0; tile < tiles; tile += stride) {
+        int opaque = 0;
+        asm volatile("" : "+s"(opaque));
+        const _Float16* lds = lds_base + opaque;
+        const bool valid = tile * 32 + r < nn;
+        const TileIn I = nI;
+        const float g0 = ng0, g1 = ng1, g2 = ng2;
+        if (tile + stride < tiles) fetch(tile + stride);
+        FwdTile<W> T;
+        forward_tile<W, false>(lds, lane, I, valid, T);
+        f32x16 dO = z;
+        if (h == 0) {
+            dO[0] = g0 * S * T.rgb[0] * (1.0f - T.rgb[0]);
+            dO[1] = g1 * S * T.rgb[1] * (1.0f - T.rgb[1]);
+            dO[2] = g2 * S * T.rgb[2] * (1.0f - T.rgb[2]);
+        }
+        const half8 dOb = pack8<0, false>(dO);
+        SOp x[MT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) x[i] = to_s(lds, lane, T.r1[i][0], ID_P0, T.r1[i][1], ID_P16);
+#pragma unroll
+        for (int o = 0; o < MT; ++o) {
+            f32x16 a = mfma(lds_frag(lds, G::B5 + o, lane), dOb, z);
+            relu_mask<0>(a, T.r2[o][0]); relu_mask<8>(a, T.r2[o][1]);
+            const SOp d = to_s(lds, lane, pack8<0, false>(a), ID_P0, pack8<8, false>(a), ID_P16);
+#pragma unroll
+            for (int i = 0; i < MT; ++i) dw_acc(acc[o][i], d, x[i]);
+        }
+    }
+    __syncthreads();
+    float* img = reinterpret_cast<float*>(smem);
+    for (int i = threadIdx.x; i < W * W; i += blockDim.x) img[i] = 0.0f;
+    __syncthreads();
+#pragma unroll
+    for (int o = 0; o < MT; ++o)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) dw_add32(img, acc[o][i], o, i, W, W, lane);
+    __syncthreads();
+    float* row = slab + (int64_t)blockIdx.x * G::N_DW + oR2;
+    for (int i = threadIdx.x; i < W * W; i += blockDim.x) row[i] = img[i] * invS;
 }
 
 // grad[p] += sum over slab rows (fixed order: deterministic).  64 columns x 4 row groups per block.
@@ -773,6 +872,10 @@ int launch_bw(const void* feat, int64_t ps, const float* dirs, int64_t n, const 
     hipLaunchKernelGGL((field_bw_kernel<W, NW>), dim3(BW_BLOCKS), dim3(64 * NW), C::LDS, stream,
                        (const _Float16*)feat, ps, dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb,
                        grad_scale, dL_dfeat, (float*)workspace, nonfinite, level_l1);
+    if constexpr (C::R2_SPLIT)
+        hipLaunchKernelGGL(field_bw_wr2_kernel<W>, dim3(BW_BLOCKS), dim3(FIELD_BLOCK),
+                           (size_t)(Geo<W>::B4 + 4) * FRAG_HALFS * 2, stream, (const _Float16*)feat, ps, dirs, n, n_dev,
+                           (const _Float16*)packed, dL_drgb, grad_scale, (float*)workspace);
     hipLaunchKernelGGL(slab_reduce_kernel<W>, dim3((Geo<W>::N_DW + 63) / 64), dim3(256), 0, stream,
                        (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
     return MFN_OK;
