@@ -11,6 +11,7 @@ bench.py train on it.
 import glob
 import math
 import os
+import struct
 
 import numpy as np
 import torch
@@ -124,6 +125,158 @@ class NSVFDataset:
         self.poses = torch.FloatTensor(np.stack(poses)) if poses else torch.zeros(0, 3, 4)
 
 
+# ---------------------------------------------------------------------------- COLMAP
+# The sparse-model readers the reference's ColmapDataset uses (datasets/colmap_utils.py:108-260, after
+# COLMAP's own binary writers): little-endian; only the fields the dataset reads are kept.
+_COLMAP_MODELS = {0: ("SIMPLE_PINHOLE", 3), 1: ("PINHOLE", 4), 2: ("SIMPLE_RADIAL", 4), 3: ("RADIAL", 5),
+                  4: ("OPENCV", 8), 5: ("OPENCV_FISHEYE", 8), 6: ("FULL_OPENCV", 12), 7: ("FOV", 5),
+                  8: ("SIMPLE_RADIAL_FISHEYE", 4), 9: ("RADIAL_FISHEYE", 5), 10: ("THIN_PRISM_FISHEYE", 12)}
+
+
+def _read(path):
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def read_colmap_cameras(path):
+    """cameras.bin -> {camera_id: (model name, width, height, params f64)}.  Layout: u64 count; per
+    camera i32 id, i32 model id, u64 width, u64 height, f64 params[n(model)]."""
+    buf = _read(path)
+    (n,) = struct.unpack_from("<Q", buf, 0)
+    off, cams = 8, {}
+    for _ in range(n):
+        cid, mid, w, h = struct.unpack_from("<iiQQ", buf, off)
+        name, k = _COLMAP_MODELS[mid]
+        cams[cid] = (name, w, h, np.array(struct.unpack_from(f"<{k}d", buf, off + 24)))
+        off += 24 + 8 * k
+    return cams
+
+
+def read_colmap_images(path):
+    """images.bin -> {image_id: (name, qvec (w, x, y, z), tvec)} in file order.  Layout: u64 count;
+    per image i32 id, f64 qvec[4], f64 tvec[3], i32 camera id, NUL-terminated name, u64 n_points2D,
+    n x (f64 x, f64 y, i64 point3D id)."""
+    buf = _read(path)
+    (n,) = struct.unpack_from("<Q", buf, 0)
+    off, ims = 8, {}
+    for _ in range(n):
+        (iid,) = struct.unpack_from("<i", buf, off)
+        q = np.array(struct.unpack_from("<4d", buf, off + 4))
+        t = np.array(struct.unpack_from("<3d", buf, off + 36))
+        end = buf.index(b"\0", off + 64)
+        (n2d,) = struct.unpack_from("<Q", buf, end + 1)
+        ims[iid] = (buf[off + 64:end].decode("utf-8"), q, t)
+        off = end + 9 + 24 * n2d
+    return ims
+
+
+def read_colmap_points3d(path):
+    """points3D.bin -> (N, 3) f64 xyz in file order.  Layout: u64 count; per point u64 id, f64 xyz[3],
+    u8 rgb[3], f64 error, u64 track length, track x (i32 image id, i32 point2D index)."""
+    buf = _read(path)
+    (n,) = struct.unpack_from("<Q", buf, 0)
+    off, xyz = 8, np.empty((n, 3))
+    for i in range(n):
+        xyz[i] = struct.unpack_from("<3d", buf, off + 8)
+        (tl,) = struct.unpack_from("<Q", buf, off + 43)
+        off += 51 + 8 * tl
+    return xyz
+
+
+def qvec_to_rotmat(q):
+    """COLMAP quaternion (w, x, y, z) -> rotation matrix, in colmap_utils.py:272-282's term order."""
+    w, x, y, z = q
+    return np.array([
+        [1 - 2 * y ** 2 - 2 * z ** 2, 2 * x * y - 2 * w * z, 2 * z * x + 2 * w * y],
+        [2 * x * y + 2 * w * z, 1 - 2 * x ** 2 - 2 * z ** 2, 2 * y * z - 2 * w * x],
+        [2 * z * x - 2 * w * y, 2 * y * z + 2 * w * x, 1 - 2 * x ** 2 - 2 * y ** 2]])
+
+
+def _normalize(v):
+    return v / np.linalg.norm(v)
+
+
+def average_pose(poses, pts3d=None):
+    """ray_utils.py:108-147: centre = mean of the point cloud (else of the camera centres), z = the
+    normalised mean z axis, x = normalize(mean y axis x z), y = z x x."""
+    center = pts3d.mean(0) if pts3d is not None else poses[..., 3].mean(0)
+    z = _normalize(poses[..., 2].mean(0))
+    y_ = poses[..., 1].mean(0)
+    x = _normalize(np.cross(y_, z))
+    y = np.cross(z, x)
+    return np.stack([x, y, z, center], 1)
+
+
+def center_poses(poses, pts3d=None):
+    """ray_utils.py:150-178: poses (and points) expressed in the frame of the average pose."""
+    avg = np.eye(4)
+    avg[:3] = average_pose(poses, pts3d)
+    inv = np.linalg.inv(avg)
+    homo = np.concatenate([poses, np.tile(np.array([0, 0, 0, 1]), (len(poses), 1, 1))], 1)
+    out = (inv @ homo)[:, :3]
+    if pts3d is None:
+        return out
+    return out, pts3d @ inv[:, :3].T + inv[:, 3:].T
+
+
+class ColmapDataset:
+    """datasets/colmap.py:15-159 for COLMAP scenes (the mip-NeRF 360 configs, e.g. garden): camera 1's
+    intrinsics scaled by `downsample` (SIMPLE_RADIAL / PINHOLE / OPENCV; distortion ignored, as
+    there), cam2world poses in image-name order centred on the sparse point cloud and scaled so the
+    nearest camera is at distance 1, every 8th image of that order as the test split, images read
+    without alpha blending; 360_v2 scenes at downsample < 1 read images_{1/downsample}.  The HDR-NeRF
+    branches and the 'test_traj' spiral are out of scope."""
+
+    def __init__(self, root_dir, split="train", downsample=1.0, read_images=True):
+        self.root_dir, self.split, self.downsample = root_dir, split, downsample
+        self.read_intrinsics()
+        self.read_meta(split, read_images)
+
+    def read_intrinsics(self):
+        model, W, H, p = read_colmap_cameras(os.path.join(self.root_dir, "sparse/0/cameras.bin"))[1]
+        ds = self.downsample
+        h, w = int(H * ds), int(W * ds)
+        self.img_wh = (w, h)
+        if model == "SIMPLE_RADIAL":
+            fx = fy = p[0] * ds
+            cx, cy = p[1] * ds, p[2] * ds
+        elif model in ("PINHOLE", "OPENCV"):
+            fx, fy, cx, cy = p[0] * ds, p[1] * ds, p[2] * ds, p[3] * ds
+        else:
+            raise ValueError(f"Please parse the intrinsics for camera model {model}!")
+        self.K = torch.FloatTensor([[fx, 0, cx], [0, fy, cy], [0, 0, 1]])
+        self.directions = get_ray_directions(h, w, self.K)
+
+    def read_meta(self, split, read_images=True):
+        r = self.root_dir
+        if split == "test_traj" or "HDR-NeRF" in r:
+            raise NotImplementedError("COLMAP test_traj / HDR-NeRF splits are out of scope")
+        ims = read_colmap_images(os.path.join(r, "sparse/0/images.bin"))
+        names = [v[0] for v in ims.values()]
+        perm = np.argsort(names)
+        folder = f"images_{int(1 / self.downsample)}" if "360_v2" in r and self.downsample < 1 else "images"
+        paths = [os.path.join(r, folder, nm) for nm in sorted(names)]
+        w2c = np.stack([np.concatenate([np.concatenate([qvec_to_rotmat(q), t.reshape(3, 1)], 1),
+                                        np.array([[0, 0, 0, 1.0]])], 0) for _, q, t in ims.values()])
+        poses = np.linalg.inv(w2c)[perm, :3]
+        pts = read_colmap_points3d(os.path.join(r, "sparse/0/points3D.bin"))
+        self.poses, self.pts3d = center_poses(poses, pts)
+        scale = np.linalg.norm(self.poses[..., 3], axis=-1).min()
+        self.poses[..., 3] /= scale
+        self.pts3d /= scale
+        keep = list(range(len(paths)))
+        if split == "train":
+            keep = [i for i in keep if i % 8 != 0]
+        elif split == "test":
+            keep = [i for i in keep if i % 8 == 0]
+        self.img_paths = [paths[i] for i in keep]
+        poses = self.poses[keep]
+        if read_images:
+            rays = [read_image(pth, self.img_wh, blend_a=False) for pth in self.img_paths]
+            self.rays = torch.FloatTensor(np.stack(rays)) if rays else torch.zeros(0, 0, 3)
+        self.poses = torch.FloatTensor(poses)
+
+
 # ---------------------------------------------------------------------------- GPU-resident batches
 class DeviceDataset:
     """Images (n_img, hw, 3), poses (n_img, 3, 4) and camera directions (hw, 3) resident in HBM;
@@ -143,8 +296,11 @@ class DeviceDataset:
         self.calls = torch.zeros(1, dtype=torch.int64, device=device)  # device draw counter
 
     @classmethod
-    def from_nsvf(cls, ds: NSVFDataset, device="cuda", **kw):
+    def from_dataset(cls, ds, device="cuda", **kw):
+        """From an NSVFDataset or a ColmapDataset (rays, poses, directions, K, img_wh)."""
         return cls(ds.rays, ds.poses, ds.directions, K=ds.K, img_wh=ds.img_wh, device=device, **kw)
+
+    from_nsvf = from_dataset
 
     def sample(self, out, img_idx=None, pix_idx=None):
         """out (3, N, 3) f32 <- [rays_o | rays_d | rgb] of N random rays."""

@@ -530,8 +530,13 @@ class TrainStep:
             self.graphs["pack"] = cap(self._pack)
         else:
             self.graphs["update"] = cap(self._update)
+            if P == 1:  # no collective between them: one graph, one launch gap less
+                self.graphs["finish_update"] = cap(lambda: (self._grid_finish(0), self._update()))
         torch.cuda.synchronize()
-        self._side = torch.cuda.Stream(device=self.dev)
+        # the next step's march runs beside this step's grid_bw scatter, whose 4096 workgroups would
+        # otherwise take every dispatch slot first (the march's small kernels then finish after the
+        # scatter, on the critical path): the side stream gets the higher queue priority
+        self._side = torch.cuda.Stream(device=self.dev, priority=torch.cuda.Stream.priority_range()[1])
         self._part_streams = [None] + [torch.cuda.Stream(device=self.dev) for _ in range(P - 1)]
         self._ev_march = [torch.cuda.Event(), torch.cuda.Event()]
         self._ev_start = torch.cuda.Event()
@@ -567,6 +572,7 @@ class TrainStep:
         grid_bw_events: optional (start, [end per part]) timing events -- start before part 0's
         grid_bw, end after each part's grid_bw."""
         g, j, P = self.graphs, self._parity, self.n_parts
+        fuse_tail = g.get("finish_update") is not None and exchange is None
         if self.dataset is not None:
             batch = None
             if prefetch is None:
@@ -600,7 +606,8 @@ class TrainStep:
                     grid_bw_events[1][q].record(sq)
                 if q > 0:  # the folds read-modify-write the shared gradient: one part at a time
                     sq.wait_event(self._ev_part[q - 1])
-                g["finish"][q].replay()
+                if not fuse_tail:
+                    g["finish"][q].replay()
                 self._ev_part[q].record(sq)
         for q in range(1, P):
             main.wait_event(self._ev_part[q])
@@ -609,6 +616,9 @@ class TrainStep:
         if self.shard is not None:
             self._optimize(None, adam=lambda _g: self._shard_adam(g["adam"].replay),
                            pack=g["pack"].replay)
+        elif fuse_tail:
+            self.adam_step += 1
+            g["finish_update"].replay()
         else:
             self._optimize(exchange, adam=lambda _g: g["update"].replay())
         self._parity = 1 - j

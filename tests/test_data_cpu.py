@@ -83,3 +83,61 @@ def test_ball_scene_renders_hits_and_background():
     d = torch.tensor([[0.0, 0.0, 1.0], [0.0, 0.0, 1.0]])
     out = sc.render(o, d)
     assert torch.allclose(out[0], sc.rgb[0]) and torch.equal(out[1], torch.ones(3))
+
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_colmap_loader_matches_reference_golden():
+    """ColmapDataset vs the reference's datasets/colmap.py run on the same generated sparse model
+    (tests/golden/make_golden_colmap.py): K, img_wh, centred + scaled poses of both splits (name
+    order, every-8th test image), the centred point cloud and the pixel values."""
+    z = np.load(os.path.join(GOLD, "golden_colmap.npz"))
+    root = os.path.join(GOLD, "colmap_scene")
+    for split in ("train", "test"):
+        ds = data.ColmapDataset(root, split=split)
+        assert ds.poses.shape == z[f"{split}_poses"].shape
+        assert np.allclose(ds.poses.numpy(), z[f"{split}_poses"], atol=1e-6, rtol=0)
+        assert np.array_equal(ds.rays.numpy(), z[f"{split}_rays"])
+    assert np.array_equal(ds.K.numpy(), z["K"]) and tuple(ds.img_wh) == tuple(z["img_wh"])
+    assert np.allclose(ds.pts3d, z["pts3d"], atol=1e-9)
+    # the nearest camera sits at distance 1 after the scaling
+    allp = data.ColmapDataset(root, split="val", read_images=False).poses
+    assert abs(float(allp[..., 3].norm(dim=-1).min()) - 1.0) < 1e-6
+
+
+def test_colmap_readers_and_360_folder(tmp_path):
+    """Binary readers on a hand-built model (SIMPLE_RADIAL intrinsics, an image with 2D points) and
+    the mip-NeRF 360 images_{1/downsample} folder rule (colmap.py:53-56)."""
+    import struct
+    from PIL import Image
+    root = tmp_path / "360_v2" / "garden"
+    (root / "sparse" / "0").mkdir(parents=True)
+    (root / "images_4").mkdir()
+    with open(root / "sparse/0/cameras.bin", "wb") as f:
+        f.write(struct.pack("<Q", 1) + struct.pack("<iiQQ", 1, 2, 80, 40) + struct.pack("<4d", 50.0, 40.0, 20.0, 0.1))
+    q = np.array([0.9, 0.1, -0.3, 0.2])
+    q /= np.linalg.norm(q)
+    with open(root / "sparse/0/images.bin", "wb") as f:
+        f.write(struct.pack("<Q", 2))
+        for k, name in enumerate(["b.jpg", "a.jpg"]):
+            f.write(struct.pack("<i4d3di", 7 + k, *q, 1.0 + k, 2.0, -1.0, 1) + name.encode() + b"\0")
+            f.write(struct.pack("<Q", 2) + struct.pack("<ddq", 1.0, 2.0, 5) * 2)
+    with open(root / "sparse/0/points3D.bin", "wb") as f:
+        f.write(struct.pack("<Q", 2))
+        for p in range(2):
+            f.write(struct.pack("<Q3d3Bd", p, 0.5 * p, -1.0, 2.0, 1, 2, 3, 0.5) + struct.pack("<Q", 1)
+                    + struct.pack("<ii", 7, 0))
+    for name in ("a.jpg", "b.jpg"):
+        Image.fromarray(np.zeros((10, 20, 3), np.uint8)).save(root / "images_4" / name)
+    cams = data.read_colmap_cameras(str(root / "sparse/0/cameras.bin"))
+    assert cams[1][0] == "SIMPLE_RADIAL" and cams[1][1:3] == (80, 40)
+    ims = data.read_colmap_images(str(root / "sparse/0/images.bin"))
+    assert [v[0] for v in ims.values()] == ["b.jpg", "a.jpg"] and np.allclose(ims[8][2], [2.0, 2.0, -1.0])
+    R = data.qvec_to_rotmat(q)
+    assert np.allclose(R @ R.T, np.eye(3), atol=1e-12) and abs(np.linalg.det(R) - 1) < 1e-12
+    assert np.allclose(data.read_colmap_points3d(str(root / "sparse/0/points3D.bin")), [[0, -1, 2], [0.5, -1, 2]])
+    ds = data.ColmapDataset(str(root), split="val", downsample=0.25)
+    assert ds.img_wh == (20, 10) and ds.img_paths[0].endswith(os.path.join("images_4", "a.jpg"))
+    assert torch.allclose(ds.K, torch.tensor([[12.5, 0, 10.0], [0, 12.5, 5.0], [0, 0, 1]]))
+    assert ds.rays.shape == (2, 200, 3)
