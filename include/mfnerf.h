@@ -296,6 +296,16 @@ int mfnerf_sample_rays(const float* images, const float* poses, const float* dir
                        int64_t n_rays, int same_image, uint64_t seed, uint64_t* call, float* out, int32_t* img_idx,
                        int32_t* pix_idx, mfnerf_stream_t stream);
 
+/* mfnerf_sample_rays (no index outputs) fused with the ray-march prologue of the engine's step:
+ * hits_t (n_rays,2) = ray_aabb_intersect of each drawn ray with the one box (center, half_size),
+ * max_hits 1 (intersection.cu:5-56), with the near clamp t1 in [0, near) -> near
+ * (rendering.py:29), and noise (n_rays) ~ U[0,1) (custom_functions.py:83) from the same counter
+ * hash as the draws.  One launch instead of sample + AABB + clamp + noise kernels. */
+int mfnerf_sample_rays_prep(const float* images, const float* poses, const float* directions, int64_t n_img,
+                            int64_t hw, int64_t n_rays, int same_image, uint64_t seed, uint64_t* call, float* out,
+                            const float* center, const float* half_size, float near, float* hits_t, float* noise,
+                            mfnerf_stream_t stream);
+
 /* ---------------------------------------------------------------- optimizer */
 
 /* Adam (apex FusedAdam semantics, adam_w_mode=False, no weight decay; train.py:136):

@@ -77,6 +77,8 @@ SIGNATURES = {
     "mfnerf_occupancy_cells": (_I, [_P, _I, _I, _F, _I64, _I, _F, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P]),
     "mfnerf_occupancy_update": (_I, [_P, _P, _P, _I64, _I, _I, _F, _P, _F, _P, _P, _P, _P]),
     "mfnerf_sample_rays": (_I, [_P, _P, _P, _I64, _I64, _I64, _I, ctypes.c_uint64, _P, _P, _P, _P, _P]),
+    "mfnerf_sample_rays_prep": (_I, [_P, _P, _P, _I64, _I64, _I64, _I, ctypes.c_uint64, _P, _P, _P, _P, _F, _P, _P,
+                                     _P]),
     "mfnerf_adam_step": (_I, [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _I, _P]),
     "mfnerf_check_finite": (_I, [_P, _I64, _P, _P]),
     "mfnerf_flag_to_shards": (_I, [_P, _I64, _I64, _P, _P]),

@@ -302,9 +302,17 @@ class DeviceDataset:
 
     from_nsvf = from_dataset
 
-    def sample(self, out, img_idx=None, pix_idx=None):
-        """out (3, N, 3) f32 <- [rays_o | rays_d | rgb] of N random rays."""
+    def sample(self, out, img_idx=None, pix_idx=None, prep=None):
+        """out (3, N, 3) f32 <- [rays_o | rays_d | rgb] of N random rays.  prep = (center, half_size,
+        near, hits_t (N,2), noise (N)): also the march prologue (AABB hit, near clamp, noise) of the
+        drawn rays, in the same launch (mfnerf_sample_rays_prep)."""
         n = out.shape[1]
+        if prep is not None:
+            center, half_size, near, hits_t, noise = prep
+            call("mfnerf_sample_rays_prep", ptr(self.images), ptr(self.poses), ptr(self.directions), self.n_img,
+                 self.hw, n, self.same_image, self.seed, ptr(self.calls), ptr(out), ptr(center), ptr(half_size),
+                 float(near), ptr(hits_t), ptr(noise), stream())
+            return out
         call("mfnerf_sample_rays", ptr(self.images), ptr(self.poses), ptr(self.directions), self.n_img, self.hw, n,
              self.same_image, self.seed, ptr(self.calls), ptr(out), ptr(img_idx), ptr(pix_idx), stream())
         return out

@@ -291,16 +291,23 @@ class TrainStep:
         self.graphs = None  # re-capture with the sharded update
 
     # ---------------------------------------------------------------- the step
-    def _march(self, batch: Batch, mb, mark):
-        """AABB + near clamp + noise for the whole batch, then one ray march per part into mb."""
+    def _draw(self, batch: Batch, mb):
+        """The attached dataset's next batch into `batch`, with the march prologue (AABB + near clamp
+        + noise) of mb in the same launch."""
+        self.dataset.sample(batch.buf, prep=(self.center, self.half_size, NEAR_DISTANCE, mb.hits, mb.noise))
+
+    def _march(self, batch: Batch, mb, mark, prepped=False):
+        """AABB + near clamp + noise for the whole batch (unless _draw did it), then one ray march per
+        part into mb."""
         c, s = self.cfg, stream()
         N, Np = c.n_rays, self.Np
-        # rendering.py:27-29 (AABB + near clamp), custom_functions.py:83 (noise)
-        call("mfnerf_ray_aabb_intersect", ptr(batch.rays_o), ptr(batch.rays_d), ptr(self.center),
-             ptr(self.half_size), N, 1, 1, ptr(mb.hit_cnt), ptr(mb.hits), ptr(mb.hits_idx), s)
-        t1 = mb.hits[:, 0, 0]
-        t1.masked_fill_((t1 >= 0) & (t1 < NEAR_DISTANCE), NEAR_DISTANCE)
-        torch.rand(N, generator=self.gen, device=self.dev, out=mb.noise)
+        if not prepped:
+            # rendering.py:27-29 (AABB + near clamp), custom_functions.py:83 (noise)
+            call("mfnerf_ray_aabb_intersect", ptr(batch.rays_o), ptr(batch.rays_d), ptr(self.center),
+                 ptr(self.half_size), N, 1, 1, ptr(mb.hit_cnt), ptr(mb.hits), ptr(mb.hits_idx), s)
+            t1 = mb.hits[:, 0, 0]
+            t1.masked_fill_((t1 >= 0) & (t1 < NEAR_DISTANCE), NEAR_DISTANCE)
+            torch.rand(N, generator=self.gen, device=self.dev, out=mb.noise)
         mark("prep")
         for q, t in enumerate(mb.part):
             r = slice(q * Np, (q + 1) * Np)
@@ -453,14 +460,15 @@ class TrainStep:
         optimize=False stops after the backward and leaves the step's gradient in self.grads (no
         Adam step, no repack; for inspection)."""
         mark = mark or (lambda name: None)
-        if batch is None:
-            batch = self._sampled
-            self.dataset.sample(batch.buf)
         mb = self.mbuf[0]
+        prepped = batch is None
+        if prepped:
+            batch = self._sampled
+            self._draw(batch, mb)
         self._use(mb)
         self.last_batch = batch
         self._primed = False  # a pipelined replay() must march its own batch next
-        self._march(batch, mb, mark)
+        self._march(batch, mb, mark, prepped=prepped)
         for q in range(self.n_parts):
             self._chain(batch, mb, q, mark)
             self._grid_bw(mb, q)
@@ -513,8 +521,8 @@ class TrainStep:
         P = self.n_parts
         def march(j):
             if self.dataset is not None:
-                self.dataset.sample(self._static[j].buf)
-            self._march(self._static[j], self.mbuf[j], nomark)
+                self._draw(self._static[j], self.mbuf[j])
+            self._march(self._static[j], self.mbuf[j], nomark, prepped=self.dataset is not None)
 
         self.graphs = {
             "march": [cap(lambda j=j: march(j), rng=True) for j in range(2)],

@@ -124,3 +124,50 @@ def test_trainer_mixedfeature_rgb128_learns_a_scene(gpu):
     print("\nMF128 TRAIN", [(h["step"], round(h["psnr"], 2)) for h in hist], "TEST psnr", round(psnr, 2),
           "white", round(white, 2))
     assert psnr > white + 6.0 and hist[-1]["skipped"] == 0
+
+
+def test_trainer_on_a_colmap_scene(gpu):
+    """The real-scene configuration (benchmark_mipnerf360_mf.sh: colmap, --scale 16): 6 cascades,
+    exp_step_factor 1/256 marching, black background, the occupancy erode -- on the generated COLMAP
+    scene of tests/golden (noise images: the check is that every piece runs and stays finite)."""
+    import os
+    from conftest import ROOT
+    ds0 = data.ColmapDataset(os.path.join(ROOT, "tests", "golden", "colmap_scene"), split="train")
+    ds = data.DeviceDataset.from_dataset(ds0, device=gpu, seed=2)
+    hp = HParams(dataset_name="colmap", scale=16.0, batch_size=1024, T=16, num_epochs=1, steps_per_epoch=300,
+                 grid="MixedFeature", N_tables=8, rgb_channels=128)
+    tr = Trainer(hp, ds, device=gpu)
+    assert tr.step.cascades == 6
+    hist = tr.fit(log_every=100)
+    assert all(math.isfinite(h["loss"]) for h in hist) and hist[-1]["skipped"] == 0
+    assert torch.isfinite(tr.step.params).all()
+
+
+def test_sample_rays_prep_matches_aabb_and_clamp(gpu):
+    """The fused draw + march prologue: the drawn rays equal mfnerf_sample_rays' (same counter), and
+    hits_t equals ray_aabb_intersect + the near clamp (rendering.py:27-29) on them, bit for bit; the
+    noise is U[0,1) and fresh on every draw."""
+    from mfnerf import vren
+    g = torch.Generator().manual_seed(1)
+    n_img, hw, N = 4, 500, 4096
+    imgs = torch.rand(n_img, hw, 3, generator=g)
+    poses = torch.cat([torch.linalg.qr(torch.randn(n_img, 3, 3, generator=g))[0],
+                       torch.rand(n_img, 3, 1, generator=g) * 3 - 1.5], 2)
+    dirs = torch.randn(hw, 3, generator=g)
+    center, half = torch.zeros(1, 3, device=gpu), torch.full((1, 3), 0.5, device=gpu)
+    a = data.DeviceDataset(imgs, poses, dirs, device=gpu, seed=4)
+    b = data.DeviceDataset(imgs, poses, dirs, device=gpu, seed=4)
+    out_a, out_b = torch.empty(3, N, 3, device=gpu), torch.empty(3, N, 3, device=gpu)
+    hits, noise = torch.empty(N, 2, device=gpu), torch.empty(N, device=gpu)
+    a.sample(out_a)
+    b.sample(out_b, prep=(center, half, 0.01, hits, noise))
+    assert torch.equal(out_a, out_b)
+    _, ht, _ = vren.ray_aabb_intersect(out_b[0].contiguous(), out_b[1].contiguous(), center, half, 1)
+    t1 = ht[:, 0, 0]
+    t1[(t1 >= 0) & (t1 < 0.01)] = 0.01
+    assert torch.equal(hits, ht[:, 0])
+    assert (hits[:, 0] >= 0).sum() > 100 and (hits[:, 0] < 0).sum() > 100
+    assert float(noise.min()) >= 0.0 and float(noise.max()) < 1.0 and abs(float(noise.mean()) - 0.5) < 0.02
+    n1 = noise.clone()
+    b.sample(out_b, prep=(center, half, 0.01, hits, noise))
+    assert not torch.equal(n1, noise)
