@@ -125,6 +125,7 @@ class TrainStep:
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # Adam's t, bumped on the device
         self.lr_dev = torch.full((1,), float(c.lr), dtype=torch.float32, device=dev)
         self.graphs = None
+        self.samples_marched = torch.zeros(1, dtype=torch.int64, device=dev)
 
         # scene bounding box (networks.py:18-23) and occupancy
         self.center = torch.zeros(1, 3, device=dev)
@@ -315,6 +316,9 @@ class TrainStep:
                  ptr(self.bitfield), self.cascades, float(c.scale), 0.0 if c.scale <= 0.5 else 1 / 256,
                  ptr(mb.noise[r]), self.G, c.max_samples, Np, self.cap_p, ptr(t.rays_a), ptr(t.xyzs), ptr(t.dirs),
                  ptr(t.deltas), ptr(t.ts), ptr(t.counter), ptr(t.march_ws), s)
+        # running total of marched samples (rm_s without a read on the step's critical path: in the
+        # graphs this runs on the march's side stream)
+        self.samples_marched.add_(mb.counters[:, 0].sum())
         mark("march")
 
     def _chain(self, batch: Batch, mb, q, mark):
