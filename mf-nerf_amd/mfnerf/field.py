@@ -116,6 +116,26 @@ class GridEncodeFunction(torch.autograd.Function):
         return None, g, None, None
 
 
+_weights_cache = {}
+
+
+def field_weights(xyz_params, rgb_params, rgb_width):
+    """(packed MLP fragments, fp16 table) of these parameter tensors, re-derived only when one of
+    them changed (their version counters): the test-time loop calls the field many times per frame
+    with the same weights."""
+    key = (xyz_params.data_ptr(), rgb_params.data_ptr(), int(rgb_width))
+    ver = (xyz_params._version, rgb_params._version)
+    hit = _weights_cache.get(key)
+    if hit is not None and hit[0] == ver:
+        return hit[1], hit[2]
+    net = xyz_params[:XYZ_NET_PARAMS].detach().contiguous()
+    table16 = xyz_params[XYZ_NET_PARAMS:].detach().half().contiguous()
+    packed = pack_field_weights(net, rgb_params.detach().contiguous(), rgb_width)
+    _weights_cache.clear()  # the current model only
+    _weights_cache[key] = (ver, packed, table16)
+    return packed, table16
+
+
 class NGPFieldFunction(torch.autograd.Function):
     """Fused NGP.forward (networks.py:134-155): world xyz, dirs -> sigma f32 (N), rgb f32 (N,3).
 
@@ -127,9 +147,7 @@ class NGPFieldFunction(torch.autograd.Function):
         xyzs = xyzs.float().contiguous()
         dirs = dirs.float().contiguous()
         n = xyzs.shape[0]
-        net = xyz_params[:XYZ_NET_PARAMS].detach().contiguous()
-        table16 = xyz_params[XYZ_NET_PARAMS:].detach().half().contiguous()
-        packed = pack_field_weights(net, rgb_params.detach().contiguous(), rgb_width)
+        packed, table16 = field_weights(xyz_params, rgb_params, rgb_width)
         feat = grid_encode_fw(xyzs, n, table16, layout, desc, x_min, x_range)
         sigma, rgb = field_fw(feat, dirs, n, packed, rgb_width)
         ctx.save_for_backward(xyzs, dirs, feat, packed, sigma)
@@ -166,9 +184,7 @@ class NGPDensityFunction(torch.autograd.Function):
     def forward(ctx, xyzs, xyz_params, rgb_params, layout, desc, x_min, x_range, rgb_width):
         xyzs = xyzs.float().contiguous()
         n = xyzs.shape[0]
-        net = xyz_params[:XYZ_NET_PARAMS].detach().contiguous()
-        table16 = xyz_params[XYZ_NET_PARAMS:].detach().half().contiguous()
-        packed = pack_field_weights(net, rgb_params.detach().contiguous(), rgb_width)
+        packed, table16 = field_weights(xyz_params, rgb_params, rgb_width)
         feat = grid_encode_fw(xyzs, n, table16, layout, desc, x_min, x_range)
         sigma, _ = field_fw(feat, None, n, packed, rgb_width, density_only=True)
         return sigma

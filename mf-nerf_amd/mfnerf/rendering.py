@@ -67,13 +67,17 @@ def _render_rays_test(model, rays_o, rays_d, hits_t, **kwargs):
         xyzs = rearrange(xyzs, "n1 n2 c -> (n1 n2) c")
         dirs = rearrange(dirs, "n1 n2 c -> (n1 n2) c")
         valid_mask = ~torch.all(dirs == 0, dim=1)
-        if valid_mask.sum() == 0:
+        # the valid samples' indices once (one host sync), instead of a mask sum plus a nonzero per
+        # boolean index below; same values as the reference's masked assignments
+        valid = valid_mask.nonzero()[:, 0]
+        if len(valid) == 0:
             break
 
         sigmas = torch.zeros(len(xyzs), device=device)
         rgbs = torch.zeros(len(xyzs), 3, device=device)
-        sigmas[valid_mask], _rgbs = model(xyzs[valid_mask], dirs[valid_mask], **kwargs)
-        rgbs[valid_mask] = _rgbs.float()
+        _sigmas, _rgbs = model(xyzs.index_select(0, valid), dirs.index_select(0, valid), **kwargs)
+        sigmas.index_copy_(0, valid, _sigmas.float())
+        rgbs.index_copy_(0, valid, _rgbs.float())
         sigmas = rearrange(sigmas, "(n1 n2) -> n1 n2", n2=N_samples)
         rgbs = rearrange(rgbs, "(n1 n2) c -> n1 n2 c", n2=N_samples)
 
