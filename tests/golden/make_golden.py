@@ -11,7 +11,9 @@ VolumeRenderer packing (vr_samples), NeRFLoss terms, TruncExp, NGP.forward's nor
 input/concat order, the test-time progressive loop, mark_invisible_cells, and the gradients the
 reference's autograd graph produces.  Only data (inputs/outputs) is written to golden_*.npz.
 
-Run from anywhere:  python tests/golden/make_golden.py   (needs /root/reference; CPU only)
+Run from anywhere:  python tests/golden/make_golden.py [mf128]   (needs /root/reference; CPU only)
+"mf128" writes golden_render_mf128.*: the same vectors for the MF benchmark field (MixedFeature
+grid with 8 shared tables, rgb_channels 128).
 """
 import math
 import os
@@ -54,7 +56,15 @@ class HP:
     grid, L, F, T, N_min, N_max, N_tables, rgb_channels, rgb_layers = "Hash", 16, 2, 12, 4, 256, 1, 64, 2
 
 
-def main():
+class HPMF(HP):
+    """The MF benchmark field (benchmark_synthetic_mf.sh: MixedFeature, 8 tables, rgb 128)."""
+    grid, N_tables, rgb_channels = "MixedFeature", 8, 128
+
+
+def main(variant=""):
+    global HP
+    if variant == "mf128":
+        HP = HPMF
     install_stubs()
     import warnings
     warnings.filterwarnings("ignore")
@@ -128,15 +138,16 @@ def main():
     out["invisible_bits"] = torch.from_numpy(np.packbits((model.density_grid[0] < 0).numpy(), bitorder="little"))
     out["mark_K"], out["mark_poses"] = K, poses[:3]
 
-    np.savez_compressed(os.path.join(HERE, "golden_render.npz"),
+    tag = "_" + variant if variant else ""
+    np.savez_compressed(os.path.join(HERE, f"golden_render{tag}.npz"),
                         **{k: v.numpy() if isinstance(v, torch.Tensor) else np.asarray(v) for k, v in out.items()})
     meta = {"hparams": {k: getattr(HP, k) for k in ("grid", "L", "F", "T", "N_min", "N_max", "N_tables",
                                                     "rgb_channels", "rgb_layers")}, "scale": scale, "n_rays": N}
     import json
-    with open(os.path.join(HERE, "golden_render.json"), "w") as f:
+    with open(os.path.join(HERE, f"golden_render{tag}.json"), "w") as f:
         json.dump(meta, f, indent=1)
-    print("wrote golden_render.npz:", {k: tuple(v.shape) for k, v in out.items() if isinstance(v, torch.Tensor)})
+    print(f"wrote golden_render{tag}.npz:", {k: tuple(v.shape) for k, v in out.items() if isinstance(v, torch.Tensor)})
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else "")

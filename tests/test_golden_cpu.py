@@ -14,10 +14,10 @@ from oracle import field_oracle as FO
 GOLD = os.path.join(ROOT, "tests", "golden")
 
 
-@pytest.fixture(scope="module")
-def gold():
-    z = np.load(os.path.join(GOLD, "golden_render.npz"))
-    meta = json.load(open(os.path.join(GOLD, "golden_render.json")))
+@pytest.fixture(scope="module", params=["", "_mf128"], ids=["hash-rgb64", "mixedfeature-rgb128"])
+def gold(request):
+    z = np.load(os.path.join(GOLD, f"golden_render{request.param}.npz"))
+    meta = json.load(open(os.path.join(GOLD, f"golden_render{request.param}.json")))
     return {k: torch.from_numpy(z[k]) for k in z.files}, meta
 
 
@@ -53,7 +53,8 @@ def test_oracle_field_and_composite_match_golden(gold, oracle):
     h = FO.mlp_forward(feat, px[:3072], 32, 16, 64, 1)
     sigma = torch.exp(h[:, 0])
     dn = d / torch.norm(d, dim=1, keepdim=True)
-    rgbs = FO.mlp_forward(torch.cat([FO.sh4((dn + 1) / 2), h], 1), z["rgb_params"], 32, 3, 64, 2, "ReLU", "Sigmoid")
+    rgbs = FO.mlp_forward(torch.cat([FO.sh4((dn + 1) / 2), h], 1), z["rgb_params"], 32, 3, hp["rgb_channels"], 2,
+                          "ReLU", "Sigmoid")
     tot, op, dep, rgb, ws = oracle.composite_train_fw(sigma.contiguous(), rgbs.contiguous(), z["deltas"], z["ts"],
                                                       z["rays_a"], 1e-4)
     assert int(tot.sum()) == int(z["vr_samples"])

@@ -19,12 +19,12 @@ class HP:
     pass
 
 
-@pytest.fixture(scope="module")
-def setup(gpu):
+@pytest.fixture(scope="module", params=["", "_mf128"], ids=["hash-rgb64", "mixedfeature-rgb128"])
+def setup(gpu, request):
     from mfnerf.networks import NGP
-    z = np.load(os.path.join(GOLD, "golden_render.npz"))
+    z = np.load(os.path.join(GOLD, f"golden_render{request.param}.npz"))
     z = {k: torch.from_numpy(z[k]) for k in z.files}
-    meta = json.load(open(os.path.join(GOLD, "golden_render.json")))
+    meta = json.load(open(os.path.join(GOLD, f"golden_render{request.param}.json")))
     hp = HP()
     for k, v in meta["hparams"].items():
         setattr(hp, k, v)
