@@ -35,13 +35,7 @@ __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ g, float*
         float4 vv = reinterpret_cast<float4*>(v)[i];
         float* pa = &pp.x; const float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float gk = ga[k] * gscale;
-            ma[k] = b1 * ma[k] + (1.0f - b1) * gk;
-            va[k] = b2 * va[k] + (1.0f - b2) * gk * gk;
-            const float denom = sqrtf(va[k] / bc2) + eps;
-            pa[k] = pa[k] - lr * ((ma[k] / bc1) / denom);
-        }
+        for (int k = 0; k < 4; ++k) mfn::adam_elem(pa[k], ma[k], va[k], ga[k] * gscale, b1, b2, eps, lr, bc1, bc2);
         reinterpret_cast<float4*>(p)[i] = pp;
         reinterpret_cast<float4*>(m)[i] = mm;
         reinterpret_cast<float4*>(v)[i] = vv;
@@ -54,11 +48,7 @@ __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ g, float*
     }
     // tail
     for (int64_t i = n4 * 4 + t0; i < n; i += stride) {
-        const float gk = g[i] * gscale;
-        m[i] = b1 * m[i] + (1.0f - b1) * gk;
-        v[i] = b2 * v[i] + (1.0f - b2) * gk * gk;
-        const float denom = sqrtf(v[i] / bc2) + eps;
-        p[i] = p[i] - lr * ((m[i] / bc1) / denom);
+        mfn::adam_elem(p[i], m[i], v[i], g[i] * gscale, b1, b2, eps, lr, bc1, bc2);
         if (zero_grads) g[i] = 0.0f;
         if (p16) p16[i] = __float2half_rn(p[i]);
     }
@@ -66,10 +56,14 @@ __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ g, float*
 
 // after the update: count the step (or the skipped step) and clear the non-finite flag for the
 // next step's producers
-__global__ void bump_step_kernel(int32_t* s, int32_t* skip) {
+}  // namespace
+
+__global__ void mfn_bump_step_kernel(int32_t* s, int32_t* skip) {
     if (skip && skip[0]) { skip[1] += 1; skip[0] = 0; }
     else if (s) *s += 1;
 }
+
+namespace {
 
 // status[0] = 1 if any x is inf/nan (status[0] must be 0 on entry); one atomic per offending wave
 __global__ void finite_kernel(const float* __restrict__ x, int64_t n, int32_t* __restrict__ status) {
@@ -129,7 +123,7 @@ extern "C" int mfnerf_adam_step(float* params, float* grads, float* m, float* v,
     const unsigned blocks = (unsigned)(want < 4096 ? (want < 1 ? 1 : want) : 4096);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(threads), 0, stream, params, grads, m, v, (__half*)p_f16, n, lr,
                        beta1, beta2, eps, grad_scale, step, step_dev, lr_dev, skip, zero_grads);
-    if (step_dev || skip) hipLaunchKernelGGL(bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, skip);
+    if (step_dev || skip) hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, skip);
     return mfn_check_launch("adam_step");
 }
 

@@ -86,6 +86,16 @@ __device__ __forceinline__ float fast_exp(float x) { return __expf(x); }
 template <typename T>
 __host__ __device__ __forceinline__ T div_up(T a, T b) { return (a + b - 1) / b; }
 
+// One Adam update (apex multi_tensor_adam ADAM_MODE, weight decay 0: m/(1-b1^t), v/(1-b2^t),
+// p -= lr*m_hat/(sqrt(v_hat)+eps)); g already scaled.  bc1/bc2 = 1 - beta^t.
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float b1, float b2, float eps,
+                                          float lr, float bc1, float bc2) {
+    m = b1 * m + (1.0f - b1) * g;
+    v = b2 * v + (1.0f - b2) * g * g;
+    const float denom = sqrtf(v / bc2) + eps;
+    p = p - lr * ((m / bc1) / denom);
+}
+
 }  // namespace mfn
 
 // Error plumbing shared by every C-ABI entry point.

@@ -401,6 +401,20 @@ __device__ __forceinline__ void dw_acc(f32x16& acc, const SOp& dy, const SOp& x)
     acc = mfma(dy.k[0], x.k[0], acc);
     acc = mfma(dy.k[1], x.k[1], acc);
 }
+// The same product into a PERSISTENT accumulator pinned to AGPRs: with MFMA results in VGPRs
+// (-amdgpu-mfma-vgpr-form, which the data-gradient chain needs) the compiler otherwise moves each
+// of the 12 accumulator tiles AGPR <-> VGPR around every update (~500 v_accvgpr moves per tile).
+// The leading s_nop covers the VALU-write -> MFMA-read hazard on the packed operands (the compiler's
+// hazard recognizer does not look into inline asm); back-to-back accumulation into the same
+// registers needs none.  Readers of the accumulators wait with xdl_drain().
+__device__ __forceinline__ void dw_acc_agpr(f32x16& acc, const SOp& dy, const SOp& x) {
+    asm("s_nop 2\n\t"
+        "v_mfma_f32_32x32x16_f16 %0, %1, %2, %0\n\t"
+        "v_mfma_f32_32x32x16_f16 %0, %3, %4, %0"
+        : "+a"(acc)
+        : "v"(dy.k[0]), "v"(x.k[0]), "v"(dy.k[1]), "v"(x.k[1]));
+}
+__device__ __forceinline__ void xdl_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
 
 // add one 32x32 dW tile (row = out 32*ot + (i&3)+8(i>>2)+4h, col = in 32*it + lane&31) into a
 // row-major fp32 LDS image of a (rows x cols) matrix; rows/cols are compile-time at every call, so
@@ -423,7 +437,7 @@ __device__ __forceinline__ void acc_tile(f32x16& reg, float* img, int rows, int 
         dw_acc(a, dy, x);
         dw_add32(img, a, ot, it, rows, cols, lane);
     } else {
-        dw_acc(reg, dy, x);
+        dw_acc_agpr(reg, dy, x);
     }
 }
 
@@ -641,6 +655,7 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
         // rgb part already is in limg)
         constexpr int N_IMG = RL ? N_XYZ_PARAMS : G::N_DW;
         static_assert((size_t)N_IMG * 4 + 64 <= C::IMG_OFF, "reduction image must fit the fragment area");
+        xdl_drain();
         __syncthreads();
         float* img = reinterpret_cast<float*>(smem);
         for (int i = threadIdx.x; i < N_IMG; i += blockDim.x) img[i] = 0.0f;
@@ -765,9 +780,10 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_wr2_kernel(
             relu_mask<0>(a, T.r2[o][0]); relu_mask<8>(a, T.r2[o][1]);
             const SOp d = to_s(lds, lane, pack8<0, false>(a), ID_P0, pack8<8, false>(a), ID_P16);
 #pragma unroll
-            for (int i = 0; i < MT; ++i) dw_acc(acc[o][i], d, x[i]);
+            for (int i = 0; i < MT; ++i) dw_acc_agpr(acc[o][i], d, x[i]);
         }
     }
+    xdl_drain();
     __syncthreads();
     float* img = reinterpret_cast<float*>(smem);
     for (int i = threadIdx.x; i < W * W; i += blockDim.x) img[i] = 0.0f;

@@ -13,6 +13,8 @@
 
 using namespace mfn;
 
+__global__ void mfn_bump_step_kernel(int32_t* s, int32_t* skip);  // adam.hip
+
 namespace {
 
 constexpr uint32_t PRIME1 = 2654435761u, PRIME2 = 805459861u;
@@ -399,6 +401,35 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_h2_kernel(const float* __re
     }
 }
 
+// Fixed-point gradient regions (shared memory, built by the whole block): the tables in address
+// order -- a level's own table, or a shared MixedFeature table counted once (the levels sharing it
+// have its offset) -- each with its table's 1/scale; lo_v[r] = first value index of region r.
+struct TableRegions {
+    float lvl_inv[MFN_MAX_LEVELS], inv_s[MFN_MAX_LEVELS];
+    int64_t lo_v[MFN_MAX_LEVELS + 1];
+    int n_reg;
+    __device__ void build(const mfnerf_grid_desc& D, const float* __restrict__ level_l1, int64_t total_vals) {
+        if (threadIdx.x < D.n_levels) {
+            const float sc = table_fixed_scale(D, level_l1, threadIdx.x);
+            lvl_inv[threadIdx.x] = sc > 0.0f ? 1.0f / sc : 0.0f;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int nr = 0;
+            int64_t last = -1;
+            for (int k = 0; k < D.n_levels; ++k) {
+                if ((int64_t)D.offset[k] <= last) continue;
+                last = D.offset[k];
+                inv_s[nr] = lvl_inv[k];
+                lo_v[nr++] = 2 * (int64_t)D.offset[k];
+            }
+            lo_v[nr] = total_vals;
+            n_reg = nr;
+        }
+        __syncthreads();
+    }
+};
+
 // grad[p] += sum_k priv[k][p]; priv[k][p] = 0 (ready for the next backward)
 __global__ __launch_bounds__(256) void fold_copies_kernel(float* __restrict__ priv, int64_t n, float* __restrict__ grad) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -423,27 +454,11 @@ __global__ __launch_bounds__(256) void fold_convert_kernel(float* __restrict__ g
                                                            const float* __restrict__ level_l1) {
     // table regions in address order -- a level's own table, or a shared MixedFeature table counted
     // once (the levels sharing it have its offset) -- each with its table's scale
-    __shared__ float lvl_inv[MFN_MAX_LEVELS], inv_s[MFN_MAX_LEVELS];
-    __shared__ int64_t lo_v[MFN_MAX_LEVELS + 1];
-    __shared__ int n_reg;
-    if (threadIdx.x < D.n_levels) {
-        const float sc = table_fixed_scale(D, level_l1, threadIdx.x);
-        lvl_inv[threadIdx.x] = sc > 0.0f ? 1.0f / sc : 0.0f;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int nr = 0;
-        int64_t last = -1;
-        for (int k = 0; k < D.n_levels; ++k) {
-            if ((int64_t)D.offset[k] <= last) continue;
-            last = D.offset[k];
-            inv_s[nr] = lvl_inv[k];
-            lo_v[nr++] = 2 * (int64_t)D.offset[k];
-        }
-        lo_v[nr] = total_vals;
-        n_reg = nr;
-    }
-    __syncthreads();
+    __shared__ TableRegions R;
+    R.build(D, level_l1, total_vals);
+    const float* inv_s = R.inv_s;
+    const int64_t* lo_v = R.lo_v;
+    const int n_reg = R.n_reg;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int l = 0;  // region of value i (i increases per thread: walk forward)
     for (int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; 4 * i4 < total_vals; i4 += stride) {
@@ -466,6 +481,72 @@ __global__ __launch_bounds__(256) void fold_convert_kernel(float* __restrict__ g
         }
         *reinterpret_cast<float4*>(grad + i) =
             make_float4((float)acc.x * is, (float)acc.y * is, (float)acc.z * is, (float)acc.w * is);
+    }
+}
+
+// fold_convert + Adam in one pass (the unsharded, collective-free step): g[0, off) are float
+// gradients (the MLPs), g[off, off + total_vals) the table's int32 fixed-point sums (the dense
+// prefix's in GRAD_COPIES private copies); each value is converted exactly as fold_convert_kernel
+// does, fed to the same Adam update as adam_kernel, and its gradient word (and copies) zeroed for
+// the next step -- one pass over the gradient instead of a convert pass + a read in Adam.
+__global__ __launch_bounds__(256) void adam_fixed_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v,
+                                                         __half* __restrict__ p16, int64_t n, int64_t off,
+                                                         int* __restrict__ priv, int64_t dense_vals,
+                                                         int64_t total_vals, const mfnerf_grid_desc D,
+                                                         const float* __restrict__ level_l1, float lr, float b1,
+                                                         float b2, float eps, const int32_t* __restrict__ step_dev,
+                                                         const float* __restrict__ lr_dev,
+                                                         const int32_t* __restrict__ skip) {
+    __shared__ TableRegions R;
+    R.build(D, level_l1, total_vals);
+    const bool skipped = skip && *skip;  // GradScaler: no update on a non-finite gradient, only the zeroing
+    const int st = *step_dev + 1;
+    if (lr_dev) lr = *lr_dev;
+    const float bc1 = 1.0f - powf(b1, (float)st);
+    const float bc2 = 1.0f - powf(b2, (float)st);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int l = 0;
+    for (int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; 4 * i4 < n; i4 += stride) {
+        const int64_t i = 4 * i4, j = i - off;  // off, dense_vals, region bounds: multiples of 4
+        float4 gg;
+        if (j < 0 || j >= total_vals) {
+            gg = reinterpret_cast<const float4*>(g)[i4];
+        } else {
+            while (l + 1 < R.n_reg && j >= R.lo_v[l + 1]) ++l;
+            const float is = R.inv_s[l];
+            int4 acc;
+            if (j < dense_vals) {
+                acc = make_int4(0, 0, 0, 0);
+#pragma unroll
+                for (int k = 0; k < GRAD_COPIES; ++k) {
+                    int4* q = reinterpret_cast<int4*>(priv + k * dense_vals + j);
+                    const int4 c = *q;
+                    acc.x += c.x; acc.y += c.y; acc.z += c.z; acc.w += c.w;
+                    *q = make_int4(0, 0, 0, 0);
+                }
+            } else {
+                acc = reinterpret_cast<const int4*>(g)[i4];
+            }
+            gg = make_float4((float)acc.x * is, (float)acc.y * is, (float)acc.z * is, (float)acc.w * is);
+        }
+        reinterpret_cast<float4*>(g)[i4] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (skipped) continue;
+        float4 pp = reinterpret_cast<float4*>(p)[i4];
+        float4 mm = reinterpret_cast<float4*>(m)[i4];
+        float4 vv = reinterpret_cast<float4*>(v)[i4];
+        mfn::adam_elem(pp.x, mm.x, vv.x, gg.x, b1, b2, eps, lr, bc1, bc2);
+        mfn::adam_elem(pp.y, mm.y, vv.y, gg.y, b1, b2, eps, lr, bc1, bc2);
+        mfn::adam_elem(pp.z, mm.z, vv.z, gg.z, b1, b2, eps, lr, bc1, bc2);
+        mfn::adam_elem(pp.w, mm.w, vv.w, gg.w, b1, b2, eps, lr, bc1, bc2);
+        reinterpret_cast<float4*>(p)[i4] = pp;
+        reinterpret_cast<float4*>(m)[i4] = mm;
+        reinterpret_cast<float4*>(v)[i4] = vv;
+        if (p16) {
+            __half2 a = __floats2half2_rn(pp.x, pp.y), b = __floats2half2_rn(pp.z, pp.w);
+            uint2 u; u.x = *reinterpret_cast<uint32_t*>(&a); u.y = *reinterpret_cast<uint32_t*>(&b);
+            reinterpret_cast<uint2*>(p16)[i4] = u;
+        }
     }
 }
 
@@ -590,6 +671,38 @@ int mfnerf_grid_encode_bw_finish(const mfnerf_grid_desc* desc, float* grad_table
                            (float*)workspace, nf, grad_table);
     }
     return mfn_check_launch("grid_encode_bw_finish");
+}
+
+int mfnerf_adam_step_fixed(float* params, float* grads, float* m, float* v, void* p_f16, int64_t n,
+                           int64_t table_offset, const mfnerf_grid_desc* desc, void* workspace,
+                           const float* level_l1, float lr, float beta1, float beta2, float eps,
+                           int32_t* step_dev, const float* lr_dev, int32_t* skip, mfnerf_stream_t stream) {
+    int st = check_desc(desc, "adam_step_fixed");
+    if (st) return st;
+    if (!params || !grads || !m || !v || !step_dev || !level_l1) {
+        mfn_set_error("adam_step_fixed: null pointer"); return MFN_ERR_INVALID;
+    }
+    if ((((uintptr_t)params) | ((uintptr_t)grads) | ((uintptr_t)m) | ((uintptr_t)v)) & 15 ||
+        (p_f16 && (((uintptr_t)p_f16) & 7))) {
+        mfn_set_error("adam_step_fixed: misaligned buffer"); return MFN_ERR_INVALID;
+    }
+    int64_t total = 0;
+    for (int l = 0; l < desc->n_levels; ++l) {
+        const int64_t e = 2 * ((int64_t)desc->offset[l] + desc->size[l]);
+        total = e > total ? e : total;
+    }
+    const int64_t dense = workspace ? dense_entries_of(desc) : 0;
+    if (n % 4 || table_offset % 4 || table_offset < 0 || table_offset + total > n) {
+        mfn_set_error("adam_step_fixed: n (%lld) and table_offset (%lld) must be multiples of 4 holding the table",
+                      (long long)n, (long long)table_offset);
+        return MFN_ERR_INVALID;
+    }
+    const int64_t want = div_up<int64_t>(n / 4, 256);
+    hipLaunchKernelGGL(adam_fixed_kernel, dim3((unsigned)(want < 4096 ? (want < 1 ? 1 : want) : 4096)), dim3(256), 0,
+                       stream, params, grads, m, v, (__half*)p_f16, n, table_offset, (int*)workspace, 2 * dense,
+                       total, *desc, level_l1, lr, beta1, beta2, eps, step_dev, lr_dev, skip);
+    hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, skip);
+    return mfn_check_launch("adam_step_fixed");
 }
 
 int mfnerf_grid_encode_bw(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,

@@ -406,6 +406,16 @@ class TrainStep:
              hi - lo, float(c.lr), 0.9, 0.999, c.eps, 1.0, 0, ptr(self.step_dev), ptr(self.lr_dev),
              ptr(self.finite_status) if c.skip_nonfinite else None, int(zero_grads), stream())
 
+    def _finish_update(self):
+        """Unsharded, no exchange, fixed-point table gradient: the finish (convert) and Adam in one
+        pass (mfnerf_adam_step_fixed), then the MLP weight repack."""
+        c = self.cfg
+        call("mfnerf_adam_step_fixed", ptr(self.params), ptr(self.grads), ptr(self.m), ptr(self.v), ptr(self.p16),
+             self.n_alloc, self.off_table, self.desc, ptr(self.parts[0].grid_ws), ptr(self._level_l1),
+             float(c.lr), 0.9, 0.999, c.eps, ptr(self.step_dev), ptr(self.lr_dev),
+             ptr(self.finite_status) if c.skip_nonfinite else None, stream())
+        self._pack()
+
     def _update(self):
         """Adam over the flat params (+ fp16 mirror, + zeroing the gradient for the next step) +
         MLP weight repack (unsharded)."""
@@ -543,7 +553,8 @@ class TrainStep:
         else:
             self.graphs["update"] = cap(self._update)
             if P == 1:  # no collective between them: one graph, one launch gap less
-                self.graphs["finish_update"] = cap(lambda: (self._grid_finish(0), self._update()))
+                self.graphs["finish_update"] = cap(self._finish_update if self._fixed() else
+                                                   lambda: (self._grid_finish(0), self._update()))
         torch.cuda.synchronize()
         # the next step's march runs beside this step's grid_bw scatter, whose 4096 workgroups would
         # otherwise take every dispatch slot first (the march's small kernels then finish after the

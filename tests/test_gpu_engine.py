@@ -110,3 +110,46 @@ def test_distortion_loss_in_the_fused_step(gpu, oracle):
         assert torch.allclose(cpu(t.dL_dws[:n]), g, rtol=1e-4, atol=1e-9)
     # same params, noise and batch in both steps: the losses differ by exactly the distortion term
     assert abs(float(st.loss_sum) - float(ref.loss_sum) - lam * dist_total / 512) <= 1e-5 * float(st.loss_sum)
+
+
+@pytest.mark.parametrize("kw", [{}, {"grid": "MixedFeature", "N_tables": 8, "rgb_width": 128}],
+                         ids=["hash-rgb64", "mixedfeature-rgb128"])
+@pytest.mark.parametrize("skip", [False, True])
+def test_fused_convert_adam_matches_finish_then_adam(gpu, kw, skip):
+    """mfnerf_adam_step_fixed (the graph-replayed tail of an unsharded step) == the finish call
+    (fixed-point -> float, private copies folded) followed by mfnerf_adam_step, bit for bit: params,
+    m, v, the fp16 mirror, Adam's step counter, and the zeroed gradient and private copies -- also on a
+    step skipped for a non-finite gradient."""
+    st = _make(gpu, 1, **kw)
+    batches = st.make_batches(2, seed=5)
+    st.run(batches[0])  # m, v non-zero
+    mb, nomark = st.mbuf[0], (lambda name: None)
+    st._use(mb)
+    st._march(batches[1], mb, nomark)
+    st._chain(batches[1], mb, 0, nomark)
+    st._grid_bw(mb, 0)
+    if skip:
+        st.finite_status[0] = 1
+    torch.cuda.synchronize()
+    names = ("params", "grads", "m", "v", "p16", "step_dev", "finite_status")
+    ws = st.parts[0].grid_ws
+    snap = {k: getattr(st, k).clone() for k in names}
+    snap_ws = ws.clone()
+    assert int((snap["grads"][st.off_table:] != 0).sum()) > 1000 and int((snap_ws != 0).sum()) > 0
+
+    st._grid_finish(0)
+    st._update()
+    torch.cuda.synchronize()
+    ref = {k: getattr(st, k).clone() for k in names}
+    for k in names:
+        getattr(st, k).copy_(snap[k])
+    ws.copy_(snap_ws)
+    st._finish_update()
+    torch.cuda.synchronize()
+    for k in names:
+        assert torch.equal(getattr(st, k), ref[k]), k
+    assert not bool(ws.any()) and not bool(st.grads.any())
+    if skip:
+        assert torch.equal(st.params, snap["params"]) and int(st.finite_status[1]) == int(snap["finite_status"][1]) + 1
+    else:
+        assert not torch.equal(st.params, snap["params"])
