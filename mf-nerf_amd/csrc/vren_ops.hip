@@ -354,18 +354,29 @@ __device__ __forceinline__ float wave_incl_scan(float v, int lane) {
 __device__ __forceinline__ float wave_sum(float v) { return readlane_f(wave_incl_scan(v, 0), 63); }
 
 // Sequential T over the chunk: returns this lane's T before its sample; T_run is advanced; *stop is
-// the first lane whose post-update T <= thr (64 if none).
+// the first lane whose post-update T <= thr (64 if none).  The reference's order is kept exactly:
+// T_j = fl(T_{j-1} * fl(1 - a_{j-1})), so T, termination and total_samples are bit-identical to its
+// sequential loop.  The chain is propagated one lane per step with a whole-wave DPP shift
+// (wave_shr:1): after k steps lanes 0..k hold their final T, so n_valid-1 steps of one shifted
+// multiply replace n_valid serial readlane/multiply/compare/branch rounds -- the long rays' chains
+// (hundreds of samples) were this kernel's critical path.
 __device__ __forceinline__ float t_chain(float a, float& T_run, float thr, int lane, int n_valid, int* stop) {
-    float myT = T_run;
-    int st = 64;
-    for (int j = 0; j < n_valid; ++j) {
-        const float aj = readlane_f(a, j);
-        if (lane == j) myT = T_run;
-        T_run *= 1.0f - aj;
-        if (T_run <= thr) { st = j; break; }
-    }
+    constexpr int WAVE_SHR1 = 0x138;
+    const float b = 1.0f - a;  // lanes past n_valid: a = 0, b = 1
+    // bs[j] = b[j-1], bs[0] = 1 (T_0 = T_run * 1 exactly)
+    const float bs = __int_as_float(
+        __builtin_amdgcn_update_dpp(__float_as_int(1.0f), __float_as_int(b), WAVE_SHR1, 0xF, 0xF, false));
+    const int t0 = __float_as_int(T_run);
+    float X = T_run;
+    const int nv = __builtin_amdgcn_readfirstlane(n_valid);  // wave-uniform: a scalar loop
+    for (int k = 1; k < nv; ++k)
+        X = __int_as_float(__builtin_amdgcn_update_dpp(t0, __float_as_int(X), WAVE_SHR1, 0xF, 0xF, false)) * bs;
+    const float Ta = X * b;  // T after this lane's sample
+    const uint64_t hit = __ballot(lane < n_valid && Ta <= thr);
+    const int st = hit ? (int)__builtin_ctzll(hit) : 64;
+    T_run = readlane_f(Ta, st < 64 ? st : n_valid - 1);
     *stop = st;
-    return myT;
+    return X;
 }
 
 __global__ __launch_bounds__(256) void composite_fw_wave_kernel(
