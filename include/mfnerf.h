@@ -252,6 +252,15 @@ int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float
                     float* grad_xyz, float* grad_rgb, void* workspace, int32_t* nonfinite, float* level_l1,
                     mfnerf_stream_t stream);
 
+/* grad_xyz = grad_rgb = NULL in mfnerf_field_bw defers the weight-gradient fold: the per-block
+ * partial sums stay in workspace (dL_dfeat, level_l1 and the data-gradient part of the non-finite
+ * flag are complete when field_bw returns) and this call adds them into grad_xyz / grad_rgb in the
+ * same fixed order (bit-identical to the undeferred call), raising nonfinite on an inf/nan weight
+ * gradient.  The training step runs it on a second stream beside the table-gradient scatter, which
+ * needs only dL_dfeat.  Part of the tcnn backward (networks.py:96-126) split for scheduling. */
+int mfnerf_field_bw_reduce(int rgb_width, const void* workspace, float* grad_xyz, float* grad_rgb,
+                           int32_t* nonfinite, mfnerf_stream_t stream);
+
 /* Debug: one v_mfma_f32_32x32x16_f16 with A (32x16) and B (16x32) f16 row-major -> D (32x32) f32,
  * through the lane maps the field kernels assume (pins them on the device). */
 int mfnerf_debug_mfma_probe(const void* A, const void* B, float* D, mfnerf_stream_t stream);

@@ -671,24 +671,30 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
                 if (r == 0) { atomicAdd(l1_part + 4 * g + 2 * h, a); atomicAdd(l1_part + 4 * g + 2 * h + 1, b); }
             }
         }
+        // the waves add their tiles one after another (each address gets one add per wave), so the
+        // block's sum -- hence the weight gradient -- has a fixed order: bit-reproducible
+        for (int wv = 0; wv < NW; ++wv) {
+            if ((int)(threadIdx.x >> 6) == wv) {
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
-            dw_add32(img, dw1[a], a, 0, 64, 32, lane);
-            dw_add32(img + 64 * 32, dw2[a], 0, a, 16, 64, lane);
-        }
-        if constexpr (!RL) {
+                for (int a = 0; a < 2; ++a) {
+                    dw_add32(img, dw1[a], a, 0, 64, 32, lane);
+                    dw_add32(img + 64 * 32, dw2[a], 0, a, 16, 64, lane);
+                }
+                if constexpr (!RL) {
 #pragma unroll
-            for (int a = 0; a < MT; ++a) {
-                dw_add32(img + oR1, dwr1[a], a, 0, W, 32, lane);
-                dw_add32(img + oR3, dwr3[a], 0, a, 16, W, lane);
+                    for (int a = 0; a < MT; ++a) {
+                        dw_add32(img + oR1, dwr1[a], a, 0, W, 32, lane);
+                        dw_add32(img + oR3, dwr3[a], 0, a, 16, W, lane);
+                    }
+#pragma unroll
+                    for (int o = 0; o < R2; ++o)
+#pragma unroll
+                        for (int i = 0; i < R2; ++i)
+                            if constexpr (!C::R2_SPLIT) dw_add32(img + oR2, dwr2[o][i], o, i, W, W, lane);
+                }
             }
-#pragma unroll
-            for (int o = 0; o < R2; ++o)
-#pragma unroll
-                for (int i = 0; i < R2; ++i)
-                    if constexpr (!C::R2_SPLIT) dw_add32(img + oR2, dwr2[o][i], o, i, W, W, lane);
+            __syncthreads();
         }
-        __syncthreads();
         for (int i = threadIdx.x; i < G::N_DW; i += blockDim.x) {
             if (C::R2_SPLIT && i >= oR2 && i < oR3) continue;  // written by field_bw_wr2_kernel
             float v;
@@ -788,11 +794,15 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_wr2_kernel(
     float* img = reinterpret_cast<float*>(smem);
     for (int i = threadIdx.x; i < W * W; i += blockDim.x) img[i] = 0.0f;
     __syncthreads();
+    for (int wv = 0; wv < FIELD_BLOCK / 64; ++wv) {  // fixed wave order (see field_bw_kernel)
+        if ((int)(threadIdx.x >> 6) == wv) {
 #pragma unroll
-    for (int o = 0; o < MT; ++o)
+            for (int o = 0; o < MT; ++o)
 #pragma unroll
-        for (int i = 0; i < MT; ++i) dw_add32(img, acc[o][i], o, i, W, W, lane);
-    __syncthreads();
+                for (int i = 0; i < MT; ++i) dw_add32(img, acc[o][i], o, i, W, W, lane);
+        }
+        __syncthreads();
+    }
     float* row = slab + (int64_t)blockIdx.x * G::N_DW + oR2;
     for (int i = threadIdx.x; i < W * W; i += blockDim.x) row[i] = img[i] * invS;
 }
@@ -802,20 +812,44 @@ template <int W>
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int rows,
                                                           float* __restrict__ gx, float* __restrict__ gr,
                                                           int32_t* __restrict__ nonfinite) {
+    // 64 parameters per block as 16 float4 columns x 16 row groups; each thread sums its rows
+    // (rows/16, all loads in flight) and the 16 partials are added in a fixed tree order
     constexpr int N_DW = Geo<W>::N_DW;
-    __shared__ float part[4][64];
-    const int l = threadIdx.x & 63, rg = threadIdx.x >> 6;
-    const int p = blockIdx.x * 64 + l;
-    float acc = 0.0f;
-    if (p < N_DW)
-        for (int b = rg; b < rows; b += 4) acc += slab[(int64_t)b * N_DW + p];
-    part[rg][l] = acc;
+    static_assert(N_DW % 4 == 0 && N_XYZ_PARAMS % 4 == 0, "float4 columns");
+    __shared__ float4 part[16][16];
+    const int c = threadIdx.x & 15, rg = threadIdx.x >> 4;
+    const int p = blockIdx.x * 64 + 4 * c;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p < N_DW) {
+        const float4* src = reinterpret_cast<const float4*>(slab + p);
+        constexpr int RS = N_DW / 4;  // row stride in float4
+        for (int b = rg; b < rows; b += 16) {
+            const float4 v = src[(int64_t)b * RS];
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+    }
+    part[rg][c] = acc;
     __syncthreads();
     if (rg == 0 && p < N_DW) {
-        const float v = (part[0][l] + part[1][l]) + (part[2][l] + part[3][l]);
-        if (p < N_XYZ_PARAMS) gx[p] += v;
-        else gr[p - N_XYZ_PARAMS] += v;
-        if (nonfinite && !isfinite(v)) atomicOr(nonfinite, 1);
+        float4 t[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) t[k] = part[k][c];
+#pragma unroll
+        for (int w = 8; w > 0; w >>= 1)
+#pragma unroll
+            for (int k = 0; k < w; ++k) {
+                t[k].x += t[k + w].x; t[k].y += t[k + w].y; t[k].z += t[k + w].z; t[k].w += t[k + w].w;
+            }
+        const float v[4] = {t[0].x, t[0].y, t[0].z, t[0].w};
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q = p + k;
+            if (q < N_XYZ_PARAMS) gx[q] += v[k];
+            else gr[q - N_XYZ_PARAMS] += v[k];
+            bad |= !isfinite(v[k]);
+        }
+        if (nonfinite && bad) atomicOr(nonfinite, 1);
     }
 }
 
@@ -892,8 +926,9 @@ int launch_bw(const void* feat, int64_t ps, const float* dirs, int64_t n, const 
         hipLaunchKernelGGL(field_bw_wr2_kernel<W>, dim3(BW_BLOCKS), dim3(FIELD_BLOCK),
                            (size_t)(Geo<W>::B4 + 4) * FRAG_HALFS * 2, stream, (const _Float16*)feat, ps, dirs, n, n_dev,
                            (const _Float16*)packed, dL_drgb, grad_scale, (float*)workspace);
-    hipLaunchKernelGGL(slab_reduce_kernel<W>, dim3((Geo<W>::N_DW + 63) / 64), dim3(256), 0, stream,
-                       (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
+    if (grad_xyz)  // else deferred: mfnerf_field_bw_reduce folds the slab later
+        hipLaunchKernelGGL(slab_reduce_kernel<W>, dim3((Geo<W>::N_DW + 63) / 64), dim3(256), 0, stream,
+                           (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
     return MFN_OK;
 }
 
@@ -958,7 +993,7 @@ int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float
         mfn_set_error("field_bw: bad size, plane stride or grad_scale"); return MFN_ERR_INVALID;
     }
     if (n == 0) return MFN_OK;
-    if (!feat_f16 || !dirs || !packed || !dL_dsigma || !dL_drgb || !dL_dfeat || !grad_xyz || !grad_rgb || !workspace) {
+    if (!feat_f16 || !dirs || !packed || !dL_dsigma || !dL_drgb || !dL_dfeat || !workspace || (!grad_xyz != !grad_rgb)) {
         mfn_set_error("field_bw: null pointer"); return MFN_ERR_INVALID;
     }
     int st;
@@ -973,6 +1008,19 @@ int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float
                               dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
     if (st != MFN_OK) return st;
     return mfn_check_launch("field_bw");
+}
+
+int mfnerf_field_bw_reduce(int rgb_width, const void* workspace, float* grad_xyz, float* grad_rgb,
+                           int32_t* nonfinite, mfnerf_stream_t stream) {
+    if (!width_ok(rgb_width)) return bad_width(rgb_width);
+    if (!workspace || !grad_xyz || !grad_rgb) { mfn_set_error("field_bw_reduce: null pointer"); return MFN_ERR_INVALID; }
+    if (rgb_width == 64)
+        hipLaunchKernelGGL(slab_reduce_kernel<64>, dim3((Geo<64>::N_DW + 63) / 64), dim3(256), 0, stream,
+                           (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
+    else
+        hipLaunchKernelGGL(slab_reduce_kernel<128>, dim3((Geo<128>::N_DW + 63) / 64), dim3(256), 0, stream,
+                           (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
+    return mfn_check_launch("field_bw_reduce");
 }
 
 int mfnerf_debug_mfma_probe(const void* A, const void* B, float* D, mfnerf_stream_t stream) {

@@ -81,6 +81,7 @@ SIGNATURES = {
                                      _P]),
     "mfnerf_adam_step": (_I, [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _I, _P]),
     "mfnerf_adam_step_fixed": (_I, [_P, _P, _P, _P, _P, _I64, _I64, ctypes.POINTER(GridDesc), _P, _P, _F, _F, _F, _F, _P, _P, _P, _P]),
+    "mfnerf_field_bw_reduce": (_I, [_I, _P, _P, _P, _P, _P]),
     "mfnerf_check_finite": (_I, [_P, _I64, _P, _P]),
     "mfnerf_flag_to_shards": (_I, [_P, _I64, _I64, _P, _P]),
     "mfnerf_flag_from_shard": (_I, [_P, _P, _P]),

@@ -48,6 +48,10 @@ def test_pipelined_replay_matches_eager(gpu, oracle, parts):
         assert torch.equal(g["noise"], r["noise"]), f"step {k}: noise stream differs"
         assert g["n"] == r["n"] and torch.equal(g["rays_a"], r["rays_a"]) and torch.equal(g["xyzs"], r["xyzs"])
         assert abs(g["loss"] - r["loss"]) <= 1e-3 * abs(r["loss"]), (k, g["loss"], r["loss"])
+    if parts == 1:
+        # one part: fixed-point table gradient, fused convert+Adam tail, MLP fold on a second stream --
+        # all order-fixed, so the replayed training is bit-identical to the eager one
+        assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(a.p16, b.p16)
     # the march each replay used is the reference's march of that batch with that noise
     k = K - 1
     o, d = batches[k].rays_o.cpu(), batches[k].rays_d.cpu()
