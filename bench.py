@@ -247,6 +247,7 @@ def main():
             ev = []
             run_step(step, batches[i % len(batches)], world, ev)
             eager_ev.append(ev)
+    host_s = time.time() - t0  # the host's issue time for the K steps (GPU-bound when well below elapsed)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -293,7 +294,7 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
                          "bytes_per_launch": round(dom_bytes)},
-            "graph": use_graph,
+            "graph": use_graph, "host_issue_ms_per_step": round(host_s / args.steps * 1e3, 4),
             "grid_bw_ms": round(grid_bw_ms, 4),
             "eager_stage_ms": {k: round(v, 4) for k, v in eager_stage_ms.items()},
             "density_update_ms": round(density_ms, 3),

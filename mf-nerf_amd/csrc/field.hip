@@ -419,12 +419,16 @@ __device__ __forceinline__ void xdl_drain() { asm volatile("s_nop 7\n\ts_nop 7\n
 // add one 32x32 dW tile (row = out 32*ot + (i&3)+8(i>>2)+4h, col = in 32*it + lane&31) into a
 // row-major fp32 LDS image of a (rows x cols) matrix; rows/cols are compile-time at every call, so
 // the register rows that can never be in range are dropped statically
-__device__ __forceinline__ void dw_add32(float* img, const f32x16& a, int ot, int it, int rows, int cols, int lane) {
+__device__ __forceinline__ void dw_add32(float* img, const f32x16& a, int ot, int it, int rows, int cols, int lane,
+                                         bool store = false) {
     const int col = 32 * it + (lane & 31), h = lane >> 5;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int row = 32 * ot + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (row < rows && col < cols) atomicAdd(img + row * cols + col, a[i]);
+        if (row < rows && col < cols) {
+            if (store) img[row * cols + col] = a[i];  // the first wave of a fixed-order sum
+            else atomicAdd(img + row * cols + col, a[i]);
+        }
     }
 }
 
@@ -657,8 +661,7 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
         static_assert((size_t)N_IMG * 4 + 64 <= C::IMG_OFF, "reduction image must fit the fragment area");
         xdl_drain();
         __syncthreads();
-        float* img = reinterpret_cast<float*>(smem);
-        for (int i = threadIdx.x; i < N_IMG; i += blockDim.x) img[i] = 0.0f;
+        float* img = reinterpret_cast<float*>(smem);  // wave 0 stores every entry first (no zeroing)
         float* l1_part = img + N_IMG;  // 16 floats after the image
         if (threadIdx.x < 16) l1_part[threadIdx.x] = 0.0f;
         __syncthreads();
@@ -675,22 +678,23 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
         // block's sum -- hence the weight gradient -- has a fixed order: bit-reproducible
         for (int wv = 0; wv < NW; ++wv) {
             if ((int)(threadIdx.x >> 6) == wv) {
+                const bool st = wv == 0;
 #pragma unroll
                 for (int a = 0; a < 2; ++a) {
-                    dw_add32(img, dw1[a], a, 0, 64, 32, lane);
-                    dw_add32(img + 64 * 32, dw2[a], 0, a, 16, 64, lane);
+                    dw_add32(img, dw1[a], a, 0, 64, 32, lane, st);
+                    dw_add32(img + 64 * 32, dw2[a], 0, a, 16, 64, lane, st);
                 }
                 if constexpr (!RL) {
 #pragma unroll
                     for (int a = 0; a < MT; ++a) {
-                        dw_add32(img + oR1, dwr1[a], a, 0, W, 32, lane);
-                        dw_add32(img + oR3, dwr3[a], 0, a, 16, W, lane);
+                        dw_add32(img + oR1, dwr1[a], a, 0, W, 32, lane, st);
+                        dw_add32(img + oR3, dwr3[a], 0, a, 16, W, lane, st);
                     }
 #pragma unroll
                     for (int o = 0; o < R2; ++o)
 #pragma unroll
                         for (int i = 0; i < R2; ++i)
-                            if constexpr (!C::R2_SPLIT) dw_add32(img + oR2, dwr2[o][i], o, i, W, W, lane);
+                            if constexpr (!C::R2_SPLIT) dw_add32(img + oR2, dwr2[o][i], o, i, W, W, lane, st);
                 }
             }
             __syncthreads();

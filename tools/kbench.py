@@ -67,6 +67,7 @@ def main():
                                      step.x_range, step.desc, ptr(t.dfeat), ptr(grad_h2), ptr(priv_h2), 2048.0, s()),
         "check": lambda: call("mfnerf_check_finite", ptr(step.grads), step.grads.numel(), ptr(step.finite_status), s()),
         "adam": lambda: step._adam(step.grads, 0, step.n_alloc, False),
+        "adam_fixed": step._finish_update,  # fused convert + Adam + repack (state changes: timing only)
         "pack": step._pack,
         "march": lambda: step._march(batch, mb, lambda _n: None),
     }
