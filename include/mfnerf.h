@@ -340,11 +340,12 @@ int mfnerf_adam_step(float* params, float* grads, float* m, float* v, void* p_f1
  * dense prefix's in workspace's private copies.  Each value is converted exactly as the finish call
  * converts it and updated exactly as mfnerf_adam_step updates it (step_dev required, grad_scale 1);
  * grads and the private copies are zeroed (also on a skipped step).  n and table_offset: multiples
- * of 4, the table inside [table_offset, n).  Replaces the two calls (and one pass over the gradient)
+ * of 4, the table inside [table_offset, n).  level_l1 is zeroed after use, ready for the next step's
+ * mfnerf_field_bw accumulation.  Replaces the two calls (and one pass over the gradient)
  * the reference makes as tcnn's backward + apex FusedAdam (train.py:136). */
 int mfnerf_adam_step_fixed(float* params, float* grads, float* m, float* v, void* p_f16, int64_t n,
                            int64_t table_offset, const mfnerf_grid_desc* desc, void* workspace,
-                           const float* level_l1, float lr, float beta1, float beta2, float eps,
+                           float* level_l1, float lr, float beta1, float beta2, float eps,
                            int32_t* step_dev, const float* lr_dev, int32_t* skip, mfnerf_stream_t stream);
 
 /* status[0] (device i32) = 1 if any of x (n f32, 16-byte aligned) is inf/nan, else 0 (a full scan;

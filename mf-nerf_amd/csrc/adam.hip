@@ -58,9 +58,10 @@ __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ g, float*
 // next step's producers
 }  // namespace
 
-__global__ void mfn_bump_step_kernel(int32_t* s, int32_t* skip) {
+__global__ void mfn_bump_step_kernel(int32_t* s, int32_t* skip, float* zero, int nz) {
     if (skip && skip[0]) { skip[1] += 1; skip[0] = 0; }
     else if (s) *s += 1;
+    for (int k = 0; k < nz; ++k) zero[k] = 0.0f;  // a small accumulator, ready for the next step
 }
 
 namespace {
@@ -123,7 +124,7 @@ extern "C" int mfnerf_adam_step(float* params, float* grads, float* m, float* v,
     const unsigned blocks = (unsigned)(want < 4096 ? (want < 1 ? 1 : want) : 4096);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(threads), 0, stream, params, grads, m, v, (__half*)p_f16, n, lr,
                        beta1, beta2, eps, grad_scale, step, step_dev, lr_dev, skip, zero_grads);
-    if (step_dev || skip) hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, skip);
+    if (step_dev || skip) hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, skip, (float*)nullptr, 0);
     return mfn_check_launch("adam_step");
 }
 

@@ -13,7 +13,7 @@
 
 using namespace mfn;
 
-__global__ void mfn_bump_step_kernel(int32_t* s, int32_t* skip);  // adam.hip
+__global__ void mfn_bump_step_kernel(int32_t* s, int32_t* skip, float* zero, int nz);  // adam.hip
 
 namespace {
 
@@ -122,6 +122,49 @@ __device__ __forceinline__ int level_group(int l) {
     return q < 8 ? q : 15 - q;
 }
 
+// one (sample, level) of the planar forward
+__device__ __forceinline__ void planar_level(const mfnerf_grid_desc& D, const __half2* __restrict__ table,
+                                             __half2* __restrict__ out, int64_t plane_stride, int64_t i, int l,
+                                             float x, float y, float z) {
+    const LevelGeo L = level_geo(D.scale[l], x, y, z);
+    const __half2* tab = table + D.offset[l];
+    const uint32_t size = D.size[l], res = D.res[l];
+    const bool dense = D.table_kind[l] == 0 && (uint64_t)res * res * res <= size;
+    const bool pow2 = (size & (size - 1)) == 0;
+    __half2 v[8];
+    // The two x-corners of a (y,z) row are adjacent entries -- dense levels: idx+1 (one
+    // unaligned 8-B load unless it wraps past the table end); hashed power-of-two levels
+    // with even x: idx^1 (one aligned 8-B load) -- so each row costs one gather lane
+    // instead of two (the kernel is bound by per-lane gather addresses).
+#pragma unroll
+    for (int yz = 0; yz < 4; ++yz) {
+        const uint32_t gy = L.g[1] + (yz & 1), gz = L.g[2] + (yz >> 1);
+        const uint32_t i0 = corner_index(D, l, L.g[0], gy, gz);
+        if (dense && i0 + 1 < size) {
+            const uint2 u = *reinterpret_cast<const uint2*>(tab + i0);
+            v[2 * yz] = *reinterpret_cast<const __half2*>(&u.x);
+            v[2 * yz + 1] = *reinterpret_cast<const __half2*>(&u.y);
+        } else if (!dense && pow2 && D.table_kind[l] == 0 && (L.g[0] & 1) == 0) {
+            const uint2 u = *reinterpret_cast<const uint2*>(tab + (i0 & ~1u));
+            const bool lo = (i0 & 1) == 0;
+            v[2 * yz] = *reinterpret_cast<const __half2*>(lo ? &u.x : &u.y);
+            v[2 * yz + 1] = *reinterpret_cast<const __half2*>(lo ? &u.y : &u.x);
+        } else {
+            v[2 * yz] = tab[i0];
+            v[2 * yz + 1] = tab[corner_index(D, l, L.g[0] + 1, gy, gz)];
+        }
+    }
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const float w = corner_weight(L, c);
+        const float2 f = __half22float2(v[c]);
+        a0 = fmaf(w, f.x, a0);
+        a1 = fmaf(w, f.y, a1);
+    }
+    out[(int64_t)l * plane_stride + i] = __floats2half2_rn(a0, a1);
+}
+
 __global__ __launch_bounds__(ENC_BLOCK) void grid_fw_planar_kernel(const float* __restrict__ X, int64_t n,
                                                                     const int32_t* __restrict__ n_dev, float x_min,
                                                                     float x_range, const mfnerf_grid_desc D,
@@ -129,52 +172,17 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_fw_planar_kernel(const float* 
                                                                     __half2* __restrict__ out, int64_t plane_stride) {
     const int grp = blockIdx.x & 7;
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
+    const int nj = 2 * ((D.n_levels + 15) >> 4);
     const int64_t stride = (int64_t)(gridDim.x >> 3) * ENC_BLOCK;
     for (int64_t i = (int64_t)(blockIdx.x >> 3) * ENC_BLOCK + threadIdx.x; i < nn; i += stride) {
         const float x = (X[3 * i] - x_min) / x_range;
         const float y = (X[3 * i + 1] - x_min) / x_range;
         const float z = (X[3 * i + 2] - x_min) / x_range;
         // this group's levels, visited directly: 16m + grp and 16m + 15 - grp
-        for (int j = 0; j < 2 * ((D.n_levels + 15) >> 4); ++j) {
+        for (int j = 0; j < nj; ++j) {
             const int l = 16 * (j >> 1) + ((j & 1) ? 15 - grp : grp);
             if (l >= D.n_levels) continue;
-            const LevelGeo L = level_geo(D.scale[l], x, y, z);
-            const __half2* tab = table + D.offset[l];
-            const uint32_t size = D.size[l], res = D.res[l];
-            const bool dense = D.table_kind[l] == 0 && (uint64_t)res * res * res <= size;
-            const bool pow2 = (size & (size - 1)) == 0;
-            __half2 v[8];
-            // The two x-corners of a (y,z) row are adjacent entries -- dense levels: idx+1 (one
-            // unaligned 8-B load unless it wraps past the table end); hashed power-of-two levels
-            // with even x: idx^1 (one aligned 8-B load) -- so each row costs one gather lane
-            // instead of two (the kernel is bound by per-lane gather addresses).
-#pragma unroll
-            for (int yz = 0; yz < 4; ++yz) {
-                const uint32_t gy = L.g[1] + (yz & 1), gz = L.g[2] + (yz >> 1);
-                const uint32_t i0 = corner_index(D, l, L.g[0], gy, gz);
-                if (dense && i0 + 1 < size) {
-                    const uint2 u = *reinterpret_cast<const uint2*>(tab + i0);
-                    v[2 * yz] = *reinterpret_cast<const __half2*>(&u.x);
-                    v[2 * yz + 1] = *reinterpret_cast<const __half2*>(&u.y);
-                } else if (!dense && pow2 && D.table_kind[l] == 0 && (L.g[0] & 1) == 0) {
-                    const uint2 u = *reinterpret_cast<const uint2*>(tab + (i0 & ~1u));
-                    const bool lo = (i0 & 1) == 0;
-                    v[2 * yz] = *reinterpret_cast<const __half2*>(lo ? &u.x : &u.y);
-                    v[2 * yz + 1] = *reinterpret_cast<const __half2*>(lo ? &u.y : &u.x);
-                } else {
-                    v[2 * yz] = tab[i0];
-                    v[2 * yz + 1] = tab[corner_index(D, l, L.g[0] + 1, gy, gz)];
-                }
-            }
-            float a0 = 0.f, a1 = 0.f;
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const float w = corner_weight(L, c);
-                const float2 f = __half22float2(v[c]);
-                a0 = fmaf(w, f.x, a0);
-                a1 = fmaf(w, f.y, a1);
-            }
-            out[(int64_t)l * plane_stride + i] = __floats2half2_rn(a0, a1);
+            planar_level(D, table, out, plane_stride, i, l, x, y, z);
         }
     }
 }
@@ -675,7 +683,7 @@ int mfnerf_grid_encode_bw_finish(const mfnerf_grid_desc* desc, float* grad_table
 
 int mfnerf_adam_step_fixed(float* params, float* grads, float* m, float* v, void* p_f16, int64_t n,
                            int64_t table_offset, const mfnerf_grid_desc* desc, void* workspace,
-                           const float* level_l1, float lr, float beta1, float beta2, float eps,
+                           float* level_l1, float lr, float beta1, float beta2, float eps,
                            int32_t* step_dev, const float* lr_dev, int32_t* skip, mfnerf_stream_t stream) {
     int st = check_desc(desc, "adam_step_fixed");
     if (st) return st;
@@ -701,7 +709,7 @@ int mfnerf_adam_step_fixed(float* params, float* grads, float* m, float* v, void
     hipLaunchKernelGGL(adam_fixed_kernel, dim3((unsigned)(want < 4096 ? (want < 1 ? 1 : want) : 4096)), dim3(256), 0,
                        stream, params, grads, m, v, (__half*)p_f16, n, table_offset, (int*)workspace, 2 * dense,
                        total, *desc, level_l1, lr, beta1, beta2, eps, step_dev, lr_dev, skip);
-    hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, skip);
+    hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, skip, level_l1, desc->n_levels);
     return mfn_check_launch("adam_step_fixed");
 }
 

@@ -328,8 +328,6 @@ class TrainStep:
         t, m = self.parts[q], mb.part[q]
         Np, cap = self.Np, self.cap_p
         if q == 0:
-            if self._fixed():
-                self._level_l1.zero_()  # accumulated by field_bw
             if self.shard is not None:
                 self.grads.zero_()  # unsharded: the previous Adam pass left it zero
             if c.lambda_distortion > 0:
@@ -392,6 +390,8 @@ class TrainStep:
         """Fold part q's private copies of the coarse levels / convert the fixed-point sums."""
         call("mfnerf_grid_encode_bw_finish", self.desc, ptr(self.grads[self.off_table:]), ptr(self.parts[q].grid_ws),
              ptr(self._level_l1) if self._fixed() else None, stream())
+        if self._fixed():
+            self._level_l1.zero_()  # field_bw accumulates it; zeroed once used (also by adam_step_fixed)
 
     def _reduce_parts(self):
         """Fold parts 1.. MLP weight grads into grads (the table part is already shared)."""

@@ -135,11 +135,12 @@ def test_fused_convert_adam_matches_finish_then_adam(gpu, kw, skip):
     if skip:
         st.finite_status[0] = 1
     torch.cuda.synchronize()
-    names = ("params", "grads", "m", "v", "p16", "step_dev", "finite_status")
+    names = ("params", "grads", "m", "v", "p16", "step_dev", "finite_status", "_level_l1")
     ws = st.parts[0].grid_ws
     snap = {k: getattr(st, k).clone() for k in names}
     snap_ws = ws.clone()
     assert int((snap["grads"][st.off_table:] != 0).sum()) > 1000 and int((snap_ws != 0).sum()) > 0
+    assert bool((snap["_level_l1"] > 0).all())
 
     st._grid_finish(0)
     st._update()
