@@ -321,13 +321,15 @@ class DeviceDataset:
 # ---------------------------------------------------------------------------- analytic scene
 class BallScene:
     """Opaque coloured balls inside [-0.5, 0.5]^3; render(o, d) = colour of the first ball hit,
-    white where nothing is hit (the synthetic-scene background of rendering.py:153-155)."""
+    white where nothing is hit (the synthetic-scene background of rendering.py:153-155).  With
+    texture_freq > 0 each ball's colour carries a world-space sin(f x) sin(f y) sin(f z) pattern."""
 
     def __init__(self, n_balls=8, seed=0, radius=(0.08, 0.2)):
         g = torch.Generator().manual_seed(seed)
         self.r = torch.rand(n_balls, generator=g) * (radius[1] - radius[0]) + radius[0]
         self.c = (torch.rand(n_balls, 3, generator=g) - 0.5) * (1.0 - 2 * self.r[:, None]).clamp(min=0)
         self.rgb = torch.rand(n_balls, 3, generator=g) * 0.8 + 0.1
+        self.texture_freq = 0.0
 
     @classmethod
     def matching_grid(cls, seed=0, n_balls=12, radius=(0.065, 0.18)):
@@ -352,6 +354,12 @@ class BallScene:
         out = torch.ones(o.shape[0], 3, dtype=torch.float64, device=o.device)
         hit = torch.isfinite(tmin)
         out[hit] = rgb[idx[hit]]
+        if self.texture_freq:  # a surface pattern in world space: detail for the fine hash levels
+            x = o[hit] + tmin[hit, None] * dn[hit]
+            f = self.texture_freq
+            pat = torch.sin(f * x[:, 0]) * torch.sin(f * x[:, 1]) * torch.sin(f * x[:, 2])
+            out[hit] = (out[hit] + 0.3 * pat[:, None] * torch.tensor([1.0, -0.6, 0.8], dtype=out.dtype,
+                                                                     device=out.device)).clamp(0, 1)
         return out.float()
 
     def density_grid(self, G=128, cascades=1):

@@ -83,6 +83,17 @@ def test_ball_scene_renders_hits_and_background():
     d = torch.tensor([[0.0, 0.0, 1.0], [0.0, 0.0, 1.0]])
     out = sc.render(o, d)
     assert torch.allclose(out[0], sc.rgb[0]) and torch.equal(out[1], torch.ones(3))
+    # textured: the hit point (0, 0, -0.25) has sin(f*0) = 0, so the pattern vanishes there;
+    # an off-axis hit carries it, the background stays white
+    sc.texture_freq = 40.0
+    o2 = torch.tensor([[0.0, 0.0, -2.0], [0.1, 0.07, -2.0], [0.0, 1.0, -2.0]])
+    d2 = torch.tensor([[0.0, 0.0, 1.0]] * 3)
+    out2 = sc.render(o2, d2)
+    assert torch.allclose(out2[0], sc.rgb[0]) and torch.equal(out2[2], torch.ones(3))
+    z = -math.sqrt(0.25 ** 2 - 0.1 ** 2 - 0.07 ** 2)
+    pat = math.sin(4.0) * math.sin(2.8) * math.sin(40.0 * z)
+    want = (sc.rgb[0].double() + 0.3 * pat * torch.tensor([1.0, -0.6, 0.8], dtype=torch.float64)).clamp(0, 1)
+    assert torch.allclose(out2[1].double(), want, atol=1e-6)
 
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
