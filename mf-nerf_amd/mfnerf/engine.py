@@ -20,6 +20,7 @@ refreshed by the same Adam pass and is what the grid kernels gather from.
 Multi-GPU: run/replay(exchange=dp.allreduce_mean_) all-reduces `grads` between backward and Adam.
 """
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -553,8 +554,11 @@ class TrainStep:
         else:
             self.graphs["update"] = cap(self._update)
             if P == 1:  # no collective between them: one graph, one launch gap less
-                self.graphs["finish_update"] = cap(self._finish_update if self._fixed() else
-                                                   lambda: (self._grid_finish(0), self._update()))
+                tail = self._finish_update if self._fixed() else lambda: (self._grid_finish(0), self._update())
+                self.graphs["finish_update"] = cap(tail)
+                # and the scatter with it (one graph transition less again) for untimed steps
+                self.graphs["grid_bw_tail"] = [cap(lambda j=j: (self._grid_bw(self.mbuf[j], 0), tail()))
+                                               for j in range(2)]
         torch.cuda.synchronize()
         # the next step's march runs beside this step's grid_bw scatter, whose 4096 workgroups would
         # otherwise take every dispatch slot first (the march's small kernels then finish after the
@@ -567,6 +571,8 @@ class TrainStep:
         self._ev_part = [torch.cuda.Event() for _ in range(P)]
         self._parity = 0
         self._primed = False
+        # where the next step's march starts: under this step's grid_bw (default) or at its start
+        self.march_early = os.environ.get("MFNERF_MARCH_EARLY", "0") == "1"
 
     def _stage_batch(self, j, batch):
         dst = self._static[j]
@@ -608,6 +614,9 @@ class TrainStep:
         self._ev_start.record(main)
         if not self._primed:
             self._march_on_side(j, batch, self._ev_start)
+        early = prefetch and self.march_early
+        if early:  # set 1-j was last read by the previous step, all of which precedes _ev_start
+            self._march_on_side(1 - j, next_batch, self._ev_start)
         main.wait_event(self._ev_march[j])
         self._use(self.mbuf[j])
         self.last_batch = self._static[j]
@@ -618,10 +627,16 @@ class TrainStep:
             with torch.cuda.stream(sq):
                 g["chain"][j][q].replay()
                 self._ev_chain[q].record(sq)
-                if q == P - 1 and prefetch:
+                if q == P - 1 and prefetch and not early:
                     # set 1-j was last read by the previous step, which this chain follows; waiting
                     # for the last chain puts the march under the grid_bw scatters, not the chains
                     self._march_on_side(1 - j, next_batch, self._ev_chain[q])
+                if fuse_tail and grid_bw_events is None:
+                    # P == 1: scatter + convert/Adam + repack as one graph (no event needed between)
+                    self.adam_step += 1
+                    g["grid_bw_tail"][j].replay()
+                    self._ev_part[q].record(sq)
+                    continue
                 if grid_bw_events is not None and q == 0:
                     grid_bw_events[0].record(sq)
                 g["grid_bw"][j][q].replay()
@@ -639,6 +654,8 @@ class TrainStep:
         if self.shard is not None:
             self._optimize(None, adam=lambda _g: self._shard_adam(g["adam"].replay),
                            pack=g["pack"].replay)
+        elif fuse_tail and grid_bw_events is None:
+            pass  # replayed with the scatter above
         elif fuse_tail:
             self.adam_step += 1
             g["finish_update"].replay()
