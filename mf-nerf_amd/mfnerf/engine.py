@@ -319,7 +319,8 @@ class TrainStep:
                  ptr(t.deltas), ptr(t.ts), ptr(t.counter), ptr(t.march_ws), s)
         # running total of marched samples (rm_s without a read on the step's critical path: in the
         # graphs this runs on the march's side stream)
-        self.samples_marched.add_(mb.counters[:, 0].sum())
+        # one kernel on the side chain for one part (a slice + reduce + add otherwise)
+        self.samples_marched.add_(mb.counters[0, 0] if self.n_parts == 1 else mb.counters[:, 0].sum())
         mark("march")
 
     def _chain(self, batch: Batch, mb, q, mark):
