@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--W", type=int, default=synthetic.LEGO_W)
     ap.add_argument("--grid", default="Hash")
     ap.add_argument("--T", type=int, default=19)
+    ap.add_argument("--mf", action="store_true",
+                    help="benchmark_synthetic_nerf_mf.sh's field and schedule: MixedFeature 8 tables, T2^20, "
+                         "rgb 128, 16384 rays, lr 2e-2, 20 epochs")
     args = ap.parse_args()
     dev = torch.device("cuda")
     W = args.W
@@ -43,7 +46,11 @@ def main():
     imgs, poses, dirs, K = data.ball_scene_views(scene, args.views, W, focal, seed=0, device=dev)
     t_imgs, t_poses, _, _ = data.ball_scene_views(scene, args.test_views, W, focal, seed=7, device=dev)
     ds = data.DeviceDataset(imgs, poses, dirs, K=K, img_wh=(W, W), device=dev, seed=5)
-    hp = HParams(num_epochs=args.epochs, steps_per_epoch=args.steps_per_epoch, grid=args.grid, T=args.T)
+    if args.mf:
+        hp = HParams(num_epochs=20, steps_per_epoch=args.steps_per_epoch, grid="MixedFeature", N_tables=8, T=20,
+                     rgb_channels=128, batch_size=16384, lr=2e-2)
+    else:
+        hp = HParams(num_epochs=args.epochs, steps_per_epoch=args.steps_per_epoch, grid=args.grid, T=args.T)
     tr = Trainer(hp, ds, device=dev)
     hist = []
 
@@ -63,8 +70,10 @@ def main():
     eval_s = time.perf_counter() - t1
     white = sum(float(-10 * torch.log10(((1 - im) ** 2).mean())) for im in t_imgs) / len(t_imgs)
     print(json.dumps({
-        "protocol": f"train.py defaults: {steps} steps x {hp.batch_size} rays, {hp.grid} L{hp.L} F{hp.F} "
-                    f"T2^{hp.T}, lr {hp.lr} cosine, occupancy every 16 steps",
+        "protocol": f"{'benchmark_synthetic_nerf_mf.sh' if args.mf else 'train.py defaults'}: {steps} steps x "
+                    f"{hp.batch_size} rays, {hp.grid} L{hp.L} F{hp.F} T2^{hp.T}"
+                    f"{' %d tables' % hp.N_tables if hp.grid == 'MixedFeature' else ''}, rgb {hp.rgb_channels}, "
+                    f"lr {hp.lr} cosine, occupancy every 16 steps",
         "scene": f"12-ball scene (bench occupancy balls), texture_freq {args.tex}, {args.views} train / "
                  f"{args.test_views} held-out views at {W}x{W}, Lego intrinsics",
         "train_wall_s": round(wall, 2), "rays_per_s_whole_run": round(steps * hp.batch_size / wall, 1),
