@@ -564,7 +564,8 @@ class TrainStep:
         # the next step's march runs beside this step's grid_bw scatter, whose 4096 workgroups would
         # otherwise take every dispatch slot first (the march's small kernels then finish after the
         # scatter, on the critical path): the side stream gets the higher queue priority
-        self._side = torch.cuda.Stream(device=self.dev, priority=torch.cuda.Stream.priority_range()[1])
+        hi = os.environ.get("MFNERF_SIDE_HIGH_PRIORITY", "1") == "1"
+        self._side = torch.cuda.Stream(device=self.dev, priority=torch.cuda.Stream.priority_range()[1] if hi else 0)
         self._part_streams = [None] + [torch.cuda.Stream(device=self.dev) for _ in range(P - 1)]
         self._ev_march = [torch.cuda.Event(), torch.cuda.Event()]
         self._ev_start = torch.cuda.Event()
