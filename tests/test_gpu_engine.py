@@ -23,6 +23,31 @@ def _record(st):
             "loss": float(st.loss_sum)}
 
 
+def test_timed_and_fused_tail_replays_match_eager(gpu):
+    """bench.py alternates replays whose scatter is its own (event-timed) graph with replays that run
+    scatter + convert/Adam + repack as one graph: any mix is bit-identical to eager steps."""
+    K = 7
+    a, b = _make(gpu, 1), _make(gpu, 1)
+    batches = a.make_batches(K + 1, seed=5)
+    for k in range(K):
+        b.run(batches[k])
+    a.run(batches[0])
+    torch.cuda.synchronize()
+    a.capture()
+    assert a.graphs.get("grid_bw_tail") is not None
+    mk = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    for k in range(1, K):
+        ev = (mk(), [mk()]) if k % 3 == 0 else None
+        a.replay(batches[k], next_batch=batches[k + 1] if k + 1 < K else None, grid_bw_events=ev)
+        if ev is not None:
+            torch.cuda.synchronize()
+            assert ev[0].elapsed_time(ev[1][0]) > 0
+    torch.cuda.synchronize()
+    assert a.adam_step == b.adam_step
+    assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
+    assert torch.equal(a.p16, b.p16) and int(a.step_dev) == int(b.step_dev)
+
+
 @pytest.mark.parametrize("parts", [1, 2, 4])
 def test_pipelined_replay_matches_eager(gpu, oracle, parts):
     K = 6
