@@ -24,15 +24,19 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "mf-nerf_amd")]
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+GRID_BW_KERNEL = "grid_bw_kernel"  # the table-gradient scatter's kernel name in the PMC summaries
 
-# algorithmic bytes per live sample of each per-sample kernel (DESIGN.md "Kernels and rooflines")
+# algorithmic bytes per live sample of each per-sample kernel, as SURVEY.md 8(d) prices them (the
+# tcnn form of the op: fp16 features and fp16 gradient scatter), DESIGN.md section 5
 L, F = 16, 2
 BYTES_PER_SAMPLE = {
     "grid_fw": 12 + L * 8 * F * 2 + L * F * 2,          # xyz + fp16 corner gathers + fp16 features = 588
-    "grid_bw": 12 + L * F * 4 + L * 8 * F * 4,          # xyz + fp32 dL/dfeat + fp32 atomic adds = 1164
+    "grid_bw": L * F * 2 + 12 + L * 8 * F * 2,          # fp16 dL/dy + xyz + fp16 scatter of 8 corners = 588
     "field_fw": L * F * 2 + 12 + 4 + 12,                 # feat + dir + sigma + rgb = 92
     "field_bw": L * F * 2 + 12 + 16 + L * F * 4,         # feat + dir + dsigma,drgb + dfeat = 220
 }
+# measured memory-side int32 atomic request ceiling of MI355X (tools/atomic_probe3.hip)
+ATOMIC_REQ_PEAK_G = 26.7
 
 
 # BASELINE.json configs as step presets.  "lego" (config 2) is the one the metric is quoted on and the
@@ -82,18 +86,24 @@ def run_step(step, batch, world, ev=None):
 
 
 def pmc_traffic(kernel_prefix):
-    """HBM-side bytes per launch of a kernel from the newest committed PMC summary
-    (profiles/rNN_pmc_traffic.json, made by tools/pmc_traffic.py from separate FETCH_SIZE /
-    WRITE_SIZE rocprofv3 passes with the guide's gfx950 corrections); (None, None) if absent."""
+    """(HBM-side bytes, memory-side atomic requests, source) per launch of a kernel from the newest
+    committed PMC summary (profiles/rNN_*pmc_traffic.json, made by tools/pmc_traffic.py from separate
+    FETCH_SIZE / WRITE_SIZE / TCC_EA0_ATOMIC rocprofv3 passes with the guide's gfx950 corrections);
+    Nones if absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    import re
+
+    def order(f):  # profiles/rNN_vMM_pmc_traffic.json: newest round, then newest version
+        m = re.match(r"r(\d+)(?:_v(\d+))?_", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2) or 0)) if m else (-1, -1)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*pmc_traffic.json")), key=order)
     if not files:
-        return None, None
+        return None, None, None
     d = json.load(open(files[-1]))
     for k, v in d["kernels"].items():
         if k.startswith(kernel_prefix):
-            return round(v["traffic_bytes"]), os.path.relpath(files[-1], ROOT)
-    return None, None
+            return round(v["traffic_bytes"]), v.get("atomic_requests"), os.path.relpath(files[-1], ROOT)
+    return None, None, None
 
 
 def stage_times(events, steps):
@@ -272,9 +282,16 @@ def main():
     # roofline: grid_bw (the dominant kernel), timed by events around it inside the timed region
     dom = "grid_bw"
     # the committed PMC summary is of the lego workload
-    traffic, traffic_src = pmc_traffic("grid_bw_kernel") if args.preset == "lego" else (None, None)
+    traffic, atomic_req, traffic_src = pmc_traffic(GRID_BW_KERNEL) if args.preset == "lego" else (None, None, None)
     dom_bytes = BYTES_PER_SAMPLE[dom] * mean_samples
     achieved = dom_bytes / (grid_bw_ms * 1e-3) / 1e9
+    # the bound the scatter actually meets: memory-side atomic requests per second
+    atomic = None
+    if atomic_req:
+        rate = atomic_req / (grid_bw_ms * 1e-3) / 1e9
+        atomic = {"requests_per_launch": round(atomic_req), "requests_per_sample": round(atomic_req / mean_samples, 2),
+                  "achieved": round(rate, 2), "peak": ATOMIC_REQ_PEAK_G, "unit": "G requests/s",
+                  "frac": round(rate / ATOMIC_REQ_PEAK_G, 4)}
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -300,7 +317,8 @@ def main():
                          "traffic_source": traffic_src,
                          "timed_launches": (len(range(0, args.steps, args.roofline_every)) if use_graph
                                             else args.steps),
-                         "bytes_per_launch": round(dom_bytes)},
+                         "bytes_per_launch": round(dom_bytes), "bytes_per_sample": BYTES_PER_SAMPLE[dom],
+                         "samples_per_launch": round(mean_samples), "atomic": atomic},
             "graph": use_graph, "host_issue_ms_per_step": round(host_s / args.steps * 1e3, 4),
             "grid_bw_ms": round(grid_bw_ms, 4),
             "eager_stage_ms": {k: round(v, 4) for k, v in eager_stage_ms.items()},

@@ -34,6 +34,23 @@ typedef struct ihipStream_t* mfnerf_stream_t; /* == hipStream_t */
 const char* mfnerf_last_error(void);
 int mfnerf_abi_version(void);
 
+/* Mixed-precision state of a training step, device-resident (32 bytes, zero-initialised by the
+ * caller, then scale / growth_interval / growth_factor / backoff_factor set): torch.cuda.amp.GradScaler
+ * as PyTorch-Lightning's precision=16 drives it (train.py:287; init scale 65536, growth 2.0 every
+ * 2000 clean steps, backoff 0.5).  Producers of the step's gradient raise `nonfinite`; the optimizer
+ * call skips the update when it is set and then runs GradScaler.update() on the device.
+ * growth_interval == 0: static scaling (the skip only; mfnerf_field_bw then uses its grad_scale). */
+typedef struct {
+    int32_t nonfinite;       /* 1 when some gradient of the step is inf/nan; cleared by the optimizer */
+    int32_t skipped;         /* optimizer steps skipped so far */
+    float scale;             /* current loss scale (dynamic mode) */
+    int32_t growth_tracker;  /* clean steps since the last scale change */
+    int32_t growth_interval; /* 2000; 0 = static */
+    float growth_factor;     /* 2.0 */
+    float backoff_factor;    /* 0.5 */
+    int32_t ticket;          /* the optimizer pass's last-workgroup ticket; 0 between calls */
+} mfnerf_amp_state;
+
 /* ---------------------------------------------------------------- vren ops */
 
 /* vren.ray_aabb_intersect (binding.cpp:4-16, intersection.cu:59-100).
@@ -238,10 +255,11 @@ int mfnerf_field_fw(const void* feat_f16, int64_t feat_plane_stride, const float
 
 /* Backward of mfnerf_field_fw (recomputes the forward; same feat layouts).  dL_dsigma (n), dL_drgb (n,3) f32 ->
  * dL_dfeat (n,32) f32, and ADDS the weight grads into grad_xyz / grad_rgb (tcnn layout f32).
- * grad_scale: power-of-two factor applied to the incoming grads before the fp16 MFMA products
+ * grad_scale: the loss scale -- factor applied to the incoming grads before the fp16 MFMA products
  * and removed from every output (keeps O(1e-6) per-sample grads out of the fp16 subnormals).
+ * grad_scale == 0: the dynamic scale amp->scale, read on the device (amp required).
  * workspace: mfnerf_field_bw_workspace() bytes (per-workgroup weight-grad slab).
- * nonfinite (optional device i32): set to 1 when any dL_dfeat or weight gradient is inf/nan (the
+ * amp (optional): amp->nonfinite is set to 1 when any dL_dfeat or weight gradient is inf/nan (the
  * table gradient of mfnerf_grid_encode_bw is a weighted sum of dL_dfeat, so this flags the whole
  * step's gradient without scanning it; feeds mfnerf_adam_step's skip).
  * level_l1 (optional device f32[16], ACCUMULATED): the per-level L1 norm of dL_dfeat, i.e. what
@@ -249,7 +267,7 @@ int mfnerf_field_fw(const void* feat_f16, int64_t feat_plane_stride, const float
 int64_t mfnerf_field_bw_workspace(int64_t n, int rgb_width);
 int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
                     int rgb_width, const float* dL_dsigma, const float* dL_drgb, float grad_scale, float* dL_dfeat,
-                    float* grad_xyz, float* grad_rgb, void* workspace, int32_t* nonfinite, float* level_l1,
+                    float* grad_xyz, float* grad_rgb, void* workspace, mfnerf_amp_state* amp, float* level_l1,
                     mfnerf_stream_t stream);
 
 /* grad_xyz = grad_rgb = NULL in mfnerf_field_bw defers the weight-gradient fold: the per-block
@@ -299,8 +317,9 @@ int mfnerf_occupancy_update(float* density_grid, const float* sigmas, const int3
  *   rays_o = c2w[:, 3], rays_d = directions[pix] @ c2w[:, :3]^T, rgb = images[img, pix].
  * images (n_img, hw, 3) f32, poses (n_img, 3, 4) f32, directions (hw, 3) f32 (camera frame).
  * out (3, n_rays, 3) f32 = [rays_o | rays_d | rgb]; img_idx / pix_idx (n_rays) i32 optional.
- * Draws: counter-based hash of (seed, *call, ray); call (optional device u64) is incremented by the
- * launch, so graph replays sample fresh batches. */
+ * Draws: counter-based hash of (seed, call[0], ray); call (optional device u64[2], zero-initialised)
+ * is call[0] = the draw counter, incremented by the launch (by its last workgroup, call[1] being the
+ * arrival ticket, 0 between launches), so graph replays sample fresh batches. */
 int mfnerf_sample_rays(const float* images, const float* poses, const float* directions, int64_t n_img, int64_t hw,
                        int64_t n_rays, int same_image, uint64_t seed, uint64_t* call, float* out, int32_t* img_idx,
                        int32_t* pix_idx, mfnerf_stream_t stream);
@@ -324,15 +343,17 @@ int mfnerf_sample_rays_prep(const float* images, const float* poses, const float
  * and the call then increments it (graph-replay safe).  Without step_dev, t = step.
  * lr_dev (optional device f32): learning rate read on the device (a schedule that does not
  * re-capture the graph); lr is used when it is NULL.
- * skip (optional device i32[2]): when skip[0] != 0 the call changes nothing (params, m, v, p_f16
- * and step_dev untouched) and increments skip[1] -- torch GradScaler's skipped step on a
- * non-finite gradient (PL precision=16, train.py:287).  The call clears skip[0] afterwards;
- * skip[0] is raised by mfnerf_field_bw's nonfinite flag or mfnerf_check_finite.
+ * amp (optional): when amp->nonfinite != 0 the call changes nothing (params, m, v, p_f16 and
+ * step_dev untouched) and increments amp->skipped -- torch GradScaler's skipped step on a
+ * non-finite gradient (PL precision=16, train.py:287); amp->nonfinite is raised by
+ * mfnerf_field_bw or mfnerf_check_finite.  Then GradScaler.update() (dynamic mode: backoff on a
+ * skip, growth after growth_interval clean steps) and amp->nonfinite cleared -- done by the pass's
+ * last workgroup (amp->ticket), no extra launch.
  * zero_grads != 0: grads is zeroed by the same pass (also on a skipped step), ready for the next
  * step's accumulation. */
 int mfnerf_adam_step(float* params, float* grads, float* m, float* v, void* p_f16, int64_t n, float lr,
                      float beta1, float beta2, float eps, float grad_scale, int step, int32_t* step_dev,
-                     const float* lr_dev, int32_t* skip, int zero_grads, mfnerf_stream_t stream);
+                     const float* lr_dev, mfnerf_amp_state* amp, int zero_grads, mfnerf_stream_t stream);
 
 /* mfnerf_grid_encode_bw_finish + mfnerf_adam_step (zero_grads on) in one pass, for a step with no
  * gradient exchange between them: grads[0, table_offset) are float gradients, grads[table_offset, ...)
@@ -346,7 +367,7 @@ int mfnerf_adam_step(float* params, float* grads, float* m, float* v, void* p_f1
 int mfnerf_adam_step_fixed(float* params, float* grads, float* m, float* v, void* p_f16, int64_t n,
                            int64_t table_offset, const mfnerf_grid_desc* desc, void* workspace,
                            float* level_l1, float lr, float beta1, float beta2, float eps,
-                           int32_t* step_dev, const float* lr_dev, int32_t* skip, mfnerf_stream_t stream);
+                           int32_t* step_dev, const float* lr_dev, mfnerf_amp_state* amp, mfnerf_stream_t stream);
 
 /* status[0] (device i32) = 1 if any of x (n f32, 16-byte aligned) is inf/nan, else 0 (a full scan;
  * the training step gets the same flag from mfnerf_field_bw's nonfinite argument instead). */

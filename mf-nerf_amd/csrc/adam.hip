@@ -9,59 +9,58 @@ namespace {
 
 __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, __half* __restrict__ p16, int64_t n, float lr, float b1, float b2,
-                            float eps, float gscale, int step, const int32_t* __restrict__ step_dev,
-                            const float* __restrict__ lr_dev, const int32_t* __restrict__ skip, int zero_grads) {
+                            float eps, float gscale, int step, int32_t* __restrict__ step_dev,
+                            const float* __restrict__ lr_dev, mfnerf_amp_state* __restrict__ amp, int zero_grads) {
     const int64_t n4 = n / 4;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (skip && *skip) {  // GradScaler: no update on a non-finite gradient (only the zeroing)
+    // step_dev counts completed steps; this update is number *step_dev + 1 (the last workgroup
+    // advances it after every workgroup has read it)
+    const bool skipped = amp && amp->nonfinite;  // GradScaler: no update on a non-finite gradient
+    const int st = step_dev ? *step_dev + 1 : step;
+    if (lr_dev) lr = *lr_dev;
+    if (skipped) {
         if (zero_grads) {
             for (int64_t i = t0; i < n4; i += stride) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
             for (int64_t i = n4 * 4 + t0; i < n; i += stride) g[i] = 0.0f;
         }
-        return;
-    }
-    // step_dev counts completed steps; this update is number *step_dev + 1 (bump_step_kernel
-    // advances it after the update, so every block reads the same value)
-    const int st = step_dev ? *step_dev + 1 : step;
-    if (lr_dev) lr = *lr_dev;
-    // apex multi_tensor_adam (ADAM_MODE, decay 0): m/(1-b1^t), v/(1-b2^t), p -= lr*m_hat/(sqrt(v_hat)+eps)
-    const float bc1 = 1.0f - powf(b1, (float)st);
-    const float bc2 = 1.0f - powf(b2, (float)st);
-    for (int64_t i = t0; i < n4; i += stride) {
-        float4 pp = reinterpret_cast<float4*>(p)[i];
-        const float4 gg = reinterpret_cast<const float4*>(g)[i];
-        float4 mm = reinterpret_cast<float4*>(m)[i];
-        float4 vv = reinterpret_cast<float4*>(v)[i];
-        float* pa = &pp.x; const float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
+    } else {
+        // apex multi_tensor_adam (ADAM_MODE, decay 0): m/(1-b1^t), v/(1-b2^t), p -= lr*m_hat/(sqrt(v_hat)+eps)
+        const float bc1 = 1.0f - powf(b1, (float)st);
+        const float bc2 = 1.0f - powf(b2, (float)st);
+        for (int64_t i = t0; i < n4; i += stride) {
+            float4 pp = reinterpret_cast<float4*>(p)[i];
+            const float4 gg = reinterpret_cast<const float4*>(g)[i];
+            float4 mm = reinterpret_cast<float4*>(m)[i];
+            float4 vv = reinterpret_cast<float4*>(v)[i];
+            float* pa = &pp.x; const float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) mfn::adam_elem(pa[k], ma[k], va[k], ga[k] * gscale, b1, b2, eps, lr, bc1, bc2);
-        reinterpret_cast<float4*>(p)[i] = pp;
-        reinterpret_cast<float4*>(m)[i] = mm;
-        reinterpret_cast<float4*>(v)[i] = vv;
-        if (zero_grads) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (p16) {
-            __half2 a = __floats2half2_rn(pp.x, pp.y), b = __floats2half2_rn(pp.z, pp.w);
-            uint2 u; u.x = *reinterpret_cast<uint32_t*>(&a); u.y = *reinterpret_cast<uint32_t*>(&b);
-            reinterpret_cast<uint2*>(p16)[i] = u;
+            for (int k = 0; k < 4; ++k) mfn::adam_elem(pa[k], ma[k], va[k], ga[k] * gscale, b1, b2, eps, lr, bc1, bc2);
+            reinterpret_cast<float4*>(p)[i] = pp;
+            reinterpret_cast<float4*>(m)[i] = mm;
+            reinterpret_cast<float4*>(v)[i] = vv;
+            if (zero_grads) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (p16) {
+                __half2 a = __floats2half2_rn(pp.x, pp.y), b = __floats2half2_rn(pp.z, pp.w);
+                uint2 u; u.x = *reinterpret_cast<uint32_t*>(&a); u.y = *reinterpret_cast<uint32_t*>(&b);
+                reinterpret_cast<uint2*>(p16)[i] = u;
+            }
+        }
+        // tail
+        for (int64_t i = n4 * 4 + t0; i < n; i += stride) {
+            mfn::adam_elem(p[i], m[i], v[i], g[i] * gscale, b1, b2, eps, lr, bc1, bc2);
+            if (zero_grads) g[i] = 0.0f;
+            if (p16) p16[i] = __float2half_rn(p[i]);
         }
     }
-    // tail
-    for (int64_t i = n4 * 4 + t0; i < n; i += stride) {
-        mfn::adam_elem(p[i], m[i], v[i], g[i] * gscale, b1, b2, eps, lr, bc1, bc2);
-        if (zero_grads) g[i] = 0.0f;
-        if (p16) p16[i] = __float2half_rn(p[i]);
-    }
+    if (amp) mfn::amp_step_end_last_block(step_dev, amp, nullptr, 0);
 }
 
-// after the update: count the step (or the skipped step) and clear the non-finite flag for the
-// next step's producers
 }  // namespace
 
-__global__ void mfn_bump_step_kernel(int32_t* s, int32_t* skip, float* zero, int nz) {
-    if (skip && skip[0]) { skip[1] += 1; skip[0] = 0; }
-    else if (s) *s += 1;
-    for (int k = 0; k < nz; ++k) zero[k] = 0.0f;  // a small accumulator, ready for the next step
+// the step's bookkeeping as its own one-thread launch (callers without an amp state)
+__global__ void mfn_bump_step_kernel(int32_t* s, mfnerf_amp_state* amp, float* zero, int nz) {
+    mfn::amp_step_end(s, amp, zero, nz);
 }
 
 namespace {
@@ -109,7 +108,7 @@ extern "C" int mfnerf_flag_from_shard(const float* g_shard, int32_t* flag, mfner
 
 extern "C" int mfnerf_adam_step(float* params, float* grads, float* m, float* v, void* p_f16, int64_t n,
                                 float lr, float beta1, float beta2, float eps, float grad_scale, int step,
-                                int32_t* step_dev, const float* lr_dev, int32_t* skip, int zero_grads,
+                                int32_t* step_dev, const float* lr_dev, mfnerf_amp_state* amp, int zero_grads,
                                 mfnerf_stream_t stream) {
     if (n < 0) { mfn_set_error("adam_step: bad size"); return MFN_ERR_INVALID; }
     if (n == 0) return MFN_OK;
@@ -123,8 +122,11 @@ extern "C" int mfnerf_adam_step(float* params, float* grads, float* m, float* v,
     const int64_t want = mfn::div_up<int64_t>(mfn::div_up<int64_t>(n, 4), threads);
     const unsigned blocks = (unsigned)(want < 4096 ? (want < 1 ? 1 : want) : 4096);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(threads), 0, stream, params, grads, m, v, (__half*)p_f16, n, lr,
-                       beta1, beta2, eps, grad_scale, step, step_dev, lr_dev, skip, zero_grads);
-    if (step_dev || skip) hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, skip, (float*)nullptr, 0);
+                       beta1, beta2, eps, grad_scale, step, step_dev, lr_dev, amp, zero_grads);
+    // with amp the last workgroup did the bookkeeping; without it only the step count remains
+    if (step_dev && !amp)
+        hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, (mfnerf_amp_state*)nullptr,
+                           (float*)nullptr, 0);
     return mfn_check_launch("adam_step");
 }
 

@@ -27,6 +27,6 @@ extern "C" {
 
 const char* mfnerf_last_error(void) { return g_err; }
 
-int mfnerf_abi_version(void) { return 1; }
+int mfnerf_abi_version(void) { return 2; }
 
 }  // extern "C"

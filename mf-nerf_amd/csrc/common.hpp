@@ -8,6 +8,8 @@
 #include <hip/hip_fp16.h>
 #include <stdint.h>
 
+#include "../../include/mfnerf.h"
+
 #define MFN_SQRT3 1.73205080757f
 
 namespace mfn {
@@ -94,6 +96,51 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
     v = b2 * v + (1.0f - b2) * g * g;
     const float denom = sqrtf(v / bc2) + eps;
     p = p - lr * ((m / bc1) / denom);
+}
+
+// The end of an optimizer step, once per launch (torch GradScaler.step + update as PL precision=16
+// drives it, train.py:287; apex FusedAdam's step count): a skipped step (amp->nonfinite) counts in
+// amp->skipped and backs the loss scale off; a clean step advances Adam's t and, after
+// growth_interval clean steps in a row, grows the scale.  The flag is cleared and `zero` (nz floats,
+// a per-step accumulator) zeroed for the next step.
+__device__ __forceinline__ void amp_step_end(int32_t* step_dev, mfnerf_amp_state* amp, float* zero, int nz) {
+    if (amp) {
+        const bool bad = amp->nonfinite != 0;
+        if (bad) amp->skipped += 1;
+        else if (step_dev) *step_dev += 1;
+        if (amp->growth_interval > 0) {  // dynamic loss scale (_amp_update_scale_)
+            if (bad) {
+                amp->scale *= amp->backoff_factor;
+                amp->growth_tracker = 0;
+            } else if (amp->growth_tracker + 1 >= amp->growth_interval) {
+                const float grown = amp->scale * amp->growth_factor;
+                if (isfinite(grown)) amp->scale = grown;
+                amp->growth_tracker = 0;
+            } else {
+                amp->growth_tracker += 1;
+            }
+        }
+        amp->nonfinite = 0;
+    } else if (step_dev) {
+        *step_dev += 1;
+    }
+    for (int k = 0; k < nz; ++k) zero[k] = 0.0f;
+}
+
+// Last-workgroup ticket: call from EVERY thread of every workgroup after the workgroup's last read of
+// the state amp_step_end changes; the workgroup that arrives last runs it (and re-arms the ticket), so
+// the step's bookkeeping needs no separate one-thread launch.
+__device__ __forceinline__ void amp_step_end_last_block(int32_t* step_dev, mfnerf_amp_state* amp, float* zero,
+                                                        int nz) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned total = gridDim.x * gridDim.y * gridDim.z;
+        const int prev = __hip_atomic_fetch_add(&amp->ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)prev == total - 1) {
+            amp_step_end(step_dev, amp, zero, nz);
+            __hip_atomic_store(&amp->ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 }  // namespace mfn

@@ -5,7 +5,8 @@
 //
 // Random draws: np.random.choice(n, k) (uniform with replacement) is replaced by a counter-based
 // hash of (seed, call, ray, stream) -- same distribution, not NumPy's stream.  `call` is read from
-// a device counter that the bump kernel advances, so graph replays draw fresh batches.
+// a device counter that the launch's last workgroup advances (call[1] is its arrival ticket), so
+// graph replays draw fresh batches without a separate one-thread launch.
 #include "common.hpp"
 #include "../../include/mfnerf.h"
 
@@ -42,14 +43,13 @@ struct MarchPrep {
     float* noise;   // (n_rays)
 };
 
-// out: (3, n_rays, 3) f32 = rays_o | rays_d | rgb
-__global__ void sample_rays_kernel(const float* __restrict__ images, const float* __restrict__ poses,
-                                   const float* __restrict__ directions, int64_t n_img, int64_t hw, int64_t n_rays,
-                                   int same_image, uint64_t seed, const uint64_t* __restrict__ call,
-                                   float* __restrict__ out, int32_t* __restrict__ img_idx,
-                                   int32_t* __restrict__ pix_idx, const MarchPrep prep) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n_rays) return;
+// one ray of the batch: image + pixel draw, rays, rgb, and optionally the march prologue
+__device__ __forceinline__ void draw_ray(int64_t r, const float* __restrict__ images, const float* __restrict__ poses,
+                                         const float* __restrict__ directions, int64_t n_img, int64_t hw,
+                                         int64_t n_rays, int same_image, uint64_t seed,
+                                         const uint64_t* __restrict__ call, float* __restrict__ out,
+                                         int32_t* __restrict__ img_idx, int32_t* __restrict__ pix_idx,
+                                         const MarchPrep& prep) {
     const uint64_t key = splitmix64(splitmix64(seed ^ 0xD1B54A32D192ED03ull) ^ (call ? *call : 0ull));
     const uint32_t im = below(key, same_image ? 0u : 2u * (uint64_t)r + 1u, (uint32_t)n_img);
     const uint32_t px = below(key, 2u * (uint64_t)r + 2u, (uint32_t)hw);
@@ -95,7 +95,28 @@ __global__ void sample_rays_kernel(const float* __restrict__ images, const float
     }
 }
 
-__global__ void bump_call_kernel(uint64_t* call) { *call += 1; }
+
+// out: (3, n_rays, 3) f32 = rays_o | rays_d | rgb
+__global__ void sample_rays_kernel(const float* __restrict__ images, const float* __restrict__ poses,
+                                   const float* __restrict__ directions, int64_t n_img, int64_t hw, int64_t n_rays,
+                                   int same_image, uint64_t seed, uint64_t* __restrict__ call,
+                                   float* __restrict__ out, int32_t* __restrict__ img_idx,
+                                   int32_t* __restrict__ pix_idx, const MarchPrep prep) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n_rays) draw_ray(r, images, poses, directions, n_img, hw, n_rays, same_image, seed, call, out, img_idx,
+                             pix_idx, prep);
+    if (call) {
+        // every thread of the block has read *call above; the last block to arrive advances it
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint64_t prev = __hip_atomic_fetch_add(call + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (prev == (uint64_t)gridDim.x - 1) {
+                call[0] += 1;
+                __hip_atomic_store(call + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+}
 
 }  // namespace
 
@@ -111,7 +132,6 @@ extern "C" int mfnerf_sample_rays(const float* images, const float* poses, const
     const MarchPrep none{nullptr, nullptr, 0.0f, nullptr, nullptr};
     hipLaunchKernelGGL(sample_rays_kernel, dim3((unsigned)div_up<int64_t>(n_rays, 256)), dim3(256), 0, stream, images,
                        poses, directions, n_img, hw, n_rays, same_image, seed, call, out, img_idx, pix_idx, none);
-    if (call) hipLaunchKernelGGL(bump_call_kernel, dim3(1), dim3(1), 0, stream, call);
     return mfn_check_launch("sample_rays");
 }
 
@@ -132,6 +152,5 @@ extern "C" int mfnerf_sample_rays_prep(const float* images, const float* poses, 
     hipLaunchKernelGGL(sample_rays_kernel, dim3((unsigned)div_up<int64_t>(n_rays, 256)), dim3(256), 0, stream, images,
                        poses, directions, n_img, hw, n_rays, same_image, seed, call, out, (int32_t*)nullptr,
                        (int32_t*)nullptr, prep);
-    if (call) hipLaunchKernelGGL(bump_call_kernel, dim3(1), dim3(1), 0, stream, call);
     return mfn_check_launch("sample_rays_prep");
 }

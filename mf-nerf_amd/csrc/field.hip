@@ -449,8 +449,8 @@ template <int W, int NW>
 __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
     const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n,
     const int32_t* __restrict__ n_dev, const _Float16* __restrict__ packed, const float* __restrict__ dL_dsigma,
-    const float* __restrict__ dL_drgb, float grad_scale, float* __restrict__ dL_dfeat, float* __restrict__ slab,
-    int32_t* __restrict__ nonfinite, float* __restrict__ level_l1) {
+    const float* __restrict__ dL_drgb, float grad_scale, const float* __restrict__ scale_dev,
+    float* __restrict__ dL_dfeat, float* __restrict__ slab, int32_t* __restrict__ nonfinite, float* __restrict__ level_l1) {
     using G = Geo<W>;
     using C = BwCfg<W, NW>;
     constexpr int MT = G::MT;
@@ -470,7 +470,7 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
     float* i_r3 = i_r2 + W * W;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const float S = grad_scale, invS = 1.0f / grad_scale;
+    const float S = scale_dev ? *scale_dev : grad_scale, invS = 1.0f / S;  // the (dynamic) loss scale
     const f32x16 z = {};
     // register accumulators, 32x32 tiles [out-tile][in-tile] (192 registers at W = 64, NW = 4)
     constexpr int R2 = RL ? 1 : MT;
@@ -718,7 +718,7 @@ template <int W>
 __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_wr2_kernel(
     const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n,
     const int32_t* __restrict__ n_dev, const _Float16* __restrict__ packed, const float* __restrict__ dL_drgb,
-    float grad_scale, float* __restrict__ slab) {
+    float grad_scale, const float* __restrict__ scale_dev, float* __restrict__ slab) {
     using G = Geo<W>;
     constexpr int MT = G::MT;
     constexpr int NF = G::B4;  // forward fragments + Wr3^T (B5)
@@ -743,7 +743,7 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_wr2_kernel(
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const float S = grad_scale, invS = 1.0f / grad_scale;
+    const float S = scale_dev ? *scale_dev : grad_scale, invS = 1.0f / S;
     const f32x16 z = {};
     f32x16 acc[MT][MT];
 #pragma unroll
@@ -912,8 +912,9 @@ void launch_fw(const void* feat, int64_t ps, const float* dirs, int64_t n, const
 
 template <int W, int NW>
 int launch_bw(const void* feat, int64_t ps, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
-              const float* dL_dsigma, const float* dL_drgb, float grad_scale, float* dL_dfeat, float* grad_xyz,
-              float* grad_rgb, void* workspace, int32_t* nonfinite, float* level_l1, mfnerf_stream_t stream) {
+              const float* dL_dsigma, const float* dL_drgb, float grad_scale, const float* scale_dev, float* dL_dfeat,
+              float* grad_xyz, float* grad_rgb, void* workspace, int32_t* nonfinite, float* level_l1,
+              mfnerf_stream_t stream) {
     using C = BwCfg<W, NW>;
     if constexpr (C::LDS > 65536) {  // more than the default dynamic-LDS limit
         static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_kernel<W, NW>),
@@ -925,11 +926,11 @@ int launch_bw(const void* feat, int64_t ps, const float* dirs, int64_t n, const 
     }
     hipLaunchKernelGGL((field_bw_kernel<W, NW>), dim3(BW_BLOCKS), dim3(64 * NW), C::LDS, stream,
                        (const _Float16*)feat, ps, dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb,
-                       grad_scale, dL_dfeat, (float*)workspace, nonfinite, level_l1);
+                       grad_scale, scale_dev, dL_dfeat, (float*)workspace, nonfinite, level_l1);
     if constexpr (C::R2_SPLIT)
         hipLaunchKernelGGL(field_bw_wr2_kernel<W>, dim3(BW_BLOCKS), dim3(FIELD_BLOCK),
                            (size_t)(Geo<W>::B4 + 4) * FRAG_HALFS * 2, stream, (const _Float16*)feat, ps, dirs, n, n_dev,
-                           (const _Float16*)packed, dL_drgb, grad_scale, (float*)workspace);
+                           (const _Float16*)packed, dL_drgb, grad_scale, scale_dev, (float*)workspace);
     if (grad_xyz)  // else deferred: mfnerf_field_bw_reduce folds the slab later
         hipLaunchKernelGGL(slab_reduce_kernel<W>, dim3((Geo<W>::N_DW + 63) / 64), dim3(256), 0, stream,
                            (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
@@ -990,26 +991,29 @@ int64_t mfnerf_field_bw_workspace(int64_t n, int rgb_width) {
 int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float* dirs, int64_t n,
                     const int32_t* n_dev, const void* packed,
                     int rgb_width, const float* dL_dsigma, const float* dL_drgb, float grad_scale, float* dL_dfeat,
-                    float* grad_xyz, float* grad_rgb, void* workspace, int32_t* nonfinite, float* level_l1,
+                    float* grad_xyz, float* grad_rgb, void* workspace, mfnerf_amp_state* amp, float* level_l1,
                     mfnerf_stream_t stream) {
     if (!width_ok(rgb_width)) return bad_width(rgb_width);
-    if (n < 0 || !(grad_scale > 0.0f) || (feat_plane_stride != 0 && feat_plane_stride < n)) {
-        mfn_set_error("field_bw: bad size, plane stride or grad_scale"); return MFN_ERR_INVALID;
+    if (n < 0 || !(grad_scale >= 0.0f) || (grad_scale == 0.0f && !amp) ||
+        (feat_plane_stride != 0 && feat_plane_stride < n)) {
+        mfn_set_error("field_bw: bad size, plane stride or grad_scale (0 = dynamic needs amp)"); return MFN_ERR_INVALID;
     }
     if (n == 0) return MFN_OK;
     if (!feat_f16 || !dirs || !packed || !dL_dsigma || !dL_drgb || !dL_dfeat || !workspace || (!grad_xyz != !grad_rgb)) {
         mfn_set_error("field_bw: null pointer"); return MFN_ERR_INVALID;
     }
+    int32_t* nonfinite = amp ? &amp->nonfinite : nullptr;
+    const float* scale_dev = grad_scale == 0.0f ? &amp->scale : nullptr;
     int st;
     if (rgb_width == 128)
         st = launch_bw<128, 4>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, dL_dsigma, dL_drgb, grad_scale,
-                               dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
+                               scale_dev, dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
     else if (bw_waves_w64() == 8)
         st = launch_bw<64, 8>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, dL_dsigma, dL_drgb, grad_scale,
-                              dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
+                              scale_dev, dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
     else
         st = launch_bw<64, 4>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, dL_dsigma, dL_drgb, grad_scale,
-                              dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
+                              scale_dev, dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
     if (st != MFN_OK) return st;
     return mfn_check_launch("field_bw");
 }

@@ -13,7 +13,7 @@
 
 using namespace mfn;
 
-__global__ void mfn_bump_step_kernel(int32_t* s, int32_t* skip, float* zero, int nz);  // adam.hip
+__global__ void mfn_bump_step_kernel(int32_t* s, mfnerf_amp_state* amp, float* zero, int nz);  // adam.hip
 
 namespace {
 
@@ -502,13 +502,13 @@ __global__ __launch_bounds__(256) void adam_fixed_kernel(float* __restrict__ p, 
                                                          __half* __restrict__ p16, int64_t n, int64_t off,
                                                          int* __restrict__ priv, int64_t dense_vals,
                                                          int64_t total_vals, const mfnerf_grid_desc D,
-                                                         const float* __restrict__ level_l1, float lr, float b1,
-                                                         float b2, float eps, const int32_t* __restrict__ step_dev,
+                                                         float* __restrict__ level_l1, float lr, float b1,
+                                                         float b2, float eps, int32_t* __restrict__ step_dev,
                                                          const float* __restrict__ lr_dev,
-                                                         const int32_t* __restrict__ skip) {
+                                                         mfnerf_amp_state* __restrict__ amp, int n_levels) {
     __shared__ TableRegions R;
     R.build(D, level_l1, total_vals);
-    const bool skipped = skip && *skip;  // GradScaler: no update on a non-finite gradient, only the zeroing
+    const bool skipped = amp && amp->nonfinite;  // GradScaler: no update on a non-finite gradient, only the zeroing
     const int st = *step_dev + 1;
     if (lr_dev) lr = *lr_dev;
     const float bc1 = 1.0f - powf(b1, (float)st);
@@ -556,6 +556,9 @@ __global__ __launch_bounds__(256) void adam_fixed_kernel(float* __restrict__ p, 
             reinterpret_cast<uint2*>(p16)[i4] = u;
         }
     }
+    // step count / skip count / loss scale, and level_l1 zeroed for the next step's field_bw, by the
+    // last workgroup (every workgroup has read level_l1, step_dev and the flag by now)
+    if (amp) mfn::amp_step_end_last_block(step_dev, amp, level_l1, n_levels);
 }
 
 int64_t dense_entries_of(const mfnerf_grid_desc* d) {
@@ -684,7 +687,7 @@ int mfnerf_grid_encode_bw_finish(const mfnerf_grid_desc* desc, float* grad_table
 int mfnerf_adam_step_fixed(float* params, float* grads, float* m, float* v, void* p_f16, int64_t n,
                            int64_t table_offset, const mfnerf_grid_desc* desc, void* workspace,
                            float* level_l1, float lr, float beta1, float beta2, float eps,
-                           int32_t* step_dev, const float* lr_dev, int32_t* skip, mfnerf_stream_t stream) {
+                           int32_t* step_dev, const float* lr_dev, mfnerf_amp_state* amp, mfnerf_stream_t stream) {
     int st = check_desc(desc, "adam_step_fixed");
     if (st) return st;
     if (!params || !grads || !m || !v || !step_dev || !level_l1) {
@@ -708,8 +711,9 @@ int mfnerf_adam_step_fixed(float* params, float* grads, float* m, float* v, void
     const int64_t want = div_up<int64_t>(n / 4, 256);
     hipLaunchKernelGGL(adam_fixed_kernel, dim3((unsigned)(want < 4096 ? (want < 1 ? 1 : want) : 4096)), dim3(256), 0,
                        stream, params, grads, m, v, (__half*)p_f16, n, table_offset, (int*)workspace, 2 * dense,
-                       total, *desc, level_l1, lr, beta1, beta2, eps, step_dev, lr_dev, skip);
-    hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, skip, level_l1, desc->n_levels);
+                       total, *desc, level_l1, lr, beta1, beta2, eps, step_dev, lr_dev, amp, desc->n_levels);
+    if (!amp)  // else the kernel's last workgroup did it
+        hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, amp, level_l1, desc->n_levels);
     return mfn_check_launch("adam_step_fixed");
 }
 
@@ -733,19 +737,25 @@ __global__ __launch_bounds__(256) void level_l1_kernel(const float* __restrict__
     __syncthreads();
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     const int row = 2 * L;
-    // thread t handles column pair (level) l = t % L of rows t / L, t / L + stride/L, ...
-    const int l = threadIdx.x % L;
-    const int64_t r0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / L;
-    const int64_t rstride = ((int64_t)gridDim.x * blockDim.x) / L;
+    // flat (row, level) pairs f = t + k*S over the grid's first S = floor(threads / L) * L threads:
+    // S is a multiple of L, so thread t always sees level l = t % L (any L, not only divisors of 64)
+    const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t S = ((int64_t)gridDim.x * blockDim.x / L) * L;
+    const int l = (int)(gt % L);
     float acc = 0.0f;
-    if ((int)threadIdx.x < (int)(blockDim.x / L) * L)
-        for (int64_t r = r0; r < nn; r += rstride) {
-            const float2 v = *reinterpret_cast<const float2*>(dy + r * row + 2 * l);
+    if (gt < S)
+        for (int64_t f = gt; f < nn * L; f += S) {
+            const float2 v = *reinterpret_cast<const float2*>(dy + (f / L) * row + 2 * l);
             acc += fabsf(v.x) + fabsf(v.y);
         }
-    // reduce the 256/L lanes of each level inside the wave first (lanes l, l+L, ... share a level)
-    for (int off = 32; off >= L; off >>= 1) acc += __shfl_xor(acc, off, 64);
-    if ((threadIdx.x & 63) < L) atomicAdd(&part[l], acc);
+    if (64 % L == 0 && (blockDim.x % L) == 0) {
+        // L divides the wave and the block: lanes l, l+L, ... of a wave share level l (block-local
+        // lane index = global index mod L); reduce inside the wave first
+        for (int off = 32; off >= L; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        if ((threadIdx.x & 63) < L) atomicAdd(&part[l], acc);
+    } else if (gt < S) {
+        atomicAdd(&part[l], acc);
+    }
     __syncthreads();
     if (threadIdx.x < L) atomicAdd(out + threadIdx.x, part[threadIdx.x]);
 }

@@ -293,7 +293,7 @@ class DeviceDataset:
         assert self.poses.shape == (self.n_img, 3, 4) and self.directions.shape == (self.hw, 3)
         self.seed = int(seed)
         self.same_image = {"all_images": 0, "same_image": 1}[strategy]
-        self.calls = torch.zeros(1, dtype=torch.int64, device=device)  # device draw counter
+        self.calls = torch.zeros(2, dtype=torch.int64, device=device)  # device draw counter + its launch ticket
 
     @classmethod
     def from_dataset(cls, ds, device="cuda", **kw):

@@ -56,6 +56,11 @@ class StepConfig:
     max_samples: int = MAX_SAMPLES
     n_parts: int = 1
     skip_nonfinite: bool = True  # GradScaler semantics: no optimizer step on an inf/nan gradient
+    # PL precision=16 (train.py:287) = torch GradScaler defaults: init 2^16, x2 after 2000 clean steps,
+    # x0.5 on an overflow; dynamic_loss_scale=False keeps a fixed 2^(floor(log2 n_rays)-2) instead
+    dynamic_loss_scale: bool = True
+    loss_scale: float = 65536.0
+    growth_interval: int = 2000
     fixed_point_grid: bool = True  # table gradient by int32 fixed-point atomics (n_parts == 1)
 
 
@@ -118,7 +123,10 @@ class TrainStep:
         self.v = torch.zeros(self.n_alloc, device=dev)
         self.p16 = self.params.half()
         self.shard = None  # (rank, lo, hi) once shard_optimizer() is on
-        self.finite_status = torch.zeros(2, dtype=torch.int32, device=dev)  # [non-finite flag, skipped steps]
+        # mfnerf_amp_state: [non-finite flag, skipped steps, scale, growth tracker, growth interval,
+        # growth factor, backoff factor, ticket] (include/mfnerf.h)
+        self.finite_status = torch.zeros(8, dtype=torch.int32, device=dev)
+        self.reset_loss_scale()
         self.packed = torch.empty(load().mfnerf_field_packed_bytes(c.rgb_width) // 2, dtype=torch.float16,
                                   device=dev)
         self._pack()
@@ -151,10 +159,34 @@ class TrainStep:
         self._use(self.mbuf[0])
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(seed + 1)
-        # fp16 backward scale: per-sample grads are O(1/n_rays); 2^(floor(log2 N)-2) keeps them normal
+        # static fp16 backward scale: per-sample grads are O(1/n_rays); 2^(floor(log2 N)-2) keeps them
+        # normal.  With the dynamic scale (default) field_bw reads amp.scale on the device instead.
         self.grad_scale = float(2.0 ** max(0, int(math.floor(math.log2(N))) - 2))
         self._primed = False
         self.dataset = None
+
+    def reset_loss_scale(self, scale=None):
+        """(Re)initialise the device GradScaler state (mfnerf_amp_state) from the config."""
+        c = self.cfg
+        a = torch.zeros(8, dtype=torch.int32)
+        af = a.view(torch.float32)
+        af[2] = float(c.loss_scale if scale is None else scale)
+        a[4] = int(c.growth_interval) if c.dynamic_loss_scale else 0
+        af[5], af[6] = 2.0, 0.5
+        self.finite_status.copy_(a.to(self.dev))
+
+    def _amp_on(self):
+        """GradScaler bookkeeping on the device: the skip (and, dynamic, the scale update)."""
+        return self.cfg.skip_nonfinite or self.cfg.dynamic_loss_scale
+
+    def _amp_ptr(self):
+        return ptr(self.finite_status) if self._amp_on() else None
+
+    def loss_scale(self):
+        """The loss scale the next backward uses (host read)."""
+        if not self.cfg.dynamic_loss_scale:
+            return self.grad_scale
+        return float(self.finite_status.view(torch.float32)[2])
 
     def attach_dataset(self, ds):
         """Draw every step's batch on the device from ds (mfnerf.data.DeviceDataset): run() and
@@ -368,9 +400,9 @@ class TrainStep:
                  ptr(t.depth), ptr(t.rgb), Np, cap, c.T_threshold, ptr(t.dsig), ptr(t.drgb_s), s)
             mark("composite_bw")
         call("mfnerf_field_bw", ptr(t.feat), cap, ptr(m.dirs), cap, ptr(m.counter), ptr(self.packed), c.rgb_width,
-             ptr(t.dsig), ptr(t.drgb_s), self.grad_scale, ptr(t.dfeat), ptr(t.mlp_grad),
+             ptr(t.dsig), ptr(t.drgb_s), 0.0 if c.dynamic_loss_scale else self.grad_scale, ptr(t.dfeat), ptr(t.mlp_grad),
              ptr(t.mlp_grad[self.off_rgb:]), ptr(t.field_ws),
-             ptr(self.finite_status) if c.skip_nonfinite else None,
+             self._amp_ptr(),
              ptr(self._level_l1) if self._fixed() else None, s)
         mark("field_bw")
 
@@ -406,7 +438,7 @@ class TrainStep:
         c = self.cfg
         call("mfnerf_adam_step", ptr(self.params[lo:hi]), ptr(grads), ptr(self.m), ptr(self.v), ptr(self.p16[lo:hi]),
              hi - lo, float(c.lr), 0.9, 0.999, c.eps, 1.0, 0, ptr(self.step_dev), ptr(self.lr_dev),
-             ptr(self.finite_status) if c.skip_nonfinite else None, int(zero_grads), stream())
+             self._amp_ptr(), int(zero_grads), stream())
 
     def _finish_update(self):
         """Unsharded, no exchange, fixed-point table gradient: the finish (convert) and Adam in one
@@ -415,7 +447,7 @@ class TrainStep:
         call("mfnerf_adam_step_fixed", ptr(self.params), ptr(self.grads), ptr(self.m), ptr(self.v), ptr(self.p16),
              self.n_alloc, self.off_table, self.desc, ptr(self.parts[0].grid_ws), ptr(self._level_l1),
              float(c.lr), 0.9, 0.999, c.eps, ptr(self.step_dev), ptr(self.lr_dev),
-             ptr(self.finite_status) if c.skip_nonfinite else None, stream())
+             self._amp_ptr(), stream())
         self._pack()
 
     def _update(self):
@@ -452,12 +484,12 @@ class TrainStep:
             rank, lo, hi = self.shard
             dp.sharded_update(self.grads, self.g_shard, self.p16, rank,
                               adam or (lambda g: self._shard_adam(lambda: self._adam(g, lo, hi, False))),
-                              flag=self.finite_status[:1] if self.cfg.skip_nonfinite else None)
+                              flag=self.finite_status[:1] if self._amp_on() else None)
             (pack or self._pack)()
         else:
             if exchange is not None:
                 # the non-finite flag rides the all-reduce: NaN in element 0 when set, read back
-                flag = self.finite_status[:1] if self.cfg.skip_nonfinite else None
+                flag = self.finite_status[:1] if self._amp_on() else None
                 if flag is not None:
                     call("mfnerf_flag_to_shards", ptr(self.grads), 1, self.n_alloc, ptr(flag), stream())
                 exchange(self.grads)

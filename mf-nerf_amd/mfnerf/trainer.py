@@ -6,11 +6,11 @@ the step.
   (train.py:154-157);
 * learning rate -- CosineAnnealingLR(T_max=num_epochs-1, eta_min=lr*0.01), stepped per epoch of
   1000 steps (train.py:136-142, datasets/base.py:17-20), held on the device (Adam reads it);
-* fp16 loss scaling -- PL precision=16 (train.py:287).  The engine runs the MLP backward in fp16
-  with a fixed power-of-two scale and un-scales inside the kernel, so there is no dynamic scale to
-  grow; what GradScaler adds beyond that -- skip the optimizer step when a gradient is not finite --
-  is done on the device every step (mfnerf_field_bw's non-finite flag feeding mfnerf_adam_step's skip; no
-  host synchronisation);
+* fp16 loss scaling -- PL precision=16 (train.py:287) = torch GradScaler: the MLP backward runs in
+  fp16 at the dynamic loss scale (init 2^16, x2 after 2000 clean steps, x0.5 on an overflow) and
+  un-scales inside the kernel; a step whose gradient is not finite is skipped.  All of it on the
+  device (mfnerf_field_bw's non-finite flag and device scale, the optimizer pass's last workgroup
+  running GradScaler.update(); mfnerf_amp_state) -- no host synchronisation;
 * metrics -- train loss / PSNR / rm_s (train.py:178-189), test PSNR with the test-time renderer
   (train.py:197-206), both read back only every `log_every` steps;
 * checkpoints -- the reference's state-dict keys (model.xyz_encoder.params, model.rgb_net.params,
@@ -210,8 +210,12 @@ class Trainer:
         st.params[st.off_rgb:st.off_table].copy_(rgb)
         st.p16.copy_(st.params.half())
         st._pack()
-        st.m.zero_()  # the reference's slim checkpoints carry no optimizer state
+        # the reference's slim checkpoints carry no optimizer state: it loads the weights before it
+        # builds FusedAdam (train.py:129,136), so the next update is Adam's step 1 with fresh moments
+        st.m.zero_()
         st.v.zero_()
+        st.step_dev.zero_()
+        st.adam_step = 0
         if "model.density_grid" in sd:
             st.density_grid.copy_(sd["model.density_grid"].to(st.dev))
         if "model.density_bitfield" in sd:

@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, f"{s} has no ctypes signature"
-    assert _lib.load().mfnerf_abi_version() == 1
+    assert _lib.load().mfnerf_abi_version() == 2
 
 
 def test_ops_reject_cpu_tensors_like_check_input():

@@ -236,6 +236,43 @@ def test_field_bw(gpu, wscale, sig_on, width):
         assert cos > 0.9995, cos
 
 
+@pytest.mark.parametrize("width", [64, 128])
+def test_field_bw_truncexp_clamp(gpu, width):
+    """TruncExp (custom_functions.py:162-173): sigma = exp(h0) forward, dL/dh0 = g * exp(clamp(h0,
+    -15, 15)) backward.  The xyz head's output row 0 is scaled so that h0 spans about +-40: the
+    clamped branch is taken on both sides, and the unclamped exp would overflow the fp16 backward at
+    this loss scale (exp(40) * g * S >> 65504; clamped, W2^T dh stays below it)."""
+    N = 4000
+    feat, dirs, px, pr = _field_inputs(N, seed=21, wscale=1.0, width=width)
+    px = px.clone()
+    px[2048:2048 + 64] *= 60.0  # W2 row 0 -> h0
+    g = torch.Generator().manual_seed(22)
+    dsig = torch.randn(N, generator=g) * 1e-6
+    drgb = torch.randn(N, 3, generator=g) * 1e-3
+    S = 8.0
+    sig_ref, _, acts = FO.ngp_field_fw16(feat, dirs, px, pr, width)
+    h0 = acts["h"][:, 0]
+    assert int((h0 > 15).sum()) > N // 10 and int((h0 < -15).sum()) > 40, "clamp branch not exercised"
+    ref16 = FO.ngp_field_bw16(acts, dsig, drgb, S)
+    packed = FLD.pack_field_weights(px.to(gpu), pr.to(gpu), width)
+    s, _ = FLD.field_fw(feat.to(gpu), dirs.to(gpu), N, packed, width)
+    assert torch.allclose(s.cpu(), sig_ref, rtol=4e-3, atol=1e-6)  # exp(h0), not clamped, forward
+    dfeat = torch.empty(N, 32, device=gpu)
+    gx, gr = torch.zeros(3072, device=gpu), torch.zeros(FLD.rgb_net_params(width), device=gpu)
+    flag = torch.zeros(2, dtype=torch.int32, device=gpu)
+    FLD.field_bw(feat.to(gpu), dirs.to(gpu), N, packed, dsig.to(gpu), drgb.to(gpu), S, dfeat, gx, gr,
+                 FLD.field_bw_workspace(N, width, gpu), width, nonfinite=flag)
+    torch.cuda.synchronize()
+    assert int(flag[0]) == 0 and torch.isfinite(dfeat).all()
+    for got, r16 in zip((dfeat.cpu(), gx.cpu(), gr.cpu()), ref16):
+        err = float((got - r16).abs().max() / r16.abs().max())
+        assert err < 2e-3, err
+    # the samples beyond the clamp: their dL/dh0 term is g*exp(+-15) exactly as the oracle's
+    big = (h0.abs() > 15)
+    err = float((dfeat.cpu()[big] - ref16[0][big]).abs().max() / ref16[0][big].abs().max())
+    assert err < 2e-3, err
+
+
 @pytest.mark.parametrize("name,args", [_layouts()[0], _layouts()[2]])
 def test_planar_encode_and_field_match_row_major(gpu, name, args):
     """The training path's level-major encode (XCD-partitioned, paired x-corner loads) equals the
