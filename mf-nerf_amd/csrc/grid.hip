@@ -239,13 +239,13 @@ __device__ __forceinline__ float table_fixed_scale(const mfnerf_grid_desc& D, co
     return fixed_scale(l1);
 }
 
+// the scatter as workgroup `bid` of `nblk` (a launch of its own, or a share of a fused launch)
 template <int ABLATE, int MAXL, bool FIX>
-__global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restrict__ X, int64_t n,
-                                                             const int32_t* __restrict__ n_dev, float x_min,
-                                                             float x_range, const mfnerf_grid_desc D,
-                                                             const float* __restrict__ dy, float* __restrict__ grad,
-                                                             float* __restrict__ priv, int64_t dense_entries,
-                                                             const float* __restrict__ level_l1) {
+__device__ __forceinline__ void grid_bw_body(int bid, int nblk, const float* __restrict__ X, int64_t n,
+                                             const int32_t* __restrict__ n_dev, float x_min, float x_range,
+                                             const mfnerf_grid_desc& D, const float* __restrict__ dy,
+                                             float* __restrict__ grad, float* __restrict__ priv,
+                                             int64_t dense_entries, const float* __restrict__ level_l1, int l_end) {
     // dL/dy of the wave's chunk (16 samples x 2L floats) is staged in LDS (rows padded by one
     // float: conflict-free column reads) and the NEXT chunk is prefetched into registers before
     // this chunk's atomics are issued.  On gfx9 no-return atomics count in vmcnt, so a global load
@@ -263,8 +263,8 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restr
     }
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     const int64_t chunks = div_up<int64_t>(nn, 16);
-    const int64_t wave0 = ((int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x) >> 6;
-    const int64_t n_waves = ((int64_t)gridDim.x * ENC_BLOCK) >> 6;
+    const int64_t wave0 = ((int64_t)bid * ENC_BLOCK + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)nblk * ENC_BLOCK) >> 6;
     const int64_t n_vals = nn * row;
 
     float pf[MAXL / 2];  // this lane's share of a chunk's dL/dy
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restr
         const float z = valid ? (pz - x_min) / x_range : 0.0f;
         if (chunk + n_waves < chunks) fetch(chunk + n_waves);  // in flight during this chunk's atomics
         const float* srow = sdy + s * rs + f;
-        for (int l = 0; l < L_; ++l) {
+        for (int l = 0; l < l_end; ++l) {
             if (ABLATE == 2 && l > 5) continue;
             if (ABLATE == 3 && l < 10) continue;
             const float g = srow[2 * l];
@@ -329,6 +329,17 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restr
             }
         }
     }
+}
+
+template <int ABLATE, int MAXL, bool FIX>
+__global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restrict__ X, int64_t n,
+                                                             const int32_t* __restrict__ n_dev, float x_min,
+                                                             float x_range, const mfnerf_grid_desc D,
+                                                             const float* __restrict__ dy, float* __restrict__ grad,
+                                                             float* __restrict__ priv, int64_t dense_entries,
+                                                             const float* __restrict__ level_l1, int l_end) {
+    grid_bw_body<ABLATE, MAXL, FIX>(blockIdx.x, gridDim.x, X, n, n_dev, x_min, x_range, D, dy, grad, priv,
+                                    dense_entries, level_l1, l_end);
 }
 
 // fp16 variant (experiment / tcnn's grad_t = __half for F = 2): one lane adds BOTH features of a
@@ -596,6 +607,521 @@ int check_desc(const mfnerf_grid_desc* d, const char* what) {
     return MFN_OK;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Partitioned table-gradient scatter ("binned").  The hashed levels' tables are small (2^19 entries
+// = 4 MB of int32 pairs per level at the Lego config) and uniformly hit: every 64-B line receives
+// ~30 adds per step from unrelated rays, so no ordering of the samples lets memory-side atomics
+// merge them (tools/sim_scatter_requests.py: >= 3 requests per sample per fine level in any window
+// of a Morton-sorted batch, 0.13 distinct lines per sample over the whole batch).  Instead each
+// table is cut into 2^shift-entry partitions, every (sample, level, (y,z) corner row) becomes a
+// 12-B record routed to its partition by a counting sort, and one workgroup per partition sums its
+// records into an LDS image with integer LDS atomics (ds_add_u32: ~4 T adds/s chip-wide at random
+// addresses, tools/lds_atomic_probe.hip -- 20x ds_add_f32), then stores the image once.  The image
+// is int64 at 2^32 x the table's int32 fixed-point scale: each contribution keeps its fp32
+// precision, the sum is exact and order-free (bit-reproducible), and the stored int32 value (the
+// format grid_bw_kernel leaves for the finish / Adam pass) is rounded ONCE per entry -- finer than
+// grid_bw_kernel's one rounding per run-merged contribution.  Passes: count (per-block bin
+// histogram; in the same launch as the dense coarse levels' scatter, which stays on grid_bw_body:
+// few hot lines, private copies, in-wave run merging -- the two overlap) -> scan (per bin over
+// blocks) -> scatter (records) -> accumulate.
+// partitions of 2^shift entries, shift in [MIN_BIN_SHIFT, MAX_BIN_SHIFT] chosen per layout so that
+// there are >= ~1024 partitions (4 workgroups per CU); 2^11 entries = 32 KB of int64 pairs
+constexpr int MIN_BIN_SHIFT = 8, MAX_BIN_SHIFT = 11, MAX_BIN_ENTRIES = 1 << MAX_BIN_SHIFT;
+constexpr int MAX_BINS = 4096;
+constexpr int BIN_BLOCKS = 1024;  // max count workgroups (sub-units): the counts array's stride
+constexpr int ACC_THREADS = 512;
+
+struct BinPlan {
+    int n_binned;                    // levels routed through the bins
+    int n_bins;                      // partitions over all their tables
+    int n_tables;
+    int shift;                       // partition = 2^shift entries of one table
+    int blocks;                      // count / scatter work units (<= BIN_BLOCKS)
+    int pair_ok;                     // no x-pair can straddle two partitions (one record per row)
+    int level[MFN_MAX_LEVELS];       // binned level list
+    int pairable[MFN_MAX_LEVELS];    // per level: x+1's entry = x's entry ^ (x ^ (x+1)) (own power-of-two hash)
+    int table_of[MFN_MAX_LEVELS];    // per level: its table
+    uint32_t t_offset[MFN_MAX_LEVELS], t_size[MFN_MAX_LEVELS];
+    int t_bin0[MFN_MAX_LEVELS + 1];  // first bin of each table; t_bin0[n_tables] = n_bins
+};
+
+__device__ __forceinline__ int bin_table(const BinPlan& P, int b) {
+    int t = 0;
+    while (t + 1 < P.n_tables && b >= P.t_bin0[t + 1]) ++t;
+    return t;
+}
+
+// The records of one (sample, binned level j): up to 4 (y,z) rows x (1 or 2 records).  EMIT(bin,
+// rec) is called per record; rec = {w0, a, b} (12 B), a/b = wy*wz*dL/dy_f * scale * 2^32 (scale:
+// the table's int32 fixed-point scale) and
+//   w0 = e0 (bits 0-10, entry in the bin) | t << 11 (4 bits) | single << 15 | sel << 16 | fx << 17,
+// fx = the x weight as 15-bit unorm (exact for the fine levels, whose positions carry <= 13
+// fraction bits).  A pair record adds (1-fx)(a,b) to e0 and fx(a,b) to e1 = e0 ^ (2^(t+1) - 1): an
+// own power-of-two hash table has idx(x+1) = idx(x) ^ (x ^ (x+1)), t = trailing ones of x, and the
+// two share a bin unless the carry reaches bit `shift` (1 x in 2^shift).  Otherwise (shared
+// MixedFeature tables, straddles) each entry gets a single record with weight sel ? fx : 1-fx.
+template <typename EMIT>
+__device__ __forceinline__ void level_records(const mfnerf_grid_desc& D, const BinPlan& P, int j, float x, float y,
+                                              float z, float g0, float g1, float fs, EMIT&& emit) {
+    const int l = P.level[j];
+    const int t = P.table_of[l];
+    const int bin0 = P.t_bin0[t];
+    const LevelGeo Lg = level_geo(D.scale[l], x, y, z);
+    const uint32_t fxq = min(32767u, (uint32_t)rintf(Lg.w[0] * 32768.0f)) << 17;
+    const uint32_t ones = (uint32_t)__builtin_ctz(~Lg.g[0]);  // trailing ones of x
+    const bool pair_hash = P.pairable[l] && ones < 15;
+    const float s0 = g0 * fs * 4294967296.0f, s1 = g1 * fs * 4294967296.0f;  // exact: powers of two
+    const uint32_t mask = (1u << P.shift) - 1;
+#pragma unroll
+    for (int yz = 0; yz < 4; ++yz) {
+        const uint32_t gy = Lg.g[1] + (yz & 1), gz = Lg.g[2] + (yz >> 1);
+        const float wy = (yz & 1) ? Lg.w[1] : 1.0f - Lg.w[1];
+        const float wz = (yz >> 1) ? Lg.w[2] : 1.0f - Lg.w[2];
+        const float wyz = wy * wz;
+        const uint32_t i0 = corner_index(D, l, Lg.g[0], gy, gz);
+        const uint32_t i1 = corner_index(D, l, Lg.g[0] + 1, gy, gz);
+        const int b0 = bin0 + (int)(i0 >> P.shift), b1 = bin0 + (int)(i1 >> P.shift);
+        const uint32_t a = __float_as_uint(wyz * s0), b = __float_as_uint(wyz * s1);
+        if (pair_hash && b0 == b1) {
+            emit(b0, make_uint3((i0 & mask) | (ones << 11) | fxq, a, b));
+        } else {
+            emit(b0, make_uint3((i0 & mask) | (1u << 15) | fxq, a, b));
+            emit(b1, make_uint3((i1 & mask) | (1u << 15) | (1u << 16) | fxq, a, b));
+        }
+    }
+}
+
+// Work units of the count and scatter passes: unit u of P.blocks owns the contiguous samples
+// [c0, c1) of the live count, so its records of one bin form one contiguous run in the bin; the
+// count pass splits each unit into SUBUNITS workgroups (contiguous sub-ranges, consecutive in the
+// scan), so a unit's run starts at its first sub-unit's offset.
+constexpr int SUBUNITS = 4;
+__device__ __forceinline__ void unit_range(int u, int nu, int64_t nn, int64_t& c0, int64_t& c1) {
+    c0 = nn * u / nu;
+    c1 = nn * (u + 1) / nu;
+}
+
+// the records of sample i at binned level j (nothing for a zero dL/dy: terminated samples)
+template <typename EMIT>
+__device__ __forceinline__ void sample_records(const mfnerf_grid_desc& D, const BinPlan& P, const float* __restrict__ X,
+                                               float x_min, float x_range, const float* __restrict__ dy,
+                                               const float* fs_s, int64_t i, int j, EMIT&& emit) {
+    const int l = P.level[j];
+    const float2 g = *reinterpret_cast<const float2*>(dy + i * (2 * D.n_levels) + 2 * l);
+    if (g.x == 0.0f && g.y == 0.0f) return;
+    const float x = (X[3 * i] - x_min) / x_range;
+    const float y = (X[3 * i + 1] - x_min) / x_range;
+    const float z = (X[3 * i + 2] - x_min) / x_range;
+    level_records(D, P, j, x, y, z, g.x, g.y, fs_s[l], emit);
+}
+
+// A sample staged in registers for all its binned levels (loaded once, then walked level by level):
+// normalised position and dL/dy of levels first_binned .. first_binned + n_binned - 1 (the binned
+// levels are the last ones: every level after the dense prefix).
+constexpr int MAX_BINNED = 16;
+struct StagedSample {
+    float x, y, z;
+    float g[2 * MAX_BINNED];
+};
+
+__device__ __forceinline__ void stage_sample(const mfnerf_grid_desc& D, const BinPlan& P, const float* __restrict__ X,
+                                             float x_min, float x_range, const float* __restrict__ dy, int64_t i,
+                                             StagedSample& S) {
+    S.x = (X[3 * i] - x_min) / x_range;
+    S.y = (X[3 * i + 1] - x_min) / x_range;
+    S.z = (X[3 * i + 2] - x_min) / x_range;
+    const float2* src = reinterpret_cast<const float2*>(dy + i * (2 * D.n_levels) + 2 * P.level[0]);
+#pragma unroll
+    for (int j = 0; j < MAX_BINNED; ++j) {
+        const float2 v = j < P.n_binned ? src[j] : make_float2(0.f, 0.f);
+        S.g[2 * j] = v.x;
+        S.g[2 * j + 1] = v.y;
+    }
+}
+
+template <typename EMIT>
+__device__ __forceinline__ void staged_records(const mfnerf_grid_desc& D, const BinPlan& P, const StagedSample& S,
+                                               const float* fs_s, int j, EMIT&& emit) {
+    float g0 = 0.f, g1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAX_BINNED; ++k)  // register-indexed select (j is uniform)
+        if (k == j) { g0 = S.g[2 * k]; g1 = S.g[2 * k + 1]; }
+    if (g0 == 0.0f && g1 == 0.0f) return;  // terminated samples: nothing to add
+    level_records(D, P, j, S.x, S.y, S.z, g0, g1, fs_s[P.level[j]], emit);
+}
+
+__device__ __forceinline__ void load_fixed_scales(const mfnerf_grid_desc& D, const float* __restrict__ level_l1,
+                                                  float* fs_s) {
+    if ((int)threadIdx.x < D.n_levels) fs_s[threadIdx.x] = table_fixed_scale(D, level_l1, threadIdx.x);
+}
+
+// pass 1: per-block histogram over the bins -> counts[bin * BIN_BLOCKS + block], fused with the
+// dense levels' atomic scatter: workgroups [0, n_dense) run grid_bw_body on the dense levels, the
+// next P.blocks count (the two overlap: one waits on memory-side atomics, the other computes)
+template <int MAXL>
+__global__ __launch_bounds__(256) void bin_count_dense_kernel(const float* __restrict__ X, int64_t n,
+                                                              const int32_t* __restrict__ n_dev, float x_min,
+                                                              float x_range, const mfnerf_grid_desc D, const BinPlan P,
+                                                              const float* __restrict__ dy,
+                                                              const float* __restrict__ level_l1,
+                                                              int32_t* __restrict__ counts, int n_dense, float* grad,
+                                                              float* priv, int64_t dense_entries, int l_end) {
+    if ((int)blockIdx.x < n_dense) {
+        grid_bw_body<0, MAXL, true>(blockIdx.x, n_dense, X, n, n_dev, x_min, x_range, D, dy, grad, priv,
+                                    dense_entries, level_l1, l_end);
+        return;
+    }
+    const int bid = blockIdx.x - n_dense;  // sub-unit: SUBUNITS per scatter unit
+    __shared__ int hist[MAX_BINS];
+    __shared__ float fs_s[MFN_MAX_LEVELS];
+    for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x) hist[b] = 0;
+    load_fixed_scales(D, level_l1, fs_s);
+    __syncthreads();
+    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
+    int64_t c0, c1;
+    unit_range(bid, P.blocks * SUBUNITS, nn, c0, c1);
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+        StagedSample S;
+        stage_sample(D, P, X, x_min, x_range, dy, i, S);
+        for (int j = 0; j < P.n_binned; ++j)
+            staged_records(D, P, S, fs_s, j, [&](int bin, uint3) { atomicAdd(&hist[bin], 1); });
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x) counts[(int64_t)b * BIN_BLOCKS + bid] = hist[b];
+}
+
+// pass 2: per bin, exclusive scan of its per-block counts (in place) and the bin's total
+__global__ __launch_bounds__(256) void bin_scan_kernel(int32_t* __restrict__ counts, int32_t* __restrict__ bin_total,
+                                                       int blocks) {
+    __shared__ int part[256];
+    int32_t* c = counts + (int64_t)blockIdx.x * BIN_BLOCKS;
+    constexpr int PER = BIN_BLOCKS / 256;
+    const int nblk = blocks;
+    int v[PER], sum = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        v[k] = threadIdx.x * PER + k < nblk ? c[threadIdx.x * PER + k] : 0;
+        sum += v[k];
+    }
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {  // Hillis-Steele inclusive scan of the 256 partials
+        const int add = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+        __syncthreads();
+        part[threadIdx.x] += add;
+        __syncthreads();
+    }
+    int run = part[threadIdx.x] - sum;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        if (threadIdx.x * PER + k < nblk) c[threadIdx.x * PER + k] = run;
+        run += v[k];
+    }
+    if (threadIdx.x == 255) bin_total[blockIdx.x] = part[255];
+}
+
+// exclusive block scan of v[0, n) (n <= 4 * blockDim.x, blockDim.x <= 1024) into out; returns the total
+__device__ __forceinline__ int block_scan(const int* v, int n, int* out) {
+    __shared__ int part[1024];
+    const int per = (n + (int)blockDim.x - 1) / (int)blockDim.x;
+    const int lo = threadIdx.x * per;
+    int sum = 0;
+    for (int k = 0; k < per && lo + k < n; ++k) sum += v[lo + k];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int off = 1; off < (int)blockDim.x; off <<= 1) {
+        const int add = (int)threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+        __syncthreads();
+        part[threadIdx.x] += add;
+        __syncthreads();
+    }
+    int run = part[threadIdx.x] - sum;
+    const int total = part[blockDim.x - 1];
+    for (int k = 0; k < per && lo + k < n; ++k) {
+        const int x = v[lo + k];
+        out[lo + k] = run;
+        run += x;
+    }
+    __syncthreads();
+    return total;
+}
+
+// exclusive scan of bin_total[0, nb) into LDS (block-wide)
+__device__ __forceinline__ void scan_bins(const int32_t* __restrict__ bin_total, int nb, int* start) {
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) start[b] = bin_total[b];
+    __syncthreads();
+    block_scan(start, nb, start);
+}
+
+// exclusive scan over the block (one value per thread, blockDim <= 1024): wave scans by lane
+// shuffles, then the wave totals; out[threadIdx.x] = this thread's offset.  Returns the total.
+__device__ __forceinline__ int wave_block_scan(int v, int* out) {
+    __shared__ int wsum[16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    const int nw = (int)(blockDim.x + 63) >> 6;
+    int before = 0, total = 0;
+    for (int k = 0; k < nw; ++k) {
+        const int t = wsum[k];
+        before += k < w ? t : 0;
+        total += t;
+    }
+    out[threadIdx.x] = before + x - v;
+    __syncthreads();
+    return total;
+}
+
+// pass 3: the records.  Unit u (one 1024-thread workgroup) walks its samples level by level in
+// tiles of up to 2048 samples: the tile's records are counted per bin of the level's table
+// (LDS atomics give each its rank), sorted by bin in LDS and stored as one contiguous run per bin
+// at the bin's cursor (bin start + the unit's offset in the bin + what earlier tiles stored): ~30
+// records per run at the Lego config, whole-line stores instead of one scattered store per record.
+constexpr int SC_THREADS = 1024;
+constexpr int MAX_TBINS = 1024;              // bins of one table
+constexpr int SC_STAGE = SC_THREADS * 8;     // staged records per tile (8 per thread)
+
+__global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __restrict__ X, int64_t n,
+                                                                 const int32_t* __restrict__ n_dev, float x_min,
+                                                                 float x_range, const mfnerf_grid_desc D,
+                                                                 const BinPlan P, const float* __restrict__ dy,
+                                                                 const float* __restrict__ level_l1,
+                                                                 const int32_t* __restrict__ counts,
+                                                                 const int32_t* __restrict__ bin_start,
+                                                                 uint3* __restrict__ rec, int debug_no_store) {
+    __shared__ int cursor[MAX_BINS];
+    __shared__ int thist[MAX_TBINS], toff[MAX_TBINS], gdst[MAX_TBINS];
+    __shared__ uint3 stage[SC_STAGE];
+    __shared__ uint16_t sbin[SC_STAGE];
+    __shared__ float fs_s[MFN_MAX_LEVELS];
+    load_fixed_scales(D, level_l1, fs_s);
+    // this unit's write position in each bin: the bin's start + the unit's first sub-unit's offset
+    for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x)
+        cursor[b] = bin_start[b] + counts[(int64_t)b * BIN_BLOCKS + blockIdx.x * SUBUNITS];
+    __syncthreads();
+    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
+    int64_t c0, c1;
+    unit_range(blockIdx.x, gridDim.x, nn, c0, c1);
+    const int spt = P.pair_ok ? 2 : 1;  // samples per thread per tile: <= 8 records each per level
+    for (int64_t base = c0; base < c1; base += (int64_t)spt * SC_THREADS) {
+        StagedSample S[2];
+        bool live[2] = {false, false};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int64_t i = base + (int64_t)q * SC_THREADS + threadIdx.x;
+            live[q] = q < spt && i < c1;
+            if (live[q]) stage_sample(D, P, X, x_min, x_range, dy, i, S[q]);
+        }
+        for (int j = 0; j < P.n_binned; ++j) {
+            const int t = P.table_of[P.level[j]];
+            const int b0 = P.t_bin0[t], tb = P.t_bin0[t + 1] - b0;
+            for (int k = threadIdx.x; k < tb; k += SC_THREADS) thist[k] = 0;
+            __syncthreads();
+            int nr = 0, lr[8];  // (local bin, rank) packed: bin << 16 | rank
+            uint3 rr[8];
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                if (live[q])
+                    staged_records(D, P, S[q], fs_s, j, [&](int bin, uint3 r) {
+                        const int lb = bin - b0;
+                        lr[nr] = (lb << 16) | atomicAdd(&thist[lb], 1);
+                        rr[nr++] = r;
+                    });
+            __syncthreads();
+            // bins -> sorted tile offsets (toff) and global destinations (gdst + sorted index)
+            const int cnt = (int)threadIdx.x < tb ? thist[threadIdx.x] : 0;
+            const int total = wave_block_scan(cnt, toff);
+            if ((int)threadIdx.x < tb) {
+                const int c = cursor[b0 + threadIdx.x];
+                gdst[threadIdx.x] = c - toff[threadIdx.x];
+                cursor[b0 + threadIdx.x] = c + cnt;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (q < nr) {
+                    const int lb = lr[q] >> 16;
+                    const int p = toff[lb] + (lr[q] & 0xFFFF);
+                    stage[p] = rr[q];
+                    sbin[p] = (uint16_t)lb;
+                }
+            __syncthreads();
+            for (int k = threadIdx.x; k < total; k += SC_THREADS)
+                if (!debug_no_store) rec[gdst[sbin[k]] + k] = stage[k];
+            __syncthreads();
+        }
+    }
+}
+
+// bin_start = exclusive scan of bin_total (one workgroup)
+__global__ __launch_bounds__(1024) void bin_start_kernel(const int32_t* __restrict__ bin_total, int nb,
+                                                         int32_t* __restrict__ bin_start) {
+    __shared__ int v[MAX_BINS];
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) v[b] = bin_total[b];
+    __syncthreads();
+    block_scan(v, nb, v);
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) bin_start[b] = v[b];
+}
+
+// pass 4: one workgroup per bin: sum the bin's records into an LDS image of its entries (int64
+// pairs, ds_add_u64), then store it rounded to int32.
+__device__ __forceinline__ int round_shift32(long long v) { return (int)((v + 0x80000000ll) >> 32); }
+
+// float -> int64 for |v| < 2^62: below 2^31 round to nearest; above, v is an integer: its 24-bit
+// mantissa shifted into place (cheaper than the library's float -> long long)
+__device__ __forceinline__ long long f2ll(float v) {
+    int e;
+    const float m = frexpf(v, &e);  // v = m * 2^e, 0.5 <= |m| < 1
+    if (e <= 30) return (long long)(int)rintf(v);
+    return (long long)(int)(m * 1073741824.0f) * (1ll << (e - 30));
+}
+
+constexpr int ACC_UNROLL = 8;
+
+__global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, const uint3* __restrict__ rec,
+                                                                const int32_t* __restrict__ bin_start,
+                                                                const int32_t* __restrict__ bin_total,
+                                                                int* __restrict__ grad) {
+    __shared__ unsigned long long img[2 * MAX_BIN_ENTRIES];
+    const int bin = blockIdx.x;
+    const int n_ent = 1 << P.shift, mask = n_ent - 1;
+    for (int i = threadIdx.x; i < 2 * n_ent; i += blockDim.x) img[i] = 0;
+    __syncthreads();
+    const int64_t lo = bin_start[bin], hi = lo + bin_total[bin];
+    for (int64_t k0 = lo + threadIdx.x; k0 < hi; k0 += (int64_t)ACC_UNROLL * blockDim.x) {
+        uint3 r[ACC_UNROLL];
+#pragma unroll
+        for (int u = 0; u < ACC_UNROLL; ++u) {  // all loads in flight first
+            const int64_t k = k0 + (int64_t)u * blockDim.x;
+            r[u] = k < hi ? rec[k] : make_uint3(0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < ACC_UNROLL; ++u) {
+            const uint32_t w = r[u].x;
+            const float a = __uint_as_float(r[u].y), b = __uint_as_float(r[u].z);
+            if (a == 0.0f && b == 0.0f) continue;  // padding (or a zero contribution)
+            const float fx = (float)(w >> 17) * (1.0f / 32768.0f);
+            const int e0 = w & mask;
+            if (w & (1u << 15)) {  // single entry, weight sel ? fx : 1 - fx
+                const float wt = (w & (1u << 16)) ? fx : 1.0f - fx;
+                atomicAdd(&img[2 * e0], (unsigned long long)f2ll(wt * a));
+                atomicAdd(&img[2 * e0 + 1], (unsigned long long)f2ll(wt * b));
+            } else {
+                const int e1 = e0 ^ ((2 << ((w >> 11) & 15)) - 1);
+                const float w0 = 1.0f - fx;
+                // |values| < 2^62: exact in int64, order-free sums
+                atomicAdd(&img[2 * e0], (unsigned long long)f2ll(w0 * a));
+                atomicAdd(&img[2 * e0 + 1], (unsigned long long)f2ll(w0 * b));
+                atomicAdd(&img[2 * e1], (unsigned long long)f2ll(fx * a));
+                atomicAdd(&img[2 * e1 + 1], (unsigned long long)f2ll(fx * b));
+            }
+        }
+    }
+    __syncthreads();
+    const int t = bin_table(P, bin);
+    const int64_t e_lo = (int64_t)(bin - P.t_bin0[t]) << P.shift;
+    const int n_e = (int)min<int64_t>(n_ent, (int64_t)P.t_size[t] - e_lo);
+    int* dst = grad + 2 * ((int64_t)P.t_offset[t] + e_lo);
+    for (int i = threadIdx.x; i < 2 * n_e; i += blockDim.x) dst[i] = round_shift32((long long)img[i]);
+}
+
+// The plan for a desc: binned levels = every level that is not a dense own table; tables in address
+// order.  Returns the number of bins (0: nothing to bin), or -1 if over MAX_BINS.
+int bin_plan(const mfnerf_grid_desc* d, BinPlan* P) {
+    *P = BinPlan{};
+    P->pair_ok = 1;
+    uint64_t entries = 0, max_x = 0;
+    for (int l = 0; l < d->n_levels; ++l) {
+        const uint64_t r = d->res[l];
+        const bool dense = d->table_kind[l] == 0 && r * r * r <= d->size[l];
+        if (dense) continue;
+        int t = 0;
+        while (t < P->n_tables && P->t_offset[t] != d->offset[l]) ++t;
+        if (t == P->n_tables) {
+            P->t_offset[t] = d->offset[l];
+            P->t_size[t] = d->size[l];
+            P->n_tables++;
+            entries += d->size[l];
+        }
+        P->table_of[l] = t;
+        P->pairable[l] = d->table_kind[l] == 0 && (d->size[l] & (d->size[l] - 1)) == 0;
+        P->level[P->n_binned++] = l;
+        max_x = max(max_x, (uint64_t)(d->table_kind[l] == 1 ? (uint32_t)d->canon_res : d->res[l]));
+    }
+    // the largest partition (fewest records to route, least LDS per entry) leaving >= 1024 of them
+    P->shift = MAX_BIN_SHIFT;
+    while (P->shift > MIN_BIN_SHIFT && (entries >> P->shift) < 1024) --P->shift;
+    int nb = 0;
+    for (int t = 0; t < P->n_tables; ++t) {
+        P->t_bin0[t] = nb;
+        nb += (int)((P->t_size[t] + (1u << P->shift) - 1) >> P->shift);
+        // x-corner indices differ below the top bit of x ^ (x+1), x + 1 <= max_x, in an own power-of-two
+        // hash table: one record per row; otherwise up to two
+        if ((P->t_size[t] & (P->t_size[t] - 1)) || max_x >= (1ull << P->shift)) P->pair_ok = 0;
+    }
+    for (int j = 0; j < P->n_binned; ++j) {
+        if (!P->pairable[P->level[j]]) P->pair_ok = 0;
+    }
+    P->t_bin0[P->n_tables] = nb;
+    P->n_bins = nb;
+    // tuning knob (read once): MFNERF_BIN_BLOCKS
+    static const int knob_blocks = [] { const char* e = getenv("MFNERF_BIN_BLOCKS"); return e ? atoi(e) : 0; }();
+    P->blocks = knob_blocks >= 64 && knob_blocks * SUBUNITS <= BIN_BLOCKS ? knob_blocks : BIN_BLOCKS / SUBUNITS;
+    if (P->n_binned > MAX_BINNED) return -1;
+    for (int j = 1; j < P->n_binned; ++j)  // the binned levels are contiguous (staged dL/dy rows)
+        if (P->level[j] != P->level[0] + j) return -1;
+    for (int t = 0; t < P->n_tables; ++t)
+        if (P->t_bin0[t + 1] - P->t_bin0[t] > MAX_TBINS) return -1;
+    return nb > MAX_BINS ? -1 : nb;
+}
+
+// first level routed through the bins (the dense levels before it use grid_bw_kernel)
+int first_binned_level(const mfnerf_grid_desc* d) {
+    for (int l = 0; l < d->n_levels; ++l) {
+        const uint64_t r = d->res[l];
+        if (!(d->table_kind[l] == 0 && r * r * r <= d->size[l])) return l;
+    }
+    return d->n_levels;
+}
+
+struct BinWorkspace {
+    float* priv;
+    int32_t *counts, *bin_total, *bin_start;
+    uint3* rec;
+};
+
+int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
+
+// MFNERF_BIN_DEBUG_NO_STORE=1: the scatter pass computes and ranks its records but stores none
+// (timing experiments only: the accumulate then reads stale records)
+int bin_debug_no_store() {
+    static const int v = [] { const char* e = getenv("MFNERF_BIN_DEBUG_NO_STORE"); return e ? atoi(e) : 0; }();
+    return v;
+}
+
+// workspace = [private copies of the dense levels | counts | bin_total | bin_start | records]
+int64_t binned_workspace_layout(const mfnerf_grid_desc* d, int64_t n_max, char* base, BinWorkspace* W) {
+    BinPlan P;
+    if (bin_plan(d, &P) < 0) return -1;
+    int64_t off = align256((int64_t)GRAD_COPIES * dense_entries_of(d) * 2 * (int64_t)sizeof(float));
+    if (W) W->priv = reinterpret_cast<float*>(base);
+    const int64_t nb = P.n_bins > 0 ? P.n_bins : 1;
+    if (W) W->counts = reinterpret_cast<int32_t*>(base + off);
+    off += align256(nb * BIN_BLOCKS * 4);
+    if (W) W->bin_total = reinterpret_cast<int32_t*>(base + off);
+    off += align256(nb * 4);
+    if (W) W->bin_start = reinterpret_cast<int32_t*>(base + off);
+    off += align256(nb * 4);
+    if (W) W->rec = reinterpret_cast<uint3*>(base + off);
+    off += align256(n_max * P.n_binned * 4 * (P.pair_ok ? 1 : 2) * (int64_t)sizeof(uint3));
+    return off;
+}
+
 }  // namespace
 
 extern "C" {
@@ -651,11 +1177,12 @@ int mfnerf_grid_encode_bw_scatter(const float* x, int64_t n, const int32_t* n_de
     if (level_l1) {
         auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, true> : grid_bw_kernel<0, 16, true>;
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range,
-                           *desc, dL_dout, grad_table, (float*)workspace, dense, level_l1);
+                           *desc, dL_dout, grad_table, (float*)workspace, dense, level_l1, desc->n_levels);
     } else {
         auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, false> : grid_bw_kernel<0, 16, false>;
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range,
-                           *desc, dL_dout, grad_table, (float*)workspace, dense, (const float*)nullptr);
+                           *desc, dL_dout, grad_table, (float*)workspace, dense, (const float*)nullptr,
+                           desc->n_levels);
     }
     return mfn_check_launch("grid_encode_bw_scatter");
 }
@@ -799,8 +1326,64 @@ int mfnerf_debug_grid_bw_ablate(int mode, const float* x, int64_t n, const int32
              : mode == 3 ? grid_bw_kernel<3, 16, false>
                          : grid_bw_kernel<0, 16, false>;
     hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc,
-                       dL_dout, grad_table, nullptr, (int64_t)0, (const float*)nullptr);
+                       dL_dout, grad_table, nullptr, (int64_t)0, (const float*)nullptr, desc->n_levels);
     return mfn_check_launch("grid_bw_ablate");
+}
+
+// Partitioned (binned) fixed-point table-gradient scatter: the dense levels through grid_bw_kernel's
+// private copies, the hashed / shared tables through count -> scan -> scatter -> LDS accumulate.
+int64_t mfnerf_grid_encode_bw_binned_workspace(const mfnerf_grid_desc* desc, int64_t n_max) {
+    if (check_desc(desc, "grid_encode_bw_binned_workspace") || n_max < 0) return -1;
+    return binned_workspace_layout(desc, n_max, nullptr, nullptr);
+}
+
+int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                                 const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
+                                 void* workspace, const float* level_l1, mfnerf_stream_t stream) {
+    int st = check_desc(desc, "grid_encode_bw_binned");
+    if (st) return st;
+    if (n < 0) { mfn_set_error("grid_encode_bw_binned: bad size"); return MFN_ERR_INVALID; }
+    if (n == 0) return MFN_OK;
+    if (!x || !dL_dout || !grad_table || !workspace || !level_l1) {
+        mfn_set_error("grid_encode_bw_binned: null pointer (workspace and level_l1 are required)");
+        return MFN_ERR_INVALID;
+    }
+    BinPlan P;
+    if (bin_plan(desc, &P) < 0) {
+        mfn_set_error("grid_encode_bw_binned: more than %d partitions of %d entries", MAX_BINS, MAX_BIN_ENTRIES);
+        return MFN_ERR_INVALID;
+    }
+    if (n * (int64_t)P.n_binned >= (1ll << 31)) {
+        mfn_set_error("grid_encode_bw_binned: n * binned levels must be < 2^31"); return MFN_ERR_INVALID;
+    }
+    BinWorkspace W;
+    binned_workspace_layout(desc, n, (char*)workspace, &W);
+    // the dense levels (request-shaped int32 atomics into the private copies) and the bin histogram
+    // in one launch; then the scan, the records and the per-partition sums
+    const int l_end = first_binned_level(desc);
+    int n_dense = 0;
+    if (l_end > 0) {
+        const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16), ENC_BLOCK / 64);
+        const int64_t cap = grid_bw_block_cap();
+        n_dense = (int)(want < cap ? want : cap);
+    }
+    const int n_count = P.n_bins > 0 ? P.blocks * SUBUNITS : 0;
+    if (n_dense + n_count > 0) {
+        auto kern = desc->n_levels > 16 ? bin_count_dense_kernel<MFN_MAX_LEVELS> : bin_count_dense_kernel<16>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)(n_dense + n_count)), dim3(256), 0, stream, x, n, n_dev, x_min,
+                           x_range, *desc, P, dL_dout, level_l1, W.counts, n_dense, grad_table, W.priv,
+                           dense_entries_of(desc), l_end);
+    }
+    if (P.n_bins > 0) {
+        hipLaunchKernelGGL(bin_scan_kernel, dim3(P.n_bins), dim3(256), 0, stream, W.counts, W.bin_total,
+                           P.blocks * SUBUNITS);
+        hipLaunchKernelGGL(bin_start_kernel, dim3(1), dim3(1024), 0, stream, W.bin_total, P.n_bins, W.bin_start);
+        hipLaunchKernelGGL(bin_scatter_kernel, dim3(P.blocks), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
+                           *desc, P, dL_dout, level_l1, W.counts, W.bin_start, W.rec, bin_debug_no_store());
+        hipLaunchKernelGGL(bin_accum_kernel, dim3(P.n_bins), dim3(ACC_THREADS), 0, stream, P, W.rec,
+                           W.bin_start, W.bin_total, (int*)grad_table);
+    }
+    return mfn_check_launch("grid_encode_bw_binned");
 }
 
 }  // extern "C"

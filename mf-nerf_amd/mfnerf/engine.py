@@ -62,6 +62,9 @@ class StepConfig:
     loss_scale: float = 65536.0
     growth_interval: int = 2000
     fixed_point_grid: bool = True  # table gradient by int32 fixed-point atomics (n_parts == 1)
+    # ... of the hashed tables by partitioned LDS sums (mfnerf_grid_encode_bw_binned); MFNERF_BINNED=0
+    # selects the memory-side-atomic scatter for A/B measurements
+    binned_grid: bool = os.environ.get("MFNERF_BINNED", "1") == "1"
 
 
 @dataclass
@@ -223,7 +226,13 @@ class TrainStep:
         t.drgb_s = torch.empty(cap, 3, **f32)
         t.dfeat = torch.empty(cap, c.L * c.F, **f32)
         t.field_ws = torch.empty(load().mfnerf_field_bw_workspace(cap, c.rgb_width) // 4, **f32)
-        t.grid_ws = torch.zeros(max(16, load().mfnerf_grid_encode_bw_workspace(self.desc)) // 4, **f32)
+        if self._binned():
+            nb = load().mfnerf_grid_encode_bw_binned_workspace(self.desc, cap)
+            if nb < 0:
+                raise ValueError("grid layout unsupported by the binned table-gradient scatter")
+        else:
+            nb = load().mfnerf_grid_encode_bw_workspace(self.desc)
+        t.grid_ws = torch.zeros(max(16, nb) // 4, **f32)
         # parts > 0 accumulate their MLP weight grads privately (field_bw's slab sum is a plain +=)
         t.mlp_grad = self.grads[:self.off_table] if q == 0 else torch.zeros(self.off_table, **f32)
         return t
@@ -413,9 +422,18 @@ class TrainStep:
         float atomics."""
         return self.n_parts == 1 and self.cfg.fixed_point_grid
 
+    def _binned(self):
+        """The fixed-point table gradient by table partitions (one part only, like _fixed)."""
+        return self.cfg.n_parts == 1 and self.cfg.fixed_point_grid and self.cfg.binned_grid
+
     def _grid_bw(self, mb, q):
         """Part q's hash-table gradient scatter (the dominant kernel, alone so it can be timed)."""
         t, m = self.parts[q], mb.part[q]
+        if self._binned():
+            call("mfnerf_grid_encode_bw_binned", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min, self.x_range,
+                 self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws), ptr(self._level_l1),
+                 stream())
+            return
         call("mfnerf_grid_encode_bw_scatter", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min, self.x_range,
              self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws),
              ptr(self._level_l1) if self._fixed() else None, stream())

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from mfnerf import field as FLD
-from mfnerf._lib import call, ptr
+from mfnerf._lib import call, load, ptr
 from mfnerf.grid import GridLayout
 from oracle import field_oracle as FO
 
@@ -76,6 +76,18 @@ def test_grid_encode_fw_bw(gpu, name, args):
             assert int((ws != 0).sum()) == 0
         fx.append(gt)
     assert torch.equal(fx[0], fx[1]) and torch.equal(fx[0], fx[2])
+    # partitioned LDS scatter (the training path): same fixed point, bit-reproducible, workspace
+    # copies left zero
+    bn = []
+    for _ in range(2):
+        ws = FLD.grid_bw_binned_workspace(desc, N, gpu)
+        gt = torch.zeros(lay.n_params, device=gpu)
+        FLD.grid_encode_bw(xg, N, dyg, gt, lay, desc, workspace=ws, binned=True)
+        assert torch.allclose(gt.cpu(), gref, rtol=1e-4, atol=1e-4 * float(gref.abs().max()))
+        nc = load().mfnerf_grid_encode_bw_workspace(desc) // 4
+        assert int((ws[:nc] != 0).sum()) == 0
+        bn.append(gt)
+    assert torch.equal(bn[0], bn[1])
     m = 4099  # not a multiple of the 16-sample chunk: the live count comes from the device
     tp = table.clone().requires_grad_(True)
     (FO.grid_encode(x[:m], tp, olay) * dy[:m]).sum().backward()
@@ -85,6 +97,10 @@ def test_grid_encode_fw_bw(gpu, name, args):
             gt = torch.zeros(lay.n_params, device=gpu)
             FLD.grid_encode_bw(xg, N, dyg, gt, lay, desc, n_dev=n_dev, workspace=ws, fixed_point=fixed)
             assert torch.allclose(gt.cpu(), tp.grad, rtol=1e-4, atol=1e-4 * float(tp.grad.abs().max()))
+    gt = torch.zeros(lay.n_params, device=gpu)
+    FLD.grid_encode_bw(xg, N, dyg, gt, lay, desc, n_dev=n_dev, workspace=FLD.grid_bw_binned_workspace(desc, N, gpu),
+                       binned=True)
+    assert torch.allclose(gt.cpu(), tp.grad, rtol=1e-4, atol=1e-4 * float(tp.grad.abs().max()))
 
 
 def test_grid_encode_bw_along_rays(gpu):
@@ -104,10 +120,10 @@ def test_grid_encode_bw_along_rays(gpu):
     (FO.grid_encode(x, table, olay) * dy).sum().backward()
     gref = table.grad
     desc = lay.desc()
-    for fixed in (False, True):
+    for fixed, binned in ((False, False), (True, False), (True, True)):
         gt = torch.zeros(lay.n_params, device=gpu)
-        FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=FLD.grid_bw_workspace(desc, gpu),
-                           fixed_point=fixed)
+        ws = FLD.grid_bw_binned_workspace(desc, N, gpu) if binned else FLD.grid_bw_workspace(desc, gpu)
+        FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=ws, fixed_point=fixed, binned=binned)
         assert torch.allclose(gt.cpu(), gref, rtol=1e-4, atol=1e-4 * float(gref.abs().max()))
     # the training regime: per-sample gradients ~1e-7 of very different size per level; the
     # fixed-point resolution (2^-30 of each level's L1) stays far below fp32's relative error
@@ -115,16 +131,17 @@ def test_grid_encode_bw_along_rays(gpu):
     tp = torch.zeros(lay.n_params).requires_grad_(True)
     (FO.grid_encode(x, tp, olay).double() * dys.double()).sum().backward()
     gref = tp.grad.double()
-    gt = torch.zeros(lay.n_params, device=gpu)
-    FLD.grid_encode_bw(x.to(gpu), N, dys.to(gpu), gt, lay, desc, workspace=FLD.grid_bw_workspace(desc, gpu),
-                       fixed_point=True)
-    got = gt.cpu().double()
-    for l in range(16):
-        a, b = lay.offsets[l] * 2, lay.offsets[l + 1] * 2 if l + 1 < 16 else lay.n_params
-        scale = float(gref[a:b].abs().max())
-        if scale > 0:
-            err = float((got[a:b] - gref[a:b]).abs().max()) / scale
-            assert err < 1e-4, (l, err)
+    for binned in (False, True):
+        gt = torch.zeros(lay.n_params, device=gpu)
+        ws = FLD.grid_bw_binned_workspace(desc, N, gpu) if binned else FLD.grid_bw_workspace(desc, gpu)
+        FLD.grid_encode_bw(x.to(gpu), N, dys.to(gpu), gt, lay, desc, workspace=ws, fixed_point=True, binned=binned)
+        got = gt.cpu().double()
+        for l in range(16):
+            a, b = lay.offsets[l] * 2, lay.offsets[l + 1] * 2 if l + 1 < 16 else lay.n_params
+            scale = float(gref[a:b].abs().max())
+            if scale > 0:
+                err = float((got[a:b] - gref[a:b]).abs().max()) / scale
+                assert err < 1e-4, (binned, l, err)
 
 
 def test_grid_encode_bw_fixed_point_extreme_range(gpu):
@@ -141,12 +158,13 @@ def test_grid_encode_bw_fixed_point_extreme_range(gpu):
         tp = torch.zeros(lay.n_params).requires_grad_(True)
         (FO.grid_encode(x, tp, olay).double() * dy.double()).sum().backward()
         gref = tp.grad.double()
-        gt = torch.zeros(lay.n_params, device=gpu)
-        FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=FLD.grid_bw_workspace(desc, gpu),
-                           fixed_point=True)
-        got = gt.cpu().double()
-        assert torch.isfinite(got).all()
-        assert float((got - gref).abs().max()) <= 1e-4 * float(gref.abs().max()), mag
+        for binned in (False, True):
+            gt = torch.zeros(lay.n_params, device=gpu)
+            ws = FLD.grid_bw_binned_workspace(desc, N, gpu) if binned else FLD.grid_bw_workspace(desc, gpu)
+            FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=ws, fixed_point=True, binned=binned)
+            got = gt.cpu().double()
+            assert torch.isfinite(got).all()
+            assert float((got - gref).abs().max()) <= 1e-4 * float(gref.abs().max()), (mag, binned)
     gt = torch.ones(lay.n_params, device=gpu) * 0
     FLD.grid_encode_bw(x.to(gpu), N, torch.zeros(N, 32, device=gpu), gt, lay, desc, fixed_point=True)
     assert int((gt != 0).sum()) == 0
@@ -336,15 +354,16 @@ def test_grid_encode_bw_fixed_point_shared_tables(gpu):
     (FO.grid_encode(x, tp, olay).double() * dy.double()).sum().backward()
     gref = tp.grad.double()
     desc = lay.desc()
-    gt = torch.zeros(lay.n_params, device=gpu)
-    FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=FLD.grid_bw_workspace(desc, gpu),
-                       fixed_point=True)
-    got = gt.cpu().double()
-    regions = sorted(set((lay.offsets[l], lay.sizes[l]) for l in range(lay.L)))
-    assert len(regions) < lay.L  # some tables are shared
-    for off, size in regions:
-        a, b = 2 * off, 2 * (off + size)
-        scale = float(gref[a:b].abs().max())
-        if scale > 0:
-            err = float((got[a:b] - gref[a:b]).abs().max()) / scale
-            assert err < 1e-4, (off, err)
+    for binned in (False, True):
+        gt = torch.zeros(lay.n_params, device=gpu)
+        ws = FLD.grid_bw_binned_workspace(desc, N, gpu) if binned else FLD.grid_bw_workspace(desc, gpu)
+        FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=ws, fixed_point=True, binned=binned)
+        got = gt.cpu().double()
+        regions = sorted(set((lay.offsets[l], lay.sizes[l]) for l in range(lay.L)))
+        assert len(regions) < lay.L  # some tables are shared
+        for off, size in regions:
+            a, b = 2 * off, 2 * (off + size)
+            scale = float(gref[a:b].abs().max())
+            if scale > 0:
+                err = float((got[a:b] - gref[a:b]).abs().max()) / scale
+                assert err < 1e-4, (binned, off, err)

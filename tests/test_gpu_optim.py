@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from mfnerf import engine, synthetic
-from mfnerf._lib import call, ptr, stream
+from mfnerf._lib import call, load, ptr, stream
 from mfnerf.trainer import HParams, cosine_lr
 
 pytestmark = pytest.mark.gpu
@@ -120,7 +120,8 @@ def test_adam_step_fixed_matches_torch_adam(gpu):
     st = engine.TrainStep(engine.StepConfig(n_rays=256, log2_T=12), device=gpu)
     lay, desc = st.layout, st.desc
     n, off = st.n_alloc, st.off_table
-    ws = st.parts[0].grid_ws.view(torch.int32)
+    # the dense levels' private copies: the workspace's prefix (binned-scatter scratch follows)
+    ws = st.parts[0].grid_ws.view(torch.int32)[:max(16, load().mfnerf_grid_encode_bw_workspace(desc)) // 4]
     dense_entries = 0
     for l in range(lay.L):
         if lay.res[l] ** 3 > lay.sizes[l] or lay.offsets[l] != dense_entries:

@@ -37,6 +37,11 @@ def main():
     grad_h2 = torch.zeros(step.layout.n_params, dtype=torch.float16, device=dev)
     priv_h2 = torch.zeros_like(t.grid_ws)
     s = stream
+    # the fixed-point scatter's per-level scales: the last Adam pass zeroed level_l1 for the next step,
+    # so recompute it from this step's dL/dfeat (else every contribution rounds to 0 and no atomic
+    # is issued: the timing would miss the scatter itself)
+    step._level_l1.zero_()
+    call("mfnerf_grid_level_l1", ptr(t.dfeat), cap, ptr(m.counter), c.L, ptr(step._level_l1), s())
 
     stages = {
         "grid_fw": lambda: call("mfnerf_grid_encode_fw", ptr(m.xyzs), cap, ptr(m.counter), step.x_min, step.x_range,
