@@ -215,20 +215,23 @@ int mfnerf_grid_encode_bw_finish(const mfnerf_grid_desc* desc, float* grad_table
                                  const float* level_l1, mfnerf_stream_t stream);
 
 /* The fixed-point scatter (level_l1 required) by table partitions instead of memory-side atomics:
- * the hashed / shared tables are cut into 4096-entry partitions; every (point, level, corner row)
- * becomes a 16-B record routed to its partition by a counting sort, and one workgroup per
- * partition sums its records in LDS with integer atomics and stores the partition once.  The dense
- * levels go through the private copies as in mfnerf_grid_encode_bw_scatter.  Same int32 fixed
- * point (each contribution rounded once to its table's scale), same workspace prefix (the private
- * copies), so mfnerf_grid_encode_bw_finish / mfnerf_adam_step_fixed convert it unchanged;
+ * the hashed / shared tables are cut into partitions of up to 2048 entries; every (point, level,
+ * corner row) becomes a 12-B record, sorted by partition in LDS and stored into fixed per-(partition,
+ * work unit) slots, and one workgroup per partition sums its records exactly (int64 LDS atomics)
+ * and stores the partition once, rounded to the same int32 fixed point as
+ * mfnerf_grid_encode_bw_scatter (one rounding per entry).  A slot overflow (pathological inputs)
+ * falls back to that call's atomics on the device.  parts: 1 = the dense coarse levels only (atomics
+ * into the workspace's private copies, as mfnerf_grid_encode_bw_scatter), 2 = the partitioned levels
+ * only, 3 = both -- 1 and 2 may run concurrently on two streams.  The workspace prefix is the private
+ * copies, so mfnerf_grid_encode_bw_finish / mfnerf_adam_step_fixed convert the result unchanged;
  * grad_table must be zero on entry.  workspace: mfnerf_grid_encode_bw_binned_workspace(desc, n)
- * bytes for this call's n (the record buffer holds n * levels * 4 records), its copies zero on the
- * first call (left zero by the finish).  Bit-reproducible.  Replaces tcnn's hash-grid backward
- * scatter (networks.py:36-49 encoding, half2 atomics there). */
+ * bytes for this call's n, its copies zero on the first call (left zero by the finish).
+ * Bit-reproducible.  Replaces tcnn's hash-grid backward scatter (networks.py:36-49 encoding, half2
+ * atomics there). */
 int64_t mfnerf_grid_encode_bw_binned_workspace(const mfnerf_grid_desc* desc, int64_t n_max);
 int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                                  const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
-                                 void* workspace, const float* level_l1, mfnerf_stream_t stream);
+                                 void* workspace, const float* level_l1, int parts, mfnerf_stream_t stream);
 
 /* out[l] += sum over rows i < n (or *n_dev) of |dL_dout[i][2l]| + |dL_dout[i][2l+1]| (f32). */
 int mfnerf_grid_level_l1(const float* dL_dout, int64_t n, const int32_t* n_dev, int n_levels, float* out,

@@ -293,7 +293,7 @@ __device__ __forceinline__ void grid_bw_body(int bid, int nblk, const float* __r
         const float z = valid ? (pz - x_min) / x_range : 0.0f;
         if (chunk + n_waves < chunks) fetch(chunk + n_waves);  // in flight during this chunk's atomics
         const float* srow = sdy + s * rs + f;
-        for (int l = 0; l < l_end; ++l) {
+        for (int l = l_end >> 8; l < (l_end & 255); ++l) {  // levels [l_end >> 8, l_end & 255)
             if (ABLATE == 2 && l > 5) continue;
             if (ABLATE == 3 && l < 10) continue;
             const float g = srow[2 * l];
@@ -628,15 +628,12 @@ int check_desc(const mfnerf_grid_desc* d, const char* what) {
 // there are >= ~1024 partitions (4 workgroups per CU); 2^11 entries = 32 KB of int64 pairs
 constexpr int MIN_BIN_SHIFT = 8, MAX_BIN_SHIFT = 11, MAX_BIN_ENTRIES = 1 << MAX_BIN_SHIFT;
 constexpr int MAX_BINS = 4096;
-constexpr int BIN_BLOCKS = 1024;  // max count workgroups (sub-units): the counts array's stride
-constexpr int ACC_THREADS = 512;
 
 struct BinPlan {
     int n_binned;                    // levels routed through the bins
     int n_bins;                      // partitions over all their tables
     int n_tables;
     int shift;                       // partition = 2^shift entries of one table
-    int blocks;                      // count / scatter work units (<= BIN_BLOCKS)
     int pair_ok;                     // no x-pair can straddle two partitions (one record per row)
     int level[MFN_MAX_LEVELS];       // binned level list
     int pairable[MFN_MAX_LEVELS];    // per level: x+1's entry = x's entry ^ (x ^ (x+1)) (own power-of-two hash)
@@ -691,15 +688,6 @@ __device__ __forceinline__ void level_records(const mfnerf_grid_desc& D, const B
     }
 }
 
-// Work units of the count and scatter passes: unit u of P.blocks owns the contiguous samples
-// [c0, c1) of the live count, so its records of one bin form one contiguous run in the bin; the
-// count pass splits each unit into SUBUNITS workgroups (contiguous sub-ranges, consecutive in the
-// scan), so a unit's run starts at its first sub-unit's offset.
-constexpr int SUBUNITS = 4;
-__device__ __forceinline__ void unit_range(int u, int nu, int64_t nn, int64_t& c0, int64_t& c1) {
-    c0 = nn * u / nu;
-    c1 = nn * (u + 1) / nu;
-}
 
 // the records of sample i at binned level j (nothing for a zero dL/dy: terminated samples)
 template <typename EMIT>
@@ -755,104 +743,6 @@ __device__ __forceinline__ void load_fixed_scales(const mfnerf_grid_desc& D, con
     if ((int)threadIdx.x < D.n_levels) fs_s[threadIdx.x] = table_fixed_scale(D, level_l1, threadIdx.x);
 }
 
-// pass 1: per-block histogram over the bins -> counts[bin * BIN_BLOCKS + block], fused with the
-// dense levels' atomic scatter: workgroups [0, n_dense) run grid_bw_body on the dense levels, the
-// next P.blocks count (the two overlap: one waits on memory-side atomics, the other computes)
-template <int MAXL>
-__global__ __launch_bounds__(256) void bin_count_dense_kernel(const float* __restrict__ X, int64_t n,
-                                                              const int32_t* __restrict__ n_dev, float x_min,
-                                                              float x_range, const mfnerf_grid_desc D, const BinPlan P,
-                                                              const float* __restrict__ dy,
-                                                              const float* __restrict__ level_l1,
-                                                              int32_t* __restrict__ counts, int n_dense, float* grad,
-                                                              float* priv, int64_t dense_entries, int l_end) {
-    if ((int)blockIdx.x < n_dense) {
-        grid_bw_body<0, MAXL, true>(blockIdx.x, n_dense, X, n, n_dev, x_min, x_range, D, dy, grad, priv,
-                                    dense_entries, level_l1, l_end);
-        return;
-    }
-    const int bid = blockIdx.x - n_dense;  // sub-unit: SUBUNITS per scatter unit
-    __shared__ int hist[MAX_BINS];
-    __shared__ float fs_s[MFN_MAX_LEVELS];
-    for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x) hist[b] = 0;
-    load_fixed_scales(D, level_l1, fs_s);
-    __syncthreads();
-    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
-    int64_t c0, c1;
-    unit_range(bid, P.blocks * SUBUNITS, nn, c0, c1);
-    for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
-        StagedSample S;
-        stage_sample(D, P, X, x_min, x_range, dy, i, S);
-        for (int j = 0; j < P.n_binned; ++j)
-            staged_records(D, P, S, fs_s, j, [&](int bin, uint3) { atomicAdd(&hist[bin], 1); });
-    }
-    __syncthreads();
-    for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x) counts[(int64_t)b * BIN_BLOCKS + bid] = hist[b];
-}
-
-// pass 2: per bin, exclusive scan of its per-block counts (in place) and the bin's total
-__global__ __launch_bounds__(256) void bin_scan_kernel(int32_t* __restrict__ counts, int32_t* __restrict__ bin_total,
-                                                       int blocks) {
-    __shared__ int part[256];
-    int32_t* c = counts + (int64_t)blockIdx.x * BIN_BLOCKS;
-    constexpr int PER = BIN_BLOCKS / 256;
-    const int nblk = blocks;
-    int v[PER], sum = 0;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        v[k] = threadIdx.x * PER + k < nblk ? c[threadIdx.x * PER + k] : 0;
-        sum += v[k];
-    }
-    part[threadIdx.x] = sum;
-    __syncthreads();
-    for (int off = 1; off < 256; off <<= 1) {  // Hillis-Steele inclusive scan of the 256 partials
-        const int add = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-        __syncthreads();
-        part[threadIdx.x] += add;
-        __syncthreads();
-    }
-    int run = part[threadIdx.x] - sum;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        if (threadIdx.x * PER + k < nblk) c[threadIdx.x * PER + k] = run;
-        run += v[k];
-    }
-    if (threadIdx.x == 255) bin_total[blockIdx.x] = part[255];
-}
-
-// exclusive block scan of v[0, n) (n <= 4 * blockDim.x, blockDim.x <= 1024) into out; returns the total
-__device__ __forceinline__ int block_scan(const int* v, int n, int* out) {
-    __shared__ int part[1024];
-    const int per = (n + (int)blockDim.x - 1) / (int)blockDim.x;
-    const int lo = threadIdx.x * per;
-    int sum = 0;
-    for (int k = 0; k < per && lo + k < n; ++k) sum += v[lo + k];
-    part[threadIdx.x] = sum;
-    __syncthreads();
-    for (int off = 1; off < (int)blockDim.x; off <<= 1) {
-        const int add = (int)threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-        __syncthreads();
-        part[threadIdx.x] += add;
-        __syncthreads();
-    }
-    int run = part[threadIdx.x] - sum;
-    const int total = part[blockDim.x - 1];
-    for (int k = 0; k < per && lo + k < n; ++k) {
-        const int x = v[lo + k];
-        out[lo + k] = run;
-        run += x;
-    }
-    __syncthreads();
-    return total;
-}
-
-// exclusive scan of bin_total[0, nb) into LDS (block-wide)
-__device__ __forceinline__ void scan_bins(const int32_t* __restrict__ bin_total, int nb, int* start) {
-    for (int b = threadIdx.x; b < nb; b += blockDim.x) start[b] = bin_total[b];
-    __syncthreads();
-    block_scan(start, nb, start);
-}
-
 // exclusive scan over the block (one value per thread, blockDim <= 1024): wave scans by lane
 // shuffles, then the wave totals; out[threadIdx.x] = this thread's offset.  Returns the total.
 __device__ __forceinline__ int wave_block_scan(int v, int* out) {
@@ -878,44 +768,56 @@ __device__ __forceinline__ int wave_block_scan(int v, int* out) {
     return total;
 }
 
-// pass 3: the records.  Unit u (one 1024-thread workgroup) walks its samples level by level in
-// tiles of up to 2048 samples: the tile's records are counted per bin of the level's table
-// (LDS atomics give each its rank), sorted by bin in LDS and stored as one contiguous run per bin
-// at the bin's cursor (bin start + the unit's offset in the bin + what earlier tiles stored): ~30
-// records per run at the Lego config, whole-line stores instead of one scattered store per record.
+// Records live in fixed slots: unit u's records of bin b at rec[(b * UNITS + u) * slot + k],
+// k < scnt[b * UNITS + u] -- no counting pass, no scan.  slot = 2 * (mean records per slot at this
+// step's live count) -- 3 x the mean + 96, so the buffer (sized for the largest live count) always holds them; a
+// slot that still overflows (a pathological sample distribution) raises `ovf`, and then the
+// accumulate stores nothing and bin_fallback_kernel scatters the binned levels by atomics instead.
+constexpr int UNITS = 256;       // scatter workgroups, each owning a contiguous sample range
 constexpr int SC_THREADS = 1024;
-constexpr int MAX_TBINS = 1024;              // bins of one table
-constexpr int SC_STAGE = SC_THREADS * 8;     // staged records per tile (8 per thread)
+constexpr int MAX_TBINS = 1024;  // bins of one table
+constexpr int SC_STAGE = SC_THREADS * 8;  // staged records per tile (8 per thread)
 
+__device__ __forceinline__ int64_t slot_size(int64_t nn, const BinPlan& P) {
+    const int64_t recs = nn * P.n_binned * (P.pair_ok ? 4 : 8);
+    return 3 * ((recs + (int64_t)P.n_bins * UNITS - 1) / ((int64_t)P.n_bins * UNITS)) + 96;
+}
+
+// pass 1: unit u (one 1024-thread workgroup) walks its samples, staged in registers, level by level
+// in tiles of up to 2048 samples: the tile's records are counted per bin of the level's table (LDS
+// atomics give each its rank), sorted by bin in LDS and stored as one contiguous run per bin in the
+// unit's slot of the bin (~30 records per run at the Lego config: whole-line stores).
 __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __restrict__ X, int64_t n,
                                                                  const int32_t* __restrict__ n_dev, float x_min,
                                                                  float x_range, const mfnerf_grid_desc D,
                                                                  const BinPlan P, const float* __restrict__ dy,
                                                                  const float* __restrict__ level_l1,
-                                                                 const int32_t* __restrict__ counts,
-                                                                 const int32_t* __restrict__ bin_start,
-                                                                 uint3* __restrict__ rec, int debug_no_store) {
+                                                                 uint3* __restrict__ rec, int32_t* __restrict__ scnt,
+                                                                 int32_t* __restrict__ ovf) {
     __shared__ int cursor[MAX_BINS];
     __shared__ int thist[MAX_TBINS], toff[MAX_TBINS], gdst[MAX_TBINS];
     __shared__ uint3 stage[SC_STAGE];
     __shared__ uint16_t sbin[SC_STAGE];
     __shared__ float fs_s[MFN_MAX_LEVELS];
     load_fixed_scales(D, level_l1, fs_s);
-    // this unit's write position in each bin: the bin's start + the unit's first sub-unit's offset
-    for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x)
-        cursor[b] = bin_start[b] + counts[(int64_t)b * BIN_BLOCKS + blockIdx.x * SUBUNITS];
+    for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x) cursor[b] = 0;
     __syncthreads();
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
-    int64_t c0, c1;
-    unit_range(blockIdx.x, gridDim.x, nn, c0, c1);
+    const int64_t slot = slot_size(nn, P);
+    // unit u owns the 16-sample chunks u, u + UNITS, u + 2 UNITS, ...: a ray's samples (which repeat
+    // the coarse levels' rows) spread over many units, so every slot fills close to the mean
+    const int u = blockIdx.x;
+    const int64_t n_chunks = (nn + 15) / 16;
+    const int64_t m = n_chunks > u ? ((n_chunks - 1 - u) / UNITS + 1) * 16 : 0;  // this unit's sample slots
     const int spt = P.pair_ok ? 2 : 1;  // samples per thread per tile: <= 8 records each per level
-    for (int64_t base = c0; base < c1; base += (int64_t)spt * SC_THREADS) {
+    for (int64_t base = 0; base < m; base += (int64_t)spt * SC_THREADS) {
         StagedSample S[2];
         bool live[2] = {false, false};
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-            const int64_t i = base + (int64_t)q * SC_THREADS + threadIdx.x;
-            live[q] = q < spt && i < c1;
+            const int64_t k = base + (int64_t)q * SC_THREADS + threadIdx.x;
+            const int64_t i = ((k >> 4) * UNITS + u) * 16 + (k & 15);  // chunk k/16 of the unit
+            live[q] = q < spt && k < m && i < nn;
             if (live[q]) stage_sample(D, P, X, x_min, x_range, dy, i, S[q]);
         }
         for (int j = 0; j < P.n_binned; ++j) {
@@ -934,7 +836,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                         rr[nr++] = r;
                     });
             __syncthreads();
-            // bins -> sorted tile offsets (toff) and global destinations (gdst + sorted index)
+            // bins -> sorted tile offsets (toff); a run's k-th record goes to its slot position gdst + k
             const int cnt = (int)threadIdx.x < tb ? thist[threadIdx.x] : 0;
             const int total = wave_block_scan(cnt, toff);
             if ((int)threadIdx.x < tb) {
@@ -951,25 +853,25 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                     sbin[p] = (uint16_t)lb;
                 }
             __syncthreads();
-            for (int k = threadIdx.x; k < total; k += SC_THREADS)
-                if (!debug_no_store) rec[gdst[sbin[k]] + k] = stage[k];
+            for (int k = threadIdx.x; k < total; k += SC_THREADS) {
+                const int lb = sbin[k];
+                const int pos = gdst[lb] + k;  // position in the unit's slot of the bin
+                if (pos < slot) rec[((int64_t)(b0 + lb) * UNITS + u) * slot + pos] = stage[k];
+            }
             __syncthreads();
         }
     }
+    bool over = false;
+    for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x) {
+        const int c = cursor[b];
+        over |= c > slot;
+        scnt[(int64_t)b * UNITS + u] = c;
+    }
+    if (over) atomicOr(ovf, 1);
 }
 
-// bin_start = exclusive scan of bin_total (one workgroup)
-__global__ __launch_bounds__(1024) void bin_start_kernel(const int32_t* __restrict__ bin_total, int nb,
-                                                         int32_t* __restrict__ bin_start) {
-    __shared__ int v[MAX_BINS];
-    for (int b = threadIdx.x; b < nb; b += blockDim.x) v[b] = bin_total[b];
-    __syncthreads();
-    block_scan(v, nb, v);
-    for (int b = threadIdx.x; b < nb; b += blockDim.x) bin_start[b] = v[b];
-}
-
-// pass 4: one workgroup per bin: sum the bin's records into an LDS image of its entries (int64
-// pairs, ds_add_u64), then store it rounded to int32.
+// pass 2: one workgroup per bin sums the bin's records (every unit's slot) into an LDS image of its
+// entries (int64 pairs, ds_add_u64) and stores it rounded to int32.
 __device__ __forceinline__ int round_shift32(long long v) { return (int)((v + 0x80000000ll) >> 32); }
 
 // float -> int64 for |v| < 2^62: below 2^31 round to nearest; above, v is an integer: its 24-bit
@@ -981,45 +883,62 @@ __device__ __forceinline__ long long f2ll(float v) {
     return (long long)(int)(m * 1073741824.0f) * (1ll << (e - 30));
 }
 
-constexpr int ACC_UNROLL = 8;
+__device__ __forceinline__ void accum_record(unsigned long long* img, int mask, uint3 r) {
+    const uint32_t w = r.x;
+    const float a = __uint_as_float(r.y), b = __uint_as_float(r.z);
+    if (a == 0.0f && b == 0.0f) return;
+    const float fx = (float)(w >> 17) * (1.0f / 32768.0f);
+    const int e0 = w & mask;
+    // |values| < 2^62: exact in int64, order-free sums
+    if (w & (1u << 15)) {  // single entry, weight sel ? fx : 1 - fx
+        const float wt = (w & (1u << 16)) ? fx : 1.0f - fx;
+        atomicAdd(&img[2 * e0], (unsigned long long)f2ll(wt * a));
+        atomicAdd(&img[2 * e0 + 1], (unsigned long long)f2ll(wt * b));
+    } else {
+        const int e1 = e0 ^ ((2 << ((w >> 11) & 15)) - 1);
+        const float w0 = 1.0f - fx;
+        atomicAdd(&img[2 * e0], (unsigned long long)f2ll(w0 * a));
+        atomicAdd(&img[2 * e0 + 1], (unsigned long long)f2ll(w0 * b));
+        atomicAdd(&img[2 * e1], (unsigned long long)f2ll(fx * a));
+        atomicAdd(&img[2 * e1 + 1], (unsigned long long)f2ll(fx * b));
+    }
+}
 
-__global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, const uint3* __restrict__ rec,
-                                                                const int32_t* __restrict__ bin_start,
-                                                                const int32_t* __restrict__ bin_total,
+constexpr int ACC_THREADS = 512;
+
+__global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, int64_t n,
+                                                                const int32_t* __restrict__ n_dev,
+                                                                const uint3* __restrict__ rec,
+                                                                const int32_t* __restrict__ scnt,
+                                                                const int32_t* __restrict__ ovf,
                                                                 int* __restrict__ grad) {
+    if (*ovf) return;  // a slot overflowed: bin_fallback_kernel scatters the binned levels
     __shared__ unsigned long long img[2 * MAX_BIN_ENTRIES];
     const int bin = blockIdx.x;
     const int n_ent = 1 << P.shift, mask = n_ent - 1;
     for (int i = threadIdx.x; i < 2 * n_ent; i += blockDim.x) img[i] = 0;
     __syncthreads();
-    const int64_t lo = bin_start[bin], hi = lo + bin_total[bin];
-    for (int64_t k0 = lo + threadIdx.x; k0 < hi; k0 += (int64_t)ACC_UNROLL * blockDim.x) {
-        uint3 r[ACC_UNROLL];
+    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
+    const int64_t slot = slot_size(nn, P);
+    // one unit's slot per half-wave (32 lanes; ~30 records per slot at the Lego config), 4 slots
+    // in flight per half-wave
+    const int hw = threadIdx.x >> 5, hl = threadIdx.x & 31, n_hw = ACC_THREADS / 32;
+    const int32_t* cnt = scnt + (int64_t)bin * UNITS;
+    const uint3* base = rec + (int64_t)bin * UNITS * slot;
+    for (int u0 = hw; u0 < UNITS; u0 += 4 * n_hw) {
+        uint3 r[4];
+        int c[4];
 #pragma unroll
-        for (int u = 0; u < ACC_UNROLL; ++u) {  // all loads in flight first
-            const int64_t k = k0 + (int64_t)u * blockDim.x;
-            r[u] = k < hi ? rec[k] : make_uint3(0u, 0u, 0u);
+        for (int q = 0; q < 4; ++q) {
+            const int u = u0 + q * n_hw;
+            c[q] = u < UNITS ? cnt[u] : 0;
+            r[q] = hl < c[q] ? base[(int64_t)u * slot + hl] : make_uint3(0u, 0u, 0u);
         }
 #pragma unroll
-        for (int u = 0; u < ACC_UNROLL; ++u) {
-            const uint32_t w = r[u].x;
-            const float a = __uint_as_float(r[u].y), b = __uint_as_float(r[u].z);
-            if (a == 0.0f && b == 0.0f) continue;  // padding (or a zero contribution)
-            const float fx = (float)(w >> 17) * (1.0f / 32768.0f);
-            const int e0 = w & mask;
-            if (w & (1u << 15)) {  // single entry, weight sel ? fx : 1 - fx
-                const float wt = (w & (1u << 16)) ? fx : 1.0f - fx;
-                atomicAdd(&img[2 * e0], (unsigned long long)f2ll(wt * a));
-                atomicAdd(&img[2 * e0 + 1], (unsigned long long)f2ll(wt * b));
-            } else {
-                const int e1 = e0 ^ ((2 << ((w >> 11) & 15)) - 1);
-                const float w0 = 1.0f - fx;
-                // |values| < 2^62: exact in int64, order-free sums
-                atomicAdd(&img[2 * e0], (unsigned long long)f2ll(w0 * a));
-                atomicAdd(&img[2 * e0 + 1], (unsigned long long)f2ll(w0 * b));
-                atomicAdd(&img[2 * e1], (unsigned long long)f2ll(fx * a));
-                atomicAdd(&img[2 * e1 + 1], (unsigned long long)f2ll(fx * b));
-            }
+        for (int q = 0; q < 4; ++q) {
+            const int u = u0 + q * n_hw;
+            accum_record(img, mask, r[q]);
+            for (int k = hl + 32; k < c[q]; k += 32) accum_record(img, mask, base[(int64_t)u * slot + k]);
         }
     }
     __syncthreads();
@@ -1030,16 +949,32 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     for (int i = threadIdx.x; i < 2 * n_e; i += blockDim.x) dst[i] = round_shift32((long long)img[i]);
 }
 
+// the binned levels by request-shaped int32 atomics (grid_bw_body), only if a slot overflowed
+template <int MAXL>
+__global__ __launch_bounds__(ENC_BLOCK) void bin_fallback_kernel(const float* __restrict__ X, int64_t n,
+                                                                 const int32_t* __restrict__ n_dev, float x_min,
+                                                                 float x_range, const mfnerf_grid_desc D,
+                                                                 const float* __restrict__ dy, float* grad,
+                                                                 const float* __restrict__ level_l1,
+                                                                 const int32_t* __restrict__ ovf, int levels) {
+    if (!*ovf) return;
+    grid_bw_body<0, MAXL, true>(blockIdx.x, gridDim.x, X, n, n_dev, x_min, x_range, D, dy, grad, nullptr, 0,
+                                level_l1, levels);
+}
+
 // The plan for a desc: binned levels = every level that is not a dense own table; tables in address
 // order.  Returns the number of bins (0: nothing to bin), or -1 if over MAX_BINS.
+int first_binned_level(const mfnerf_grid_desc* d);
+
 int bin_plan(const mfnerf_grid_desc* d, BinPlan* P) {
     *P = BinPlan{};
+    const int l_first = first_binned_level(d);
     P->pair_ok = 1;
     uint64_t entries = 0, max_x = 0;
     for (int l = 0; l < d->n_levels; ++l) {
         const uint64_t r = d->res[l];
-        const bool dense = d->table_kind[l] == 0 && r * r * r <= d->size[l];
-        if (dense) continue;
+        (void)r;
+        if (l < l_first) continue;  // dense levels, and the coarse hashed ones: atomics
         int t = 0;
         while (t < P->n_tables && P->t_offset[t] != d->offset[l]) ++t;
         if (t == P->n_tables) {
@@ -1069,9 +1004,6 @@ int bin_plan(const mfnerf_grid_desc* d, BinPlan* P) {
     }
     P->t_bin0[P->n_tables] = nb;
     P->n_bins = nb;
-    // tuning knob (read once): MFNERF_BIN_BLOCKS
-    static const int knob_blocks = [] { const char* e = getenv("MFNERF_BIN_BLOCKS"); return e ? atoi(e) : 0; }();
-    P->blocks = knob_blocks >= 64 && knob_blocks * SUBUNITS <= BIN_BLOCKS ? knob_blocks : BIN_BLOCKS / SUBUNITS;
     if (P->n_binned > MAX_BINNED) return -1;
     for (int j = 1; j < P->n_binned; ++j)  // the binned levels are contiguous (staged dL/dy rows)
         if (P->level[j] != P->level[0] + j) return -1;
@@ -1081,44 +1013,51 @@ int bin_plan(const mfnerf_grid_desc* d, BinPlan* P) {
 }
 
 // first level routed through the bins (the dense levels before it use grid_bw_kernel)
+// The partitioned levels: the last MFNERF_BIN_LEVELS (default 6) hashed ones -- the fine levels,
+// whose rows no run merging collapses; the coarser hashed levels repeat rows along a ray and stay
+// on the run-merging atomics -- extended down to every level that shares a table with them
+// (MixedFeature), since a partition is stored whole.
 int first_binned_level(const mfnerf_grid_desc* d) {
+    static const int knob = [] { const char* e = getenv("MFNERF_BIN_LEVELS"); return e ? atoi(e) : 6; }();
+    int first_hashed = d->n_levels;
     for (int l = 0; l < d->n_levels; ++l) {
         const uint64_t r = d->res[l];
-        if (!(d->table_kind[l] == 0 && r * r * r <= d->size[l])) return l;
+        if (!(d->table_kind[l] == 0 && r * r * r <= d->size[l])) { first_hashed = l; break; }
     }
-    return d->n_levels;
+    int l0 = d->n_levels - knob;
+    if (l0 < first_hashed) l0 = first_hashed;
+    for (bool moved = true; moved;) {
+        moved = false;
+        for (int a = first_hashed; a < l0 && !moved; ++a)
+            for (int b = l0; b < d->n_levels; ++b)
+                if (d->offset[a] == d->offset[b]) { l0 = a; moved = true; break; }
+    }
+    return l0;
 }
 
 struct BinWorkspace {
     float* priv;
-    int32_t *counts, *bin_total, *bin_start;
+    int32_t *scnt, *ovf;
     uint3* rec;
 };
 
 int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
 
-// MFNERF_BIN_DEBUG_NO_STORE=1: the scatter pass computes and ranks its records but stores none
-// (timing experiments only: the accumulate then reads stale records)
-int bin_debug_no_store() {
-    static const int v = [] { const char* e = getenv("MFNERF_BIN_DEBUG_NO_STORE"); return e ? atoi(e) : 0; }();
-    return v;
-}
-
-// workspace = [private copies of the dense levels | counts | bin_total | bin_start | records]
+// workspace = [private copies of the dense levels | slot counts | overflow flag | record slots]
 int64_t binned_workspace_layout(const mfnerf_grid_desc* d, int64_t n_max, char* base, BinWorkspace* W) {
     BinPlan P;
     if (bin_plan(d, &P) < 0) return -1;
     int64_t off = align256((int64_t)GRAD_COPIES * dense_entries_of(d) * 2 * (int64_t)sizeof(float));
     if (W) W->priv = reinterpret_cast<float*>(base);
     const int64_t nb = P.n_bins > 0 ? P.n_bins : 1;
-    if (W) W->counts = reinterpret_cast<int32_t*>(base + off);
-    off += align256(nb * BIN_BLOCKS * 4);
-    if (W) W->bin_total = reinterpret_cast<int32_t*>(base + off);
-    off += align256(nb * 4);
-    if (W) W->bin_start = reinterpret_cast<int32_t*>(base + off);
-    off += align256(nb * 4);
+    if (W) W->scnt = reinterpret_cast<int32_t*>(base + off);
+    off += align256(nb * UNITS * 4);
+    if (W) W->ovf = reinterpret_cast<int32_t*>(base + off);
+    off += 256;
     if (W) W->rec = reinterpret_cast<uint3*>(base + off);
-    off += align256(n_max * P.n_binned * 4 * (P.pair_ok ? 1 : 2) * (int64_t)sizeof(uint3));
+    // slots at the largest live count: 3 x (its records + one per slot) + 96 per slot (slot_size)
+    const int64_t recs = n_max * P.n_binned * (P.pair_ok ? 4 : 8);
+    off += align256((3 * recs + 3 * nb * UNITS + 96 * nb * UNITS) * (int64_t)sizeof(uint3));
     return off;
 }
 
@@ -1330,8 +1269,8 @@ int mfnerf_debug_grid_bw_ablate(int mode, const float* x, int64_t n, const int32
     return mfn_check_launch("grid_bw_ablate");
 }
 
-// Partitioned (binned) fixed-point table-gradient scatter: the dense levels through grid_bw_kernel's
-// private copies, the hashed / shared tables through count -> scan -> scatter -> LDS accumulate.
+// Partitioned (binned) fixed-point table-gradient scatter: the dense levels through grid_bw_body's
+// private copies (parts & 1), the hashed / shared tables through scatter -> LDS accumulate (parts & 2).
 int64_t mfnerf_grid_encode_bw_binned_workspace(const mfnerf_grid_desc* desc, int64_t n_max) {
     if (check_desc(desc, "grid_encode_bw_binned_workspace") || n_max < 0) return -1;
     return binned_workspace_layout(desc, n_max, nullptr, nullptr);
@@ -1339,10 +1278,10 @@ int64_t mfnerf_grid_encode_bw_binned_workspace(const mfnerf_grid_desc* desc, int
 
 int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                                  const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
-                                 void* workspace, const float* level_l1, mfnerf_stream_t stream) {
+                                 void* workspace, const float* level_l1, int parts, mfnerf_stream_t stream) {
     int st = check_desc(desc, "grid_encode_bw_binned");
     if (st) return st;
-    if (n < 0) { mfn_set_error("grid_encode_bw_binned: bad size"); return MFN_ERR_INVALID; }
+    if (n < 0 || parts < 1 || parts > 3) { mfn_set_error("grid_encode_bw_binned: bad size or parts"); return MFN_ERR_INVALID; }
     if (n == 0) return MFN_OK;
     if (!x || !dL_dout || !grad_table || !workspace || !level_l1) {
         mfn_set_error("grid_encode_bw_binned: null pointer (workspace and level_l1 are required)");
@@ -1350,38 +1289,32 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
     }
     BinPlan P;
     if (bin_plan(desc, &P) < 0) {
-        mfn_set_error("grid_encode_bw_binned: more than %d partitions of %d entries", MAX_BINS, MAX_BIN_ENTRIES);
+        mfn_set_error("grid_encode_bw_binned: unsupported layout (> %d partitions, > %d bins per table, or binned "
+                      "levels not the contiguous last %d)", MAX_BINS, MAX_TBINS, MAX_BINNED);
         return MFN_ERR_INVALID;
-    }
-    if (n * (int64_t)P.n_binned >= (1ll << 31)) {
-        mfn_set_error("grid_encode_bw_binned: n * binned levels must be < 2^31"); return MFN_ERR_INVALID;
     }
     BinWorkspace W;
     binned_workspace_layout(desc, n, (char*)workspace, &W);
-    // the dense levels (request-shaped int32 atomics into the private copies) and the bin histogram
-    // in one launch; then the scan, the records and the per-partition sums
-    const int l_end = first_binned_level(desc);
-    int n_dense = 0;
-    if (l_end > 0) {
-        const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16), ENC_BLOCK / 64);
-        const int64_t cap = grid_bw_block_cap();
-        n_dense = (int)(want < cap ? want : cap);
+    const int l_first = first_binned_level(desc);
+    const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16), ENC_BLOCK / 64);
+    const int64_t cap = grid_bw_block_cap();
+    const int64_t atomic_blocks = want < cap ? want : cap;
+    const bool big = desc->n_levels > 16;
+    if ((parts & 1) && l_first > 0) {  // dense levels [0, l_first): request-shaped atomics, private copies
+        auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, true> : grid_bw_kernel<0, 16, true>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)atomic_blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min,
+                           x_range, *desc, dL_dout, grad_table, W.priv, dense_entries_of(desc), level_l1, l_first);
     }
-    const int n_count = P.n_bins > 0 ? P.blocks * SUBUNITS : 0;
-    if (n_dense + n_count > 0) {
-        auto kern = desc->n_levels > 16 ? bin_count_dense_kernel<MFN_MAX_LEVELS> : bin_count_dense_kernel<16>;
-        hipLaunchKernelGGL(kern, dim3((unsigned)(n_dense + n_count)), dim3(256), 0, stream, x, n, n_dev, x_min,
-                           x_range, *desc, P, dL_dout, level_l1, W.counts, n_dense, grad_table, W.priv,
-                           dense_entries_of(desc), l_end);
-    }
-    if (P.n_bins > 0) {
-        hipLaunchKernelGGL(bin_scan_kernel, dim3(P.n_bins), dim3(256), 0, stream, W.counts, W.bin_total,
-                           P.blocks * SUBUNITS);
-        hipLaunchKernelGGL(bin_start_kernel, dim3(1), dim3(1024), 0, stream, W.bin_total, P.n_bins, W.bin_start);
-        hipLaunchKernelGGL(bin_scatter_kernel, dim3(P.blocks), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
-                           *desc, P, dL_dout, level_l1, W.counts, W.bin_start, W.rec, bin_debug_no_store());
-        hipLaunchKernelGGL(bin_accum_kernel, dim3(P.n_bins), dim3(ACC_THREADS), 0, stream, P, W.rec,
-                           W.bin_start, W.bin_total, (int*)grad_table);
+    if ((parts & 2) && P.n_bins > 0) {
+        (void)hipMemsetAsync(W.ovf, 0, sizeof(int32_t), stream);
+        hipLaunchKernelGGL(bin_scatter_kernel, dim3(UNITS), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
+                           *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.ovf);
+        hipLaunchKernelGGL(bin_accum_kernel, dim3(P.n_bins), dim3(ACC_THREADS), 0, stream, P, n, n_dev, W.rec,
+                           W.scnt, W.ovf, (int*)grad_table);
+        // levels [l_first, L) by atomics, only when a slot overflowed (exits at once otherwise)
+        auto fb = big ? bin_fallback_kernel<MFN_MAX_LEVELS> : bin_fallback_kernel<16>;
+        hipLaunchKernelGGL(fb, dim3(256), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc, dL_dout,
+                           grad_table, level_l1, W.ovf, (l_first << 8) | desc->n_levels);
     }
     return mfn_check_launch("grid_encode_bw_binned");
 }

@@ -88,6 +88,21 @@ def _packed_batch(buf):
     return b
 
 
+def init_params(c: StepConfig, n_params, n_alloc, seed):
+    """The flat initial parameters [xyz MLP | rgb MLP | table] (host tensor, n_alloc long, zero
+    padding): tcnn's init -- Xavier-uniform per MLP matrix, table U(-1e-4, 1e-4) -- from a seeded
+    generator, so a CPU restatement of the step can start from the very same weights."""
+    g = torch.Generator().manual_seed(seed)
+    p = torch.zeros(n_alloc)
+    off = 0
+    for o, k in [(64, 32), (16, 64), (c.rgb_width, 32), (c.rgb_width, c.rgb_width), (16, c.rgb_width)]:
+        s = math.sqrt(6.0 / (o + k))  # tcnn Xavier-uniform per matrix
+        p[off:off + o * k].uniform_(-s, s, generator=g)
+        off += o * k
+    p[off:n_params].uniform_(-1e-4, 1e-4, generator=g)  # tcnn grid init
+    return p
+
+
 class TrainStep:
     def __init__(self, cfg: StepConfig, device="cuda", seed=0):
         self.cfg = cfg
@@ -112,15 +127,7 @@ class TrainStep:
         self.x_min, self.x_range = float(-s32), float(np.float32(s32) - np.float32(-s32))
 
         dev = self.dev
-        g = torch.Generator().manual_seed(seed)
-        p = torch.zeros(self.n_alloc)
-        off = 0
-        for o, k in [(64, 32), (16, 64), (c.rgb_width, 32), (c.rgb_width, c.rgb_width), (16, c.rgb_width)]:
-            s = math.sqrt(6.0 / (o + k))  # tcnn Xavier-uniform per matrix
-            p[off:off + o * k].uniform_(-s, s, generator=g)
-            off += o * k
-        p[self.off_table:self.n_params].uniform_(-1e-4, 1e-4, generator=g)  # tcnn grid init
-        self.params = p.to(dev)
+        self.params = init_params(c, self.n_params, self.n_alloc, seed).to(dev)
         self.grads = torch.zeros(self.n_alloc, device=dev)
         self.m = torch.zeros(self.n_alloc, device=dev)
         self.v = torch.zeros(self.n_alloc, device=dev)
@@ -339,7 +346,7 @@ class TrainStep:
         + noise) of mb in the same launch."""
         self.dataset.sample(batch.buf, prep=(self.center, self.half_size, NEAR_DISTANCE, mb.hits, mb.noise))
 
-    def _march(self, batch: Batch, mb, mark, prepped=False):
+    def _march(self, batch: Batch, mb, mark, prepped=False, noise=None):
         """AABB + near clamp + noise for the whole batch (unless _draw did it), then one ray march per
         part into mb."""
         c, s = self.cfg, stream()
@@ -350,7 +357,10 @@ class TrainStep:
                  ptr(self.half_size), N, 1, 1, ptr(mb.hit_cnt), ptr(mb.hits), ptr(mb.hits_idx), s)
             t1 = mb.hits[:, 0, 0]
             t1.masked_fill_((t1 >= 0) & (t1 < NEAR_DISTANCE), NEAR_DISTANCE)
-            torch.rand(N, generator=self.gen, device=self.dev, out=mb.noise)
+            if noise is None:
+                torch.rand(N, generator=self.gen, device=self.dev, out=mb.noise)
+            else:  # a given perturbation (parity tests driving the reference with the same draws)
+                mb.noise.copy_(noise)
         mark("prep")
         for q, t in enumerate(mb.part):
             r = slice(q * Np, (q + 1) * Np)
@@ -430,9 +440,12 @@ class TrainStep:
         """Part q's hash-table gradient scatter (the dominant kernel, alone so it can be timed)."""
         t, m = self.parts[q], mb.part[q]
         if self._binned():
+            # both parts in sequence on this stream: the coarse levels' atomics, then the fine levels'
+            # partitioned sums (the two on separate streams inside the graphs measured 1.32 vs
+            # 0.87 ms per step: the extra branch slowed every kernel beside it)
             call("mfnerf_grid_encode_bw_binned", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min, self.x_range,
                  self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws), ptr(self._level_l1),
-                 stream())
+                 3, stream())
             return
         call("mfnerf_grid_encode_bw_scatter", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min, self.x_range,
              self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws),
@@ -519,7 +532,7 @@ class TrainStep:
             else:
                 self._update()
 
-    def run(self, batch: Batch = None, mark=None, exchange=None, optimize=True):
+    def run(self, batch: Batch = None, mark=None, exchange=None, optimize=True, noise=None):
         """One training step, eagerly on the current stream, parts in sequence, march buffer set 0.
         mark(name) is called after each stage (bench timing); exchange(grads) runs between backward
         and Adam (the data-parallel all-reduce).  batch=None: drawn from the attached dataset.
@@ -534,7 +547,7 @@ class TrainStep:
         self._use(mb)
         self.last_batch = batch
         self._primed = False  # a pipelined replay() must march its own batch next
-        self._march(batch, mb, mark, prepped=prepped)
+        self._march(batch, mb, mark, prepped=prepped, noise=noise)
         for q in range(self.n_parts):
             self._chain(batch, mb, q, mark)
             self._grid_bw(mb, q)

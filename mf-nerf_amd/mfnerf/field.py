@@ -52,7 +52,7 @@ def grid_encode_bw(x, n, dL_dfeat, grad_table, layout, desc, x_min=0.0, x_range=
         call("mfnerf_grid_level_l1", ptr(dL_dfeat), int(n), ptr(n_dev), layout.L, ptr(l1), stream())
     if binned:
         call("mfnerf_grid_encode_bw_binned", ptr(x), int(n), ptr(n_dev), float(x_min), float(x_range), desc,
-             ptr(dL_dfeat), ptr(grad_table), ptr(workspace), ptr(l1), stream())
+             ptr(dL_dfeat), ptr(grad_table), ptr(workspace), ptr(l1), 3, stream())
         call("mfnerf_grid_encode_bw_finish", desc, ptr(grad_table), ptr(workspace), ptr(l1), stream())
         return
     call("mfnerf_grid_encode_bw", ptr(x), int(n), ptr(n_dev), float(x_min), float(x_range), desc, ptr(dL_dfeat),

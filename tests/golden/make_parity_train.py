@@ -1,0 +1,95 @@
+"""Generate tests/golden/parity_train.json: a short training run of the REFERENCE's own host code
+(models/rendering.py render + losses.py NeRFLoss + the models/networks.py NGP it trains, with
+this repo's CPU oracle injected as vren / tinycudann exactly as make_golden.py does) under the
+protocol of tests/parity_protocol.py -- BASELINE config 1's shape: 64x64 views, 256 rays per batch,
+Lego's default field (Hash L16 F2 T2^19, rgb 64x2), Adam(lr 1e-2, eps 1e-15) as train.py:136
+configures FusedAdam, fp32 on the CPU.  It records the loss every LOG_EVERY steps and the test-time
+PSNR (rendering.py:46-118, render(test_time=True)) of the held-out views at the end.
+tests/test_gpu_parity_train.py trains this repo's fused MI355X step from the same weights, rays and
+perturbations and checks the held-out PSNR against these numbers (north_star: within 0.2 dB).
+
+Only data is written (numbers); the reference never leaves this container.
+    python tests/golden/make_parity_train.py          (needs /root/reference; CPU, a few minutes)
+"""
+import json
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.dont_write_bytecode = True
+sys.path[:0] = [HERE, os.path.dirname(HERE), ROOT, os.path.join(ROOT, "mf-nerf_amd")]
+
+import make_golden  # noqa: E402  (install_stubs: oracle as vren / tinycudann / torch_scatter)
+import parity_protocol as PP  # noqa: E402
+from oracle import vren_oracle  # noqa: E402
+
+
+class HP:
+    """opt.py defaults (opt.py:70-90) for the Lego field."""
+    grid, L, F, T, N_min, N_max, N_tables, rgb_channels, rgb_layers = "Hash", 16, 2, 19, 16, 2048, 1, 64, 2
+
+
+def main():
+    make_golden.install_stubs()
+    import warnings
+    warnings.filterwarnings("ignore")
+    from losses import NeRFLoss
+    from models import rendering
+    from models.networks import NGP
+
+    torch.set_num_threads(os.cpu_count() or 1)
+    cfg = PP.config()
+    model = NGP(scale=cfg.scale, hparams=HP)
+    xyz0, rgb0 = PP.init_params(cfg)
+    with torch.no_grad():
+        assert model.xyz_encoder.params.numel() == xyz0.numel() and model.rgb_net.params.numel() == rgb0.numel()
+        model.xyz_encoder.params.copy_(xyz0)
+        model.rgb_net.params.copy_(rgb0)
+        vren_oracle.packbits(PP.density_grid().contiguous(), 0.01 * 1024 / 3 ** 0.5, model.density_bitfield)
+    opt = torch.optim.Adam([model.xyz_encoder.params, model.rgb_net.params], lr=PP.LR, eps=1e-15)
+    loss_fn = NeRFLoss(lambda_distortion=0)
+    train, test = PP.scene()
+    hist = []
+    t0 = time.time()
+    real_rand_like = torch.rand_like
+    for step in range(PP.STEPS):
+        o, d, rgb = PP.batch(train, step)
+        nz = PP.noise(step)
+        torch.rand_like = lambda t, *a, **k: nz.clone() if t.shape == nz.shape else real_rand_like(t, *a, **k)
+        try:
+            res = rendering.render(model, o, d)
+        finally:
+            torch.rand_like = real_rand_like
+        ld = loss_fn(res, {"rgb": rgb})
+        loss = sum(v.mean() for v in ld.values())
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        if (step + 1) % PP.LOG_EVERY == 0:
+            pred = res["rgb"].detach()
+            hist.append({"step": step + 1, "loss": float(loss), "train_psnr": PP.psnr(pred, rgb)})
+            print(hist[-1], f"{time.time() - t0:.0f}s", flush=True)
+    imgs, poses, dirs, _ = test
+    views = []
+    with torch.no_grad():
+        for img, pose in zip(imgs, poses):
+            o = pose[:, 3].expand(dirs.shape[0], 3).contiguous()
+            dd = (dirs @ pose[:, :3].T).contiguous()
+            rt = rendering.render(model, o, dd, test_time=True)
+            views.append(PP.psnr(rt["rgb"], img))
+    out = {"protocol": {"W": PP.W, "n_train": PP.N_TRAIN, "n_test": PP.N_TEST, "n_rays": PP.N_RAYS,
+                        "steps": PP.STEPS, "lr": PP.LR, "init_seed": PP.INIT_SEED, "field": "Hash L16 F2 T2^19 rgb64x2",
+                        "occupancy": "fixed ball union", "precision": "fp32 (reference on CPU, oracle kernels)"},
+           "history": hist, "test_psnr_views": views, "test_psnr": sum(views) / len(views),
+           "seconds": round(time.time() - t0, 1)}
+    with open(os.path.join(HERE, "parity_train.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print("test PSNR", out["test_psnr"], views)
+
+
+if __name__ == "__main__":
+    main()

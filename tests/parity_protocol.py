@@ -1,0 +1,76 @@
+"""The short-horizon training-parity protocol (BASELINE config 1 shape: 64x64 views, 256 rays per
+batch), shared by tests/golden/make_parity_train.py (which drives the REFERENCE's own render /
+NeRFLoss with the CPU oracle injected, in the build container) and tests/test_gpu_parity_train.py
+(which drives this repo's fused training step on the GPU).  Everything both sides consume is made
+here, deterministically, on the host: the analytic scene and its views, every step's ray batch and
+march perturbation, the occupancy bitfield and the initial weights.
+
+Deliberate simplifications (identical on both sides): the occupancy grid is the scene's exact ball
+union, held fixed (the refresh cadence is covered by its own bit-exact tests); the learning rate
+stays at its first-epoch value (the cosine schedule steps per 1000-step epoch, train.py:140-142).
+"""
+import math
+
+import torch
+
+from mfnerf import data, engine, synthetic
+
+W = 64                      # config 1: Lego 64x64 (--downsample 0.08)
+FOCAL = 0.5 * W / math.tan(0.5 * 0.6911112)  # the Lego field of view
+N_TRAIN, N_TEST = 40, 4
+N_RAYS = 256                # config 1's batch
+STEPS = 400
+LR = 1e-2
+INIT_SEED = 1337
+LOG_EVERY = 20
+
+
+def config():
+    """The Lego defaults (opt.py): Hash L16 F2 T2^19, N_min 16, N_max 2048, rgb 64x2, scale 0.5."""
+    return engine.StepConfig(n_rays=N_RAYS, lr=LR)
+
+
+def scene():
+    sc = data.BallScene.matching_grid(seed=0)  # the balls of synthetic.ball_density_grid()
+    train = data.ball_scene_views(sc, N_TRAIN, W, FOCAL, seed=3)
+    test = data.ball_scene_views(sc, N_TEST, W, FOCAL, seed=7)
+    return train, test
+
+
+def density_grid():
+    return synthetic.ball_density_grid()
+
+
+def batch(train, step):
+    """(rays_o, rays_d, rgb) of step `step`: a random pixel of a random training view per ray
+    (datasets/base.py:22-35 'all_images'), rays as ray_utils.get_rays builds them."""
+    imgs, poses, dirs, _ = train
+    g = torch.Generator().manual_seed(10000 + step)
+    img = torch.randint(imgs.shape[0], (N_RAYS,), generator=g)
+    pix = torch.randint(imgs.shape[1], (N_RAYS,), generator=g)
+    c2w = poses[img]
+    rays_d = (dirs[pix][:, None, :] @ c2w[:, :, :3].transpose(1, 2))[:, 0].contiguous()
+    rays_o = c2w[:, :, 3].contiguous()
+    return rays_o, rays_d, imgs[img, pix].contiguous()
+
+
+def noise(step):
+    """The march perturbation of step `step` (custom_functions.py:83, torch.rand_like)."""
+    return torch.rand(N_RAYS, generator=torch.Generator().manual_seed(20000 + step))
+
+
+def init_params(cfg):
+    """(xyz_encoder.params = [xyz MLP | table], rgb_net.params) in tcnn's layout, fp32, host."""
+    from mfnerf.field import XYZ_NET_PARAMS, rgb_net_params
+    from mfnerf.grid import GridLayout
+    b = float(math.exp(math.log(cfg.N_max * cfg.scale / cfg.N_min) / (cfg.L - 1)))
+    lay = GridLayout(cfg.L, cfg.F, cfg.log2_T, cfg.N_min, b, cfg.grid, cfg.N_tables)
+    n_rgb = rgb_net_params(cfg.rgb_width)
+    n_params = XYZ_NET_PARAMS + n_rgb + lay.n_params
+    p = engine.init_params(cfg, n_params, n_params, INIT_SEED)
+    xyz = torch.cat([p[:XYZ_NET_PARAMS], p[XYZ_NET_PARAMS + n_rgb:n_params]])
+    return xyz, p[XYZ_NET_PARAMS:XYZ_NET_PARAMS + n_rgb].clone()
+
+
+def psnr(pred, gt):
+    return float(-10.0 * torch.log10(((pred.float() - gt.float()) ** 2).mean()))

@@ -170,6 +170,27 @@ def test_grid_encode_bw_fixed_point_extreme_range(gpu):
     assert int((gt != 0).sum()) == 0
 
 
+def test_grid_encode_bw_binned_slot_overflow_falls_back(gpu):
+    """Pathological input for the partitioned scatter: every sample at one of two points, so each
+    level's records pile into a few partitions and overflow their fixed slots; the device then
+    scatters the partitioned levels by atomics instead -- same sums (vs the fp64 oracle)."""
+    lay = GridLayout(16, 2, 19, 16, LEGO_B)
+    olay = FO.GridLayout(16, 2, 19, 16, LEGO_B)
+    g = torch.Generator().manual_seed(17)
+    N = 40000
+    x = torch.tensor([[0.31, 0.42, 0.53], [0.77, 0.12, 0.64]])[torch.randint(0, 2, (N,), generator=g)]
+    dy = torch.randn(N, 32, generator=g) * 1e-3
+    tp = torch.zeros(lay.n_params).requires_grad_(True)
+    (FO.grid_encode(x, tp, olay).double() * dy.double()).sum().backward()
+    gref = tp.grad.double()
+    desc = lay.desc()
+    gt = torch.zeros(lay.n_params, device=gpu)
+    FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=FLD.grid_bw_binned_workspace(desc, N, gpu),
+                       binned=True)
+    got = gt.cpu().double()
+    assert float((got - gref).abs().max()) <= 1e-4 * float(gref.abs().max())
+
+
 def test_grid_encode_world_coords_normalisation(gpu):
     lay = GridLayout(16, 2, 19, 16, LEGO_B)
     olay = FO.GridLayout(16, 2, 19, 16, LEGO_B)
