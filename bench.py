@@ -24,7 +24,9 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "mf-nerf_amd")]
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-GRID_BW_KERNEL = "grid_bw_kernel"  # the table-gradient scatter's kernel name in the PMC summaries
+# the table-gradient scatter's kernels in the PMC summaries: the run-merging atomics (dense and coarse
+# hashed levels) and the partitioned fine levels' scatter / accumulate / (idle) fallback
+GRID_BW_KERNEL = ("grid_bw_kernel", "bin_scatter_kernel", "bin_accum_kernel", "bin_fallback_kernel")
 
 # algorithmic bytes per live sample of each per-sample kernel, as SURVEY.md 8(d) prices them (the
 # tcnn form of the op: fp16 features and fp16 gradient scatter), DESIGN.md section 5
@@ -86,7 +88,8 @@ def run_step(step, batch, world, ev=None):
 
 
 def pmc_traffic(kernel_prefix):
-    """(HBM-side bytes, memory-side atomic requests, source) per launch of a kernel from the newest
+    """(HBM-side bytes, memory-side atomic requests, source) per launch, summed over the kernels whose
+    names start with one of `kernel_prefix` (one step's launches of them), from the newest
     committed PMC summary (profiles/rNN_*pmc_traffic.json, made by tools/pmc_traffic.py from separate
     FETCH_SIZE / WRITE_SIZE / TCC_EA0_ATOMIC rocprofv3 passes with the guide's gfx950 corrections);
     Nones if absent."""
@@ -100,10 +103,12 @@ def pmc_traffic(kernel_prefix):
     if not files:
         return None, None, None
     d = json.load(open(files[-1]))
-    for k, v in d["kernels"].items():
-        if k.startswith(kernel_prefix):
-            return round(v["traffic_bytes"]), v.get("atomic_requests"), os.path.relpath(files[-1], ROOT)
-    return None, None, None
+    hits = [v for k, v in d["kernels"].items() if any(k.startswith(p) for p in kernel_prefix)]
+    if not hits:
+        return None, None, None
+    req = [v.get("atomic_requests") for v in hits]
+    return (round(sum(v["traffic_bytes"] for v in hits)), sum(req) if all(r is not None for r in req) else None,
+            os.path.relpath(files[-1], ROOT))
 
 
 def stage_times(events, steps):
@@ -241,7 +246,7 @@ def main():
     use_graph = not args.eager
     if use_graph:
         step.capture()
-        for i in range(5):
+        for i in range(20):  # the first replays of fresh graphs run slow: settle before timing
             step.replay(exchange=ex)
     mk = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     gb_ev = [(mk(), [mk() for _ in range(step.n_parts)]) for _ in range(args.steps)]
@@ -312,7 +317,8 @@ def main():
                        "preset": args.preset, "global_batch": args.n_rays * world, "rm_s": round(mean_samples / args.n_rays, 2),
                        "parallelism": f"dp{world}" + ("-sharded-adam" if world > 1 and args.dp == "shard" else ""),
                        "psnr": None},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": dom + " (" + "+".join(GRID_BW_KERNEL) + ")",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
                          "timed_launches": (len(range(0, args.steps, args.roofline_every)) if use_graph

@@ -224,14 +224,18 @@ int mfnerf_grid_encode_bw_finish(const mfnerf_grid_desc* desc, float* grad_table
  * into the workspace's private copies, as mfnerf_grid_encode_bw_scatter), 2 = the partitioned levels
  * only, 3 = both -- 1 and 2 may run concurrently on two streams.  The workspace prefix is the private
  * copies, so mfnerf_grid_encode_bw_finish / mfnerf_adam_step_fixed convert the result unchanged;
- * grad_table must be zero on entry.  workspace: mfnerf_grid_encode_bw_binned_workspace(desc, n)
- * bytes for this call's n, its copies zero on the first call (left zero by the finish).
+ * grad_table must be zero on entry.  workspace: mfnerf_grid_encode_bw_binned_workspace(desc, n_slots)
+ * bytes, its copies zero on the first call (left zero by the finish); n_slots (0 or > n: n) is the
+ * live sample count the record slots are sized for -- a training step passes its expected count,
+ * not its capacity (rays x 1024 samples): a live count well above n_slots overflows slots and takes
+ * the atomic fallback (same result, slower).
  * Bit-reproducible.  Replaces tcnn's hash-grid backward scatter (networks.py:36-49 encoding, half2
  * atomics there). */
 int64_t mfnerf_grid_encode_bw_binned_workspace(const mfnerf_grid_desc* desc, int64_t n_max);
 int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                                  const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
-                                 void* workspace, const float* level_l1, int parts, mfnerf_stream_t stream);
+                                 void* workspace, int64_t n_slots, const float* level_l1, int parts,
+                                 mfnerf_stream_t stream);
 
 /* out[l] += sum over rows i < n (or *n_dev) of |dL_dout[i][2l]| + |dL_dout[i][2l+1]| (f32). */
 int mfnerf_grid_level_l1(const float* dL_dout, int64_t n, const int32_t* n_dev, int n_levels, float* out,

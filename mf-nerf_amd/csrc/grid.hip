@@ -337,7 +337,11 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restr
                                                              float x_range, const mfnerf_grid_desc D,
                                                              const float* __restrict__ dy, float* __restrict__ grad,
                                                              float* __restrict__ priv, int64_t dense_entries,
-                                                             const float* __restrict__ level_l1, int l_end) {
+                                                             const float* __restrict__ level_l1, int l_end,
+                                                             int32_t* __restrict__ zero_flag) {
+    // zero_flag: a flag the NEXT launches on the stream start from zero (the binned scatter's slot
+    // overflow), cleared here instead of by a memset launch of its own
+    if (zero_flag && blockIdx.x == 0 && threadIdx.x == 0) *zero_flag = 0;
     grid_bw_body<ABLATE, MAXL, FIX>(blockIdx.x, gridDim.x, X, n, n_dev, x_min, x_range, D, dy, grad, priv,
                                     dense_entries, level_l1, l_end);
 }
@@ -772,15 +776,18 @@ __device__ __forceinline__ int wave_block_scan(int v, int* out) {
 // k < scnt[b * UNITS + u] -- no counting pass, no scan.  slot = 2 * (mean records per slot at this
 // step's live count) -- 3 x the mean + 96, so the buffer (sized for the largest live count) always holds them; a
 // slot that still overflows (a pathological sample distribution) raises `ovf`, and then the
-// accumulate stores nothing and bin_fallback_kernel scatters the binned levels by atomics instead.
+// accumulate launch scatters the binned levels by grid_bw_body's atomics instead of summing slots.
 constexpr int UNITS = 256;       // scatter workgroups, each owning a contiguous sample range
 constexpr int SC_THREADS = 1024;
 constexpr int MAX_TBINS = 1024;  // bins of one table
 constexpr int SC_STAGE = SC_THREADS * 8;  // staged records per tile (8 per thread)
 
-__device__ __forceinline__ int64_t slot_size(int64_t nn, const BinPlan& P) {
+// records per (partition, unit) slot at live count nn; non-decreasing in nn, so the workspace sized
+// with slot_size(n_max) (binned_workspace_layout) holds every slot of any nn <= n_max
+__host__ __device__ __forceinline__ int64_t slot_size(int64_t nn, const BinPlan& P) {
     const int64_t recs = nn * P.n_binned * (P.pair_ok ? 4 : 8);
-    return 3 * ((recs + (int64_t)P.n_bins * UNITS - 1) / ((int64_t)P.n_bins * UNITS)) + 96;
+    const int64_t s = 3 * ((recs + (int64_t)P.n_bins * UNITS - 1) / ((int64_t)P.n_bins * UNITS)) + 96;
+    return (s + 15) / 16 * 16;  // 16 records = 192 B: every slot starts on a 64-B line
 }
 
 // pass 1: unit u (one 1024-thread workgroup) walks its samples, staged in registers, level by level
@@ -793,7 +800,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                                                                  const BinPlan P, const float* __restrict__ dy,
                                                                  const float* __restrict__ level_l1,
                                                                  uint3* __restrict__ rec, int32_t* __restrict__ scnt,
-                                                                 int32_t* __restrict__ ovf) {
+                                                                 int32_t* __restrict__ ovf, int64_t n_slots) {
     __shared__ int cursor[MAX_BINS];
     __shared__ int thist[MAX_TBINS], toff[MAX_TBINS], gdst[MAX_TBINS];
     __shared__ uint3 stage[SC_STAGE];
@@ -803,7 +810,8 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
     for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x) cursor[b] = 0;
     __syncthreads();
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
-    const int64_t slot = slot_size(nn, P);
+    // slots sized for at most the workspace's count: beyond it a slot may overflow (-> atomics)
+    const int64_t slot = slot_size(min(nn, n_slots), P);
     // unit u owns the 16-sample chunks u, u + UNITS, u + 2 UNITS, ...: a ray's samples (which repeat
     // the coarse levels' rows) spread over many units, so every slot fills close to the mean
     const int u = blockIdx.x;
@@ -904,22 +912,31 @@ __device__ __forceinline__ void accum_record(unsigned long long* img, int mask, 
     }
 }
 
-constexpr int ACC_THREADS = 512;
+constexpr int ACC_THREADS = ENC_BLOCK;  // = grid_bw_body's block: the fallback runs in the same launch
 
+template <int MAXL>
 __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, int64_t n,
                                                                 const int32_t* __restrict__ n_dev,
                                                                 const uint3* __restrict__ rec,
                                                                 const int32_t* __restrict__ scnt,
                                                                 const int32_t* __restrict__ ovf,
-                                                                int* __restrict__ grad) {
-    if (*ovf) return;  // a slot overflowed: bin_fallback_kernel scatters the binned levels
+                                                                int* __restrict__ grad, const float* __restrict__ X,
+                                                                float x_min, float x_range, const mfnerf_grid_desc D,
+                                                                const float* __restrict__ dy,
+                                                                const float* __restrict__ level_l1, int levels,
+                                                                int64_t n_slots) {
+    if (*ovf) {  // a slot overflowed: the binned levels by request-shaped atomics instead (rare)
+        grid_bw_body<0, MAXL, true>(blockIdx.x, gridDim.x, X, n, n_dev, x_min, x_range, D, dy, (float*)grad,
+                                    nullptr, 0, level_l1, levels);
+        return;
+    }
     __shared__ unsigned long long img[2 * MAX_BIN_ENTRIES];
     const int bin = blockIdx.x;
     const int n_ent = 1 << P.shift, mask = n_ent - 1;
     for (int i = threadIdx.x; i < 2 * n_ent; i += blockDim.x) img[i] = 0;
     __syncthreads();
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
-    const int64_t slot = slot_size(nn, P);
+    const int64_t slot = slot_size(min(nn, n_slots), P);  // = bin_scatter_kernel's
     // one unit's slot per half-wave (32 lanes; ~30 records per slot at the Lego config), 4 slots
     // in flight per half-wave
     const int hw = threadIdx.x >> 5, hl = threadIdx.x & 31, n_hw = ACC_THREADS / 32;
@@ -947,19 +964,6 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     const int n_e = (int)min<int64_t>(n_ent, (int64_t)P.t_size[t] - e_lo);
     int* dst = grad + 2 * ((int64_t)P.t_offset[t] + e_lo);
     for (int i = threadIdx.x; i < 2 * n_e; i += blockDim.x) dst[i] = round_shift32((long long)img[i]);
-}
-
-// the binned levels by request-shaped int32 atomics (grid_bw_body), only if a slot overflowed
-template <int MAXL>
-__global__ __launch_bounds__(ENC_BLOCK) void bin_fallback_kernel(const float* __restrict__ X, int64_t n,
-                                                                 const int32_t* __restrict__ n_dev, float x_min,
-                                                                 float x_range, const mfnerf_grid_desc D,
-                                                                 const float* __restrict__ dy, float* grad,
-                                                                 const float* __restrict__ level_l1,
-                                                                 const int32_t* __restrict__ ovf, int levels) {
-    if (!*ovf) return;
-    grid_bw_body<0, MAXL, true>(blockIdx.x, gridDim.x, X, n, n_dev, x_min, x_range, D, dy, grad, nullptr, 0,
-                                level_l1, levels);
 }
 
 // The plan for a desc: binned levels = every level that is not a dense own table; tables in address
@@ -1055,9 +1059,8 @@ int64_t binned_workspace_layout(const mfnerf_grid_desc* d, int64_t n_max, char* 
     if (W) W->ovf = reinterpret_cast<int32_t*>(base + off);
     off += 256;
     if (W) W->rec = reinterpret_cast<uint3*>(base + off);
-    // slots at the largest live count: 3 x (its records + one per slot) + 96 per slot (slot_size)
-    const int64_t recs = n_max * P.n_binned * (P.pair_ok ? 4 : 8);
-    off += align256((3 * recs + 3 * nb * UNITS + 96 * nb * UNITS) * (int64_t)sizeof(uint3));
+    // every slot at the largest live count (the same function the kernels size them with)
+    off += align256(nb * UNITS * slot_size(n_max, P) * (int64_t)sizeof(uint3));
     return off;
 }
 
@@ -1116,12 +1119,13 @@ int mfnerf_grid_encode_bw_scatter(const float* x, int64_t n, const int32_t* n_de
     if (level_l1) {
         auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, true> : grid_bw_kernel<0, 16, true>;
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range,
-                           *desc, dL_dout, grad_table, (float*)workspace, dense, level_l1, desc->n_levels);
+                           *desc, dL_dout, grad_table, (float*)workspace, dense, level_l1, desc->n_levels,
+                           (int32_t*)nullptr);
     } else {
         auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, false> : grid_bw_kernel<0, 16, false>;
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range,
                            *desc, dL_dout, grad_table, (float*)workspace, dense, (const float*)nullptr,
-                           desc->n_levels);
+                           desc->n_levels, (int32_t*)nullptr);
     }
     return mfn_check_launch("grid_encode_bw_scatter");
 }
@@ -1265,7 +1269,8 @@ int mfnerf_debug_grid_bw_ablate(int mode, const float* x, int64_t n, const int32
              : mode == 3 ? grid_bw_kernel<3, 16, false>
                          : grid_bw_kernel<0, 16, false>;
     hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc,
-                       dL_dout, grad_table, nullptr, (int64_t)0, (const float*)nullptr, desc->n_levels);
+                       dL_dout, grad_table, nullptr, (int64_t)0, (const float*)nullptr, desc->n_levels,
+                       (int32_t*)nullptr);
     return mfn_check_launch("grid_bw_ablate");
 }
 
@@ -1278,9 +1283,11 @@ int64_t mfnerf_grid_encode_bw_binned_workspace(const mfnerf_grid_desc* desc, int
 
 int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                                  const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
-                                 void* workspace, const float* level_l1, int parts, mfnerf_stream_t stream) {
+                                 void* workspace, int64_t n_slots, const float* level_l1, int parts,
+                                 mfnerf_stream_t stream) {
     int st = check_desc(desc, "grid_encode_bw_binned");
     if (st) return st;
+    if (n_slots <= 0 || n_slots > n) n_slots = n;
     if (n < 0 || parts < 1 || parts > 3) { mfn_set_error("grid_encode_bw_binned: bad size or parts"); return MFN_ERR_INVALID; }
     if (n == 0) return MFN_OK;
     if (!x || !dL_dout || !grad_table || !workspace || !level_l1) {
@@ -1294,7 +1301,7 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
         return MFN_ERR_INVALID;
     }
     BinWorkspace W;
-    binned_workspace_layout(desc, n, (char*)workspace, &W);
+    binned_workspace_layout(desc, n_slots, (char*)workspace, &W);
     const int l_first = first_binned_level(desc);
     const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16), ENC_BLOCK / 64);
     const int64_t cap = grid_bw_block_cap();
@@ -1303,18 +1310,18 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
     if ((parts & 1) && l_first > 0) {  // dense levels [0, l_first): request-shaped atomics, private copies
         auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, true> : grid_bw_kernel<0, 16, true>;
         hipLaunchKernelGGL(kern, dim3((unsigned)atomic_blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min,
-                           x_range, *desc, dL_dout, grad_table, W.priv, dense_entries_of(desc), level_l1, l_first);
+                           x_range, *desc, dL_dout, grad_table, W.priv, dense_entries_of(desc), level_l1, l_first,
+                           (parts & 2) ? W.ovf : (int32_t*)nullptr);
     }
     if ((parts & 2) && P.n_bins > 0) {
-        (void)hipMemsetAsync(W.ovf, 0, sizeof(int32_t), stream);
+        if (!((parts & 1) && l_first > 0)) (void)hipMemsetAsync(W.ovf, 0, sizeof(int32_t), stream);
         hipLaunchKernelGGL(bin_scatter_kernel, dim3(UNITS), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
-                           *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.ovf);
-        hipLaunchKernelGGL(bin_accum_kernel, dim3(P.n_bins), dim3(ACC_THREADS), 0, stream, P, n, n_dev, W.rec,
-                           W.scnt, W.ovf, (int*)grad_table);
-        // levels [l_first, L) by atomics, only when a slot overflowed (exits at once otherwise)
-        auto fb = big ? bin_fallback_kernel<MFN_MAX_LEVELS> : bin_fallback_kernel<16>;
-        hipLaunchKernelGGL(fb, dim3(256), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc, dL_dout,
-                           grad_table, level_l1, W.ovf, (l_first << 8) | desc->n_levels);
+                           *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.ovf, n_slots);
+        // the per-partition sums -- or, if a slot overflowed, levels [l_first, L) by atomics
+        auto acc = big ? bin_accum_kernel<MFN_MAX_LEVELS> : bin_accum_kernel<16>;
+        hipLaunchKernelGGL(acc, dim3(P.n_bins), dim3(ACC_THREADS), 0, stream, P, n, n_dev, W.rec, W.scnt, W.ovf,
+                           (int*)grad_table, x, x_min, x_range, *desc, dL_dout, level_l1,
+                           (l_first << 8) | desc->n_levels, n_slots);
     }
     return mfn_check_launch("grid_encode_bw_binned");
 }

@@ -63,7 +63,8 @@ SIGNATURES = {
     "mfnerf_grid_encode_bw_scatter": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _P, _P]),
     "mfnerf_grid_encode_bw_finish": (_I, [ctypes.POINTER(GridDesc), _P, _P, _P, _P]),
     "mfnerf_grid_encode_bw_binned_workspace": (_I64, [ctypes.POINTER(GridDesc), _I64]),
-    "mfnerf_grid_encode_bw_binned": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _P, _I, _P]),
+    "mfnerf_grid_encode_bw_binned": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _I64, _P, _I,
+                                          _P]),
     "mfnerf_grid_level_l1": (_I, [_P, _I64, _P, _I, _P, _P]),
     "mfnerf_debug_grid_bw_half": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _F, _P]),
     "mfnerf_debug_grid_bw_ablate": (_I, [_I, _P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P]),

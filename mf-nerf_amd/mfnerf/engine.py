@@ -65,6 +65,10 @@ class StepConfig:
     # ... of the hashed tables by partitioned LDS sums (mfnerf_grid_encode_bw_binned); MFNERF_BINNED=0
     # selects the memory-side-atomic scatter for A/B measurements
     binned_grid: bool = os.environ.get("MFNERF_BINNED", "1") == "1"
+    # the binned scatter's record slots are sized for this many samples per ray (the capacity is
+    # max_samples = 1024 per ray; trained scenes march ~60): a step marching more than ~3x this
+    # (the first steps, before the occupancy grid is pruned) takes the atomic fallback
+    bin_samples_per_ray: int = 128
 
 
 @dataclass
@@ -234,7 +238,7 @@ class TrainStep:
         t.dfeat = torch.empty(cap, c.L * c.F, **f32)
         t.field_ws = torch.empty(load().mfnerf_field_bw_workspace(cap, c.rgb_width) // 4, **f32)
         if self._binned():
-            nb = load().mfnerf_grid_encode_bw_binned_workspace(self.desc, cap)
+            nb = load().mfnerf_grid_encode_bw_binned_workspace(self.desc, self._bin_slots())
             if nb < 0:
                 raise ValueError("grid layout unsupported by the binned table-gradient scatter")
         else:
@@ -436,6 +440,10 @@ class TrainStep:
         """The fixed-point table gradient by table partitions (one part only, like _fixed)."""
         return self.cfg.n_parts == 1 and self.cfg.fixed_point_grid and self.cfg.binned_grid
 
+    def _bin_slots(self):
+        """Samples per part the binned scatter's record slots are sized for."""
+        return min(self.cap_p, self.Np * max(1, self.cfg.bin_samples_per_ray))
+
     def _grid_bw(self, mb, q):
         """Part q's hash-table gradient scatter (the dominant kernel, alone so it can be timed)."""
         t, m = self.parts[q], mb.part[q]
@@ -444,8 +452,8 @@ class TrainStep:
             # partitioned sums (the two on separate streams inside the graphs measured 1.32 vs
             # 0.87 ms per step: the extra branch slowed every kernel beside it)
             call("mfnerf_grid_encode_bw_binned", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min, self.x_range,
-                 self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws), ptr(self._level_l1),
-                 3, stream())
+                 self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws), self._bin_slots(),
+                 ptr(self._level_l1), 3, stream())
             return
         call("mfnerf_grid_encode_bw_scatter", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min, self.x_range,
              self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws),

@@ -42,17 +42,18 @@ def grid_bw_binned_workspace(desc, n, device):
 
 
 def grid_encode_bw(x, n, dL_dfeat, grad_table, layout, desc, x_min=0.0, x_range=1.0, n_dev=None, workspace=None,
-                   fixed_point=False, binned=False):
+                   fixed_point=False, binned=False, n_slots=0):
     """Accumulates into grad_table (float atomics); fixed_point=True: int32 fixed-point atomics with
     per-level scales from the L1 norm of dL_dfeat (grad_table must be zero; it is overwritten);
-    binned=True (implies fixed point): the partitioned LDS scatter (workspace: grid_bw_binned_workspace)."""
+    binned=True (implies fixed point): the partitioned LDS scatter (workspace:
+    grid_bw_binned_workspace(desc, n_slots or n); n_slots: the count its record slots are sized for)."""
     l1 = None
     if fixed_point or binned:
         l1 = torch.zeros(layout.L, dtype=torch.float32, device=x.device)
         call("mfnerf_grid_level_l1", ptr(dL_dfeat), int(n), ptr(n_dev), layout.L, ptr(l1), stream())
     if binned:
         call("mfnerf_grid_encode_bw_binned", ptr(x), int(n), ptr(n_dev), float(x_min), float(x_range), desc,
-             ptr(dL_dfeat), ptr(grad_table), ptr(workspace), ptr(l1), 3, stream())
+             ptr(dL_dfeat), ptr(grad_table), ptr(workspace), int(n_slots), ptr(l1), 3, stream())
         call("mfnerf_grid_encode_bw_finish", desc, ptr(grad_table), ptr(workspace), ptr(l1), stream())
         return
     call("mfnerf_grid_encode_bw", ptr(x), int(n), ptr(n_dev), float(x_min), float(x_range), desc, ptr(dL_dfeat),

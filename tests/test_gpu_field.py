@@ -191,6 +191,30 @@ def test_grid_encode_bw_binned_slot_overflow_falls_back(gpu):
     assert float((got - gref).abs().max()) <= 1e-4 * float(gref.abs().max())
 
 
+@pytest.mark.parametrize("div", [1, 2, 16])
+def test_grid_encode_bw_binned_slots_sized_below_the_count(gpu, div):
+    """The record slots sized for n_slots = n / div samples (a training step sizes them for its
+    expected count, not its capacity): a live count within ~3x of it still bins; far above it the
+    slots overflow and the device falls back to atomics -- the same sums either way."""
+    lay = GridLayout(16, 2, 19, 16, LEGO_B)
+    olay = FO.GridLayout(16, 2, 19, 16, LEGO_B)
+    g = torch.Generator().manual_seed(21)
+    N = 20000
+    x = torch.rand(N, 3, generator=g)
+    dy = torch.randn(N, 32, generator=g) * 1e-3
+    tp = torch.zeros(lay.n_params).requires_grad_(True)
+    (FO.grid_encode(x, tp, olay).double() * dy.double()).sum().backward()
+    gref = tp.grad.double()
+    desc = lay.desc()
+    ns = N // div
+    ws = FLD.grid_bw_binned_workspace(desc, ns, gpu)
+    assert ws.numel() * 4 == max(16, load().mfnerf_grid_encode_bw_binned_workspace(desc, ns))
+    gt = torch.zeros(lay.n_params, device=gpu)
+    FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=ws, binned=True, n_slots=ns)
+    got = gt.cpu().double()
+    assert float((got - gref).abs().max()) <= 1e-4 * float(gref.abs().max())
+
+
 def test_grid_encode_world_coords_normalisation(gpu):
     lay = GridLayout(16, 2, 19, 16, LEGO_B)
     olay = FO.GridLayout(16, 2, 19, 16, LEGO_B)
