@@ -776,7 +776,7 @@ __device__ __forceinline__ int wave_block_scan(int v, int* out) {
 // k < scnt[b * UNITS + u] -- no counting pass, no scan.  slot = 2 * (mean records per slot at this
 // step's live count) -- 3 x the mean + 96, so the buffer (sized for the largest live count) always holds them; a
 // slot that still overflows (a pathological sample distribution) raises `ovf`, and then the
-// accumulate launch scatters the binned levels by grid_bw_body's atomics instead of summing slots.
+// accumulate stores nothing and bin_fallback_kernel scatters the binned levels by atomics instead.
 constexpr int UNITS = 256;       // scatter workgroups, each owning a contiguous sample range
 constexpr int SC_THREADS = 1024;
 constexpr int MAX_TBINS = 1024;  // bins of one table
@@ -787,7 +787,10 @@ constexpr int SC_STAGE = SC_THREADS * 8;  // staged records per tile (8 per thre
 __host__ __device__ __forceinline__ int64_t slot_size(int64_t nn, const BinPlan& P) {
     const int64_t recs = nn * P.n_binned * (P.pair_ok ? 4 : 8);
     const int64_t s = 3 * ((recs + (int64_t)P.n_bins * UNITS - 1) / ((int64_t)P.n_bins * UNITS)) + 96;
-    return (s + 15) / 16 * 16;  // 16 records = 192 B: every slot starts on a 64-B line
+#ifndef MFN_SLOT_ALIGN
+#define MFN_SLOT_ALIGN 16  // 16 records = 192 B: every slot starts on a 64-B line
+#endif
+    return (s + MFN_SLOT_ALIGN - 1) / MFN_SLOT_ALIGN * MFN_SLOT_ALIGN;
 }
 
 // pass 1: unit u (one 1024-thread workgroup) walks its samples, staged in registers, level by level
@@ -912,24 +915,15 @@ __device__ __forceinline__ void accum_record(unsigned long long* img, int mask, 
     }
 }
 
-constexpr int ACC_THREADS = ENC_BLOCK;  // = grid_bw_body's block: the fallback runs in the same launch
+constexpr int ACC_THREADS = 512;
 
-template <int MAXL>
 __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, int64_t n,
                                                                 const int32_t* __restrict__ n_dev,
                                                                 const uint3* __restrict__ rec,
                                                                 const int32_t* __restrict__ scnt,
                                                                 const int32_t* __restrict__ ovf,
-                                                                int* __restrict__ grad, const float* __restrict__ X,
-                                                                float x_min, float x_range, const mfnerf_grid_desc D,
-                                                                const float* __restrict__ dy,
-                                                                const float* __restrict__ level_l1, int levels,
-                                                                int64_t n_slots) {
-    if (*ovf) {  // a slot overflowed: the binned levels by request-shaped atomics instead (rare)
-        grid_bw_body<0, MAXL, true>(blockIdx.x, gridDim.x, X, n, n_dev, x_min, x_range, D, dy, (float*)grad,
-                                    nullptr, 0, level_l1, levels);
-        return;
-    }
+                                                                int* __restrict__ grad, int64_t n_slots) {
+    if (*ovf) return;  // a slot overflowed: bin_fallback_kernel scatters the binned levels
     __shared__ unsigned long long img[2 * MAX_BIN_ENTRIES];
     const int bin = blockIdx.x;
     const int n_ent = 1 << P.shift, mask = n_ent - 1;
@@ -964,6 +958,20 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     const int n_e = (int)min<int64_t>(n_ent, (int64_t)P.t_size[t] - e_lo);
     int* dst = grad + 2 * ((int64_t)P.t_offset[t] + e_lo);
     for (int i = threadIdx.x; i < 2 * n_e; i += blockDim.x) dst[i] = round_shift32((long long)img[i]);
+}
+
+// the binned levels by request-shaped int32 atomics (grid_bw_body), only if a slot overflowed (a
+// launch of its own: grid_bw_body's registers inside bin_accum_kernel halve that kernel's occupancy)
+template <int MAXL>
+__global__ __launch_bounds__(ENC_BLOCK) void bin_fallback_kernel(const float* __restrict__ X, int64_t n,
+                                                                 const int32_t* __restrict__ n_dev, float x_min,
+                                                                 float x_range, const mfnerf_grid_desc D,
+                                                                 const float* __restrict__ dy, float* grad,
+                                                                 const float* __restrict__ level_l1,
+                                                                 const int32_t* __restrict__ ovf, int levels) {
+    if (!*ovf) return;
+    grid_bw_body<0, MAXL, true>(blockIdx.x, gridDim.x, X, n, n_dev, x_min, x_range, D, dy, grad, nullptr, 0,
+                                level_l1, levels);
 }
 
 // The plan for a desc: binned levels = every level that is not a dense own table; tables in address
@@ -1317,11 +1325,12 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
         if (!((parts & 1) && l_first > 0)) (void)hipMemsetAsync(W.ovf, 0, sizeof(int32_t), stream);
         hipLaunchKernelGGL(bin_scatter_kernel, dim3(UNITS), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
                            *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.ovf, n_slots);
-        // the per-partition sums -- or, if a slot overflowed, levels [l_first, L) by atomics
-        auto acc = big ? bin_accum_kernel<MFN_MAX_LEVELS> : bin_accum_kernel<16>;
-        hipLaunchKernelGGL(acc, dim3(P.n_bins), dim3(ACC_THREADS), 0, stream, P, n, n_dev, W.rec, W.scnt, W.ovf,
-                           (int*)grad_table, x, x_min, x_range, *desc, dL_dout, level_l1,
-                           (l_first << 8) | desc->n_levels, n_slots);
+        hipLaunchKernelGGL(bin_accum_kernel, dim3(P.n_bins), dim3(ACC_THREADS), 0, stream, P, n, n_dev, W.rec,
+                           W.scnt, W.ovf, (int*)grad_table, n_slots);
+        // levels [l_first, L) by atomics, only when a slot overflowed (exits at once otherwise)
+        auto fb = big ? bin_fallback_kernel<MFN_MAX_LEVELS> : bin_fallback_kernel<16>;
+        hipLaunchKernelGGL(fb, dim3(256), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc, dL_dout,
+                           grad_table, level_l1, W.ovf, (l_first << 8) | desc->n_levels);
     }
     return mfn_check_launch("grid_encode_bw_binned");
 }
