@@ -258,7 +258,12 @@ __device__ __forceinline__ void forward_tile(const _Float16* lds, int lane, cons
         for (int i = 0; i < 16; ++i) shv[i] = 0.0f;
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) T.sh[j] = (_Float16)(h ? shv[8 + j] : shv[j]);
+    for (int j = 0; j < 8; ++j) {
+        // select the loaded VALUES (a conditional of the two array lvalues is an lvalue: a load
+        // through a selected pointer, which kept shv in scratch memory)
+        const float lo = shv[j], hi = shv[8 + j];
+        T.sh[j] = (_Float16)(h ? hi : lo);
+    }
     // rgb layer 1
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {

@@ -36,15 +36,28 @@ __device__ __forceinline__ LevelGeo level_geo(float scale, float x, float y, flo
 
 // tcnn grid_index: dense strides while res^3 <= size, else the coherent prime hash; `% size`.
 // MixedFeature shared tables hash the point's coordinates on the canonical grid.
+// floor(x * rc / res) exactly, for x * rc < 2^31 (check_desc): the float quotient is within one of
+// it (relative error ~2^-22 on a quotient <= 2^16), one integer correction each way.  A 64-bit
+// division here (24 of them per sample-level, inlined) made the scatter kernels' code outgrow the
+// instruction cache.
+__device__ __forceinline__ uint32_t canon_coord(uint32_t x, uint32_t rc, uint32_t res, float inv) {
+    const uint32_t n = x * rc;
+    uint32_t q = (uint32_t)((float)n * inv);
+    if (q * res > n) --q;
+    else if ((q + 1) * res <= n) ++q;
+    return q;
+}
+
 __device__ __forceinline__ uint32_t corner_index(const mfnerf_grid_desc& D, int l, uint32_t x, uint32_t y,
                                                  uint32_t z) {
     const uint32_t res = D.res[l], size = D.size[l];
     uint32_t idx;
     if (D.table_kind[l] == 1) {
         const uint32_t rc = (uint32_t)D.canon_res;
-        x = (uint32_t)(((uint64_t)x * rc) / res);
-        y = (uint32_t)(((uint64_t)y * rc) / res);
-        z = (uint32_t)(((uint64_t)z * rc) / res);
+        const float inv = 1.0f / (float)res;  // one per level after CSE over the corners
+        x = canon_coord(x, rc, res, inv);
+        y = canon_coord(y, rc, res, inv);
+        z = canon_coord(z, rc, res, inv);
         idx = (x * 1u) ^ (y * PRIME1) ^ (z * PRIME2);
     } else if ((uint64_t)res * res * res <= size) {
         idx = x + y * res + z * res * res;
@@ -605,7 +618,9 @@ int check_desc(const mfnerf_grid_desc* d, const char* what) {
         return MFN_ERR_INVALID;
     }
     for (int l = 0; l < d->n_levels; ++l)
-        if (d->size[l] == 0 || d->res[l] == 0 || d->table_kind[l] < 0 || d->table_kind[l] > 1) {
+        if (d->size[l] == 0 || d->res[l] == 0 || d->table_kind[l] < 0 || d->table_kind[l] > 1 ||
+            // the canonical-grid map computes (coord + 1) * canon_res in 32 bits (canon_coord)
+            (d->table_kind[l] == 1 && ((uint64_t)d->res[l] + 2) * (uint64_t)d->canon_res >= (1ull << 31))) {
             mfn_set_error("%s: bad level %d", what, l); return MFN_ERR_INVALID;
         }
     return MFN_OK;
@@ -683,60 +698,47 @@ __device__ __forceinline__ void level_records(const mfnerf_grid_desc& D, const B
         const uint32_t i1 = corner_index(D, l, Lg.g[0] + 1, gy, gz);
         const int b0 = bin0 + (int)(i0 >> P.shift), b1 = bin0 + (int)(i1 >> P.shift);
         const uint32_t a = __float_as_uint(wyz * s0), b = __float_as_uint(wyz * s1);
-        if (pair_hash && b0 == b1) {
-            emit(b0, make_uint3((i0 & mask) | (ones << 11) | fxq, a, b));
-        } else {
-            emit(b0, make_uint3((i0 & mask) | (1u << 15) | fxq, a, b));
-            emit(b1, make_uint3((i1 & mask) | (1u << 15) | (1u << 16) | fxq, a, b));
-        }
+        // static record slots 2 yz, 2 yz + 1, both always emitted (bin -1: no record), so the
+        // caller's per-slot register arrays see constant indices on every path and stay registers
+        const bool pair = pair_hash && b0 == b1;
+        emit(2 * yz, b0, make_uint3((i0 & mask) | (pair ? (ones << 11) : (1u << 15)) | fxq, a, b));
+        emit(2 * yz + 1, pair ? -1 : b1, make_uint3((i1 & mask) | (1u << 15) | (1u << 16) | fxq, a, b));
     }
 }
 
 
-// the records of sample i at binned level j (nothing for a zero dL/dy: terminated samples)
-template <typename EMIT>
-__device__ __forceinline__ void sample_records(const mfnerf_grid_desc& D, const BinPlan& P, const float* __restrict__ X,
-                                               float x_min, float x_range, const float* __restrict__ dy,
-                                               const float* fs_s, int64_t i, int j, EMIT&& emit) {
-    const int l = P.level[j];
-    const float2 g = *reinterpret_cast<const float2*>(dy + i * (2 * D.n_levels) + 2 * l);
-    if (g.x == 0.0f && g.y == 0.0f) return;
-    const float x = (X[3 * i] - x_min) / x_range;
-    const float y = (X[3 * i + 1] - x_min) / x_range;
-    const float z = (X[3 * i + 2] - x_min) / x_range;
-    level_records(D, P, j, x, y, z, g.x, g.y, fs_s[l], emit);
-}
-
-// A sample staged in registers for all its binned levels (loaded once, then walked level by level):
-// normalised position and dL/dy of levels first_binned .. first_binned + n_binned - 1 (the binned
-// levels are the last ones: every level after the dense prefix).
+// A sample staged in registers for all its binned levels: normalised position and dL/dy of the
+// binned levels (contiguous), loaded once before the level loop -- a load inside the loop would
+// wait behind the previous level's record stores (one in-order vmcnt), serialising the levels.
 constexpr int MAX_BINNED = 16;
+template <int MAXB>
 struct StagedSample {
     float x, y, z;
-    float g[2 * MAX_BINNED];
+    float g[2 * MAXB];
 };
 
+template <int MAXB>
 __device__ __forceinline__ void stage_sample(const mfnerf_grid_desc& D, const BinPlan& P, const float* __restrict__ X,
                                              float x_min, float x_range, const float* __restrict__ dy, int64_t i,
-                                             StagedSample& S) {
+                                             StagedSample<MAXB>& S) {
     S.x = (X[3 * i] - x_min) / x_range;
     S.y = (X[3 * i + 1] - x_min) / x_range;
     S.z = (X[3 * i + 2] - x_min) / x_range;
     const float2* src = reinterpret_cast<const float2*>(dy + i * (2 * D.n_levels) + 2 * P.level[0]);
 #pragma unroll
-    for (int j = 0; j < MAX_BINNED; ++j) {
+    for (int j = 0; j < MAXB; ++j) {
         const float2 v = j < P.n_binned ? src[j] : make_float2(0.f, 0.f);
         S.g[2 * j] = v.x;
         S.g[2 * j + 1] = v.y;
     }
 }
 
-template <typename EMIT>
-__device__ __forceinline__ void staged_records(const mfnerf_grid_desc& D, const BinPlan& P, const StagedSample& S,
-                                               const float* fs_s, int j, EMIT&& emit) {
+template <int MAXB, typename EMIT>
+__device__ __forceinline__ void staged_records(const mfnerf_grid_desc& D, const BinPlan& P,
+                                               const StagedSample<MAXB>& S, const float* fs_s, int j, EMIT&& emit) {
     float g0 = 0.f, g1 = 0.f;
 #pragma unroll
-    for (int k = 0; k < MAX_BINNED; ++k)  // register-indexed select (j is uniform)
+    for (int k = 0; k < MAXB; ++k)  // register-indexed select (j is uniform)
         if (k == j) { g0 = S.g[2 * k]; g1 = S.g[2 * k + 1]; }
     if (g0 == 0.0f && g1 == 0.0f) return;  // terminated samples: nothing to add
     level_records(D, P, j, S.x, S.y, S.z, g0, g1, fs_s[P.level[j]], emit);
@@ -797,6 +799,7 @@ __host__ __device__ __forceinline__ int64_t slot_size(int64_t nn, const BinPlan&
 // in tiles of up to 2048 samples: the tile's records are counted per bin of the level's table (LDS
 // atomics give each its rank), sorted by bin in LDS and stored as one contiguous run per bin in the
 // unit's slot of the bin (~30 records per run at the Lego config: whole-line stores).
+template <int MAXB>
 __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __restrict__ X, int64_t n,
                                                                  const int32_t* __restrict__ n_dev, float x_min,
                                                                  float x_range, const mfnerf_grid_desc D,
@@ -822,7 +825,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
     const int64_t m = n_chunks > u ? ((n_chunks - 1 - u) / UNITS + 1) * 16 : 0;  // this unit's sample slots
     const int spt = P.pair_ok ? 2 : 1;  // samples per thread per tile: <= 8 records each per level
     for (int64_t base = 0; base < m; base += (int64_t)spt * SC_THREADS) {
-        StagedSample S[2];
+        StagedSample<MAXB> S[2];
         bool live[2] = {false, false};
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -836,15 +839,15 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
             const int b0 = P.t_bin0[t], tb = P.t_bin0[t + 1] - b0;
             for (int k = threadIdx.x; k < tb; k += SC_THREADS) thist[k] = 0;
             __syncthreads();
-            int nr = 0, lr[8];  // (local bin, rank) packed: bin << 16 | rank
-            uint3 rr[8];
+            // the records are computed twice (ALU is cheap): once to count them per bin, once after
+            // the scan to place them, each at an LDS-atomic cursor of its bin -- the order inside a
+            // bin's run is arbitrary, which the accumulate's exact integer sum does not see.  No
+            // per-record state stays in registers between the passes.
 #pragma unroll
             for (int q = 0; q < 2; ++q)
                 if (live[q])
-                    staged_records(D, P, S[q], fs_s, j, [&](int bin, uint3 r) {
-                        const int lb = bin - b0;
-                        lr[nr] = (lb << 16) | atomicAdd(&thist[lb], 1);
-                        rr[nr++] = r;
+                    staged_records(D, P, S[q], fs_s, j, [&](int, int bin, uint3) {
+                        if (bin >= 0) atomicAdd(&thist[bin - b0], 1);
                     });
             __syncthreads();
             // bins -> sorted tile offsets (toff); a run's k-th record goes to its slot position gdst + k
@@ -854,20 +857,39 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                 const int c = cursor[b0 + threadIdx.x];
                 gdst[threadIdx.x] = c - toff[threadIdx.x];
                 cursor[b0 + threadIdx.x] = c + cnt;
+                thist[threadIdx.x] = toff[threadIdx.x];  // the placement cursors
             }
+            __syncthreads();
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
-                if (q < nr) {
-                    const int lb = lr[q] >> 16;
-                    const int p = toff[lb] + (lr[q] & 0xFFFF);
-                    stage[p] = rr[q];
-                    sbin[p] = (uint16_t)lb;
-                }
+            for (int q = 0; q < 2; ++q)
+                if (live[q])
+                    staged_records(D, P, S[q], fs_s, j, [&](int, int bin, uint3 r) {
+                        if (bin < 0) return;
+                        const int lb = bin - b0;
+                        const int p = atomicAdd(&thist[lb], 1);
+                        stage[p] = r;
+                        sbin[p] = (uint16_t)lb;
+                    });
             __syncthreads();
             for (int k = threadIdx.x; k < total; k += SC_THREADS) {
                 const int lb = sbin[k];
                 const int pos = gdst[lb] + k;  // position in the unit's slot of the bin
-                if (pos < slot) rec[((int64_t)(b0 + lb) * UNITS + u) * slot + pos] = stage[k];
+#ifndef MFN_REC_STORE
+#define MFN_REC_STORE 1  // 1: nontemporal record stores (streamed once, read once by the accumulate)
+#endif
+                if (pos < slot) {
+                    uint3* dst = rec + ((int64_t)(b0 + lb) * UNITS + u) * slot + pos;
+#if MFN_REC_STORE == 0
+                    *dst = stage[k];
+#elif MFN_REC_STORE == 1
+                    const uint3 r = stage[k];
+                    __builtin_nontemporal_store(r.x, &dst->x);
+                    __builtin_nontemporal_store(r.y, &dst->y);
+                    __builtin_nontemporal_store(r.z, &dst->z);
+#else
+                    if (stage[k].x == 0xFFFFFFFFu && stage[k].y == 0x7) *dst = stage[k];  // ablation: no stores
+#endif
+                }
             }
             __syncthreads();
         }
@@ -1323,7 +1345,10 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
     }
     if ((parts & 2) && P.n_bins > 0) {
         if (!((parts & 1) && l_first > 0)) (void)hipMemsetAsync(W.ovf, 0, sizeof(int32_t), stream);
-        hipLaunchKernelGGL(bin_scatter_kernel, dim3(UNITS), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
+        // the staged dL/dy rows sized for the binned levels (8 at the Lego layout; MixedFeature's
+        // shared tables bin more)
+        auto sk = P.n_binned <= 8 ? bin_scatter_kernel<8> : bin_scatter_kernel<MAX_BINNED>;
+        hipLaunchKernelGGL(sk, dim3(UNITS), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
                            *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.ovf, n_slots);
         hipLaunchKernelGGL(bin_accum_kernel, dim3(P.n_bins), dim3(ACC_THREADS), 0, stream, P, n, n_dev, W.rec,
                            W.scnt, W.ovf, (int*)grad_table, n_slots);

@@ -67,6 +67,13 @@ def main():
                                  c.rgb_width, ptr(t.dsig), ptr(t.drgb_s), step.grad_scale, ptr(t.dfeat),
                                  ptr(t.mlp_grad), ptr(t.mlp_grad[step.off_rgb:]), ptr(t.field_ws), None, None, s()),
         "grid_bw": lambda: step._grid_bw(mb, 0),
+        # the binned path's two halves: the coarse levels' atomics, the fine levels' partitions
+        "grid_bw_coarse": lambda: call("mfnerf_grid_encode_bw_binned", ptr(m.xyzs), cap, ptr(m.counter), step.x_min,
+                                       step.x_range, step.desc, ptr(t.dfeat), ptr(step.grads[step.off_table:]),
+                                       ptr(t.grid_ws), step._bin_slots(), ptr(step._level_l1), 1, s()),
+        "grid_bw_binned": lambda: call("mfnerf_grid_encode_bw_binned", ptr(m.xyzs), cap, ptr(m.counter), step.x_min,
+                                       step.x_range, step.desc, ptr(t.dfeat), ptr(step.grads[step.off_table:]),
+                                       ptr(t.grid_ws), step._bin_slots(), ptr(step._level_l1), 2, s()),
         "grid_finish": lambda: step._grid_finish(0),
         "grid_bw_half": lambda: call("mfnerf_debug_grid_bw_half", ptr(m.xyzs), cap, ptr(m.counter), step.x_min,
                                      step.x_range, step.desc, ptr(t.dfeat), ptr(grad_h2), ptr(priv_h2), 2048.0, s()),
