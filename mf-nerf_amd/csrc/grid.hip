@@ -213,7 +213,10 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_fw_planar_kernel(const float* 
 //     merges such runs and only run heads issue the atomic;
 //   * the dense coarse levels (a few hundred to a few thousand hot lines) add into GRAD_COPIES
 //     private copies, picked per wave, folded back by fold_copies_kernel.
-constexpr int GRAD_COPIES = 8;
+#ifndef MFN_GRAD_COPIES
+#define MFN_GRAD_COPIES 8
+#endif
+constexpr int GRAD_COPIES = MFN_GRAD_COPIES;  // power of two
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
@@ -330,7 +333,14 @@ __device__ __forceinline__ void grid_bw_body(int bid, int nblk, const float* __r
                 { const float vp = dpp_f<DPP_ROW_SHL(2)>(v); const int sp = dpp_i<DPP_ROW_SHL(2)>(stop); if (!stop) { v += vp; stop = sp; } }
                 { const float vp = dpp_f<DPP_ROW_SHL(4)>(v); const int sp = dpp_i<DPP_ROW_SHL(4)>(stop); if (!stop) { v += vp; stop = sp; } }
                 { const float vp = dpp_f<DPP_ROW_SHL(8)>(v); const int sp = dpp_i<DPP_ROW_SHL(8)>(stop); if (!stop) { v += vp; stop = sp; } }
-                if (FIX) {
+                if (FIX && spread) {  // private copies: both features as one packed 64-bit add
+                    const int q = (int)rintf(v * fs);
+                    const int q1 = __shfl_down(q, 16, 64);  // the f = 1 lane of this (sample, corner)
+                    const long long pq = (long long)((uint64_t)(uint32_t)q1 << 32) + (long long)q;
+                    if (f == 0 && head && valid && pq != 0)
+                        __hip_atomic_fetch_add(reinterpret_cast<long long*>(gt) + idx, pq, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                } else if (FIX) {
                     const int q = (int)rintf(v * fs);
                     if (head && valid && q != 0)
                         __hip_atomic_fetch_add(reinterpret_cast<int*>(gt) + 2 * idx + f, q, __ATOMIC_RELAXED,
@@ -357,6 +367,226 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restr
     if (zero_flag && blockIdx.x == 0 && threadIdx.x == 0) *zero_flag = 0;
     grid_bw_body<ABLATE, MAXL, FIX>(blockIdx.x, gridDim.x, X, n, n_dev, x_min, x_range, D, dy, grad, priv,
                                     dense_entries, level_l1, l_end);
+}
+
+// Dense own-table levels [0, l_hi) into the private copies, one SAMPLE per lane.  The kernels above
+// give each sample 4 lanes (x-corner x feature) and issue VALU work per lane: they are VALU-bound
+// (PMC: ~58 VALU wave-instructions per 16-sample row step, the same time with the atomics
+// compiled out).  Here a lane holds its sample's whole (y,z) row -- x-pair x 2 features -- so the
+// geometry is computed once per sample and one segmented scan step serves 64 samples:
+//   * the window = DENSE_CPW chunks of 64 consecutive samples; per level and (y,z) row, runs of
+//     equal row keys are merged by a segmented prefix scan over the wave (DPP row_shr 1/2/4/8, then
+//     row_bcast:15 / :31 for the rows' open runs); lane 63's run stays open into the next chunk;
+//   * closed runs (tails; a carried run that the next chunk does not continue) are compacted into
+//     an LDS list and issued two lanes per run, one 64-bit atomic per x-corner carrying BOTH
+//     features as one packed integer hi * 2^32 + lo -- integer addition is exact, so the packed sum
+//     is (sum hi) * 2^32 + (sum lo) and the fold decodes lo = int32(low word), hi = int32(high
+//     word) + (lo < 0) (|sum| < 2^31 by the scale bound): 32 runs per instruction, one 16-B span
+//     (one request) per run.
+// Requires every level < l_hi to be a dense own table inside the private copies.
+#ifndef MFN_DENSE_ABLATE
+#define MFN_DENSE_ABLATE 0
+#endif
+constexpr int DENSE_CPW = 2;
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dppz_f(float v) {  // lanes without a source (or outside ROW_MASK) read 0
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
+}
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ int dppo_i(int v) {  // ... read 1 (a run flag: "still open")
+    return __builtin_amdgcn_update_dpp(1, v, CTRL, ROW_MASK, 0xF, false);
+}
+
+__global__ __launch_bounds__(ENC_BLOCK) void grid_bw_dense_kernel(const float* __restrict__ X, int64_t n,
+                                                                  const int32_t* __restrict__ n_dev, float x_min,
+                                                                  float x_range, const mfnerf_grid_desc D,
+                                                                  const float* __restrict__ dy,
+                                                                  float* __restrict__ priv, int64_t dense_entries,
+                                                                  const float* __restrict__ level_l1, int l_hi,
+                                                                  int32_t* __restrict__ zero_flag) {
+    if (zero_flag && blockIdx.x == 0 && threadIdx.x == 0) *zero_flag = 0;
+    constexpr int WS = DENSE_CPW * 64;
+    extern __shared__ float sdy_dyn[];  // per wave: WS rows of 2 l_hi + 1 floats, then the run list
+    __shared__ float fs_s[MFN_MAX_LEVELS];
+    __shared__ int lkey[ENC_BLOCK / 64][66][2];
+    __shared__ long long lval[ENC_BLOCK / 64][66][2];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if ((int)threadIdx.x < D.n_levels) fs_s[threadIdx.x] = table_fixed_scale(D, level_l1, threadIdx.x);
+    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
+    const int64_t n_waves = ((int64_t)gridDim.x * ENC_BLOCK) >> 6;
+    const int cols = 2 * l_hi, rs = 2 * l_hi + 1, row = 2 * D.n_levels;
+    float* sdy = sdy_dyn + wv * (WS * rs);
+    int(*lk)[2] = lkey[wv];
+    long long(*lv)[2] = lval[wv];
+    __syncthreads();  // fs_s
+    for (int64_t wave = ((int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x) >> 6; wave * WS < nn; wave += n_waves) {
+        const int64_t i0 = wave * WS;
+        __builtin_amdgcn_wave_barrier();
+        float px[DENSE_CPW], py[DENSE_CPW], pz[DENSE_CPW];
+#pragma unroll
+        for (int k = 0; k < DENSE_CPW; ++k) {  // lane stages sample i0 + 64 k + lane: loads first
+            const int64_t i = i0 + 64 * k + lane;
+            const bool ok = i < nn;
+            const float4* src = reinterpret_cast<const float4*>(dy + (ok ? i : 0) * row);
+            float4 t[MFN_MAX_LEVELS / 2];
+            const int ng = (cols + 3) >> 2;
+#pragma unroll
+            for (int j = 0; j < MFN_MAX_LEVELS / 2; ++j)
+                t[j] = (ok && j < ng) ? src[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+            px[k] = ok ? (X[3 * i] - x_min) / x_range : 0.0f;
+            py[k] = ok ? (X[3 * i + 1] - x_min) / x_range : 0.0f;
+            pz[k] = ok ? (X[3 * i + 2] - x_min) / x_range : 0.0f;
+            float* dst = sdy + (64 * k + lane) * rs;
+#pragma unroll
+            for (int j = 0; j < MFN_MAX_LEVELS / 2; ++j) {
+                if (4 * j < cols) dst[4 * j] = t[j].x;
+                if (4 * j + 1 < cols) dst[4 * j + 1] = t[j].y;
+                if (4 * j + 2 < cols) dst[4 * j + 2] = t[j].z;
+                if (4 * j + 3 < cols) dst[4 * j + 3] = t[j].w;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (int l = 0; l < l_hi; ++l) {
+            const float fs = fs_s[l];
+            long long* gt = reinterpret_cast<long long*>(priv) +
+                            ((wave & (GRAD_COPIES - 1)) * dense_entries + (int64_t)D.offset[l]);
+            int ckey[4], ckey1[4];
+            float cv[4][4];
+#pragma unroll
+            for (int yz = 0; yz < 4; ++yz) {
+                ckey[yz] = -1;
+                ckey1[yz] = -1;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) cv[yz][c] = 0.0f;
+            }
+#pragma unroll
+            for (int k = 0; k < DENSE_CPW; ++k) {
+                const bool valid = i0 + 64 * k + lane < nn;
+                const float g0 = sdy[(64 * k + lane) * rs + 2 * l], g1 = sdy[(64 * k + lane) * rs + 2 * l + 1];
+                const LevelGeo Lg = level_geo(D.scale[l], px[k], py[k], pz[k]);
+                int key[4], key1[4], open[4];
+                float v[4][4];
+                bool tail[4];
+                // dense index x + y res + z res^2 with corner_index's `% size`: the corners of points
+                // in [0,1]^3 stay below 2 size, where one conditional subtraction is that modulo
+                // (a full integer modulo per corner dominated this kernel's VALU count)
+                const uint32_t res = D.res[l], size = D.size[l];
+                bool far = false;
+#pragma unroll
+                for (int yz = 0; yz < 4; ++yz) {
+                    const uint32_t gy = Lg.g[1] + (yz & 1), gz = Lg.g[2] + (yz >> 1);
+                    const uint32_t k0 = Lg.g[0] + (gy + gz * res) * res, k1 = k0 + 1;
+                    far |= valid && (k1 >= 2 * size || k1 < k0);
+                    key[yz] = valid ? (int)(k0 >= size ? k0 - size : k0) : -1;
+                    key1[yz] = (int)(k1 >= size ? k1 - size : k1);
+                }
+                if (__builtin_expect(__ballot(far) != 0, 0)) {  // points far outside the unit cube
+#pragma unroll
+                    for (int yz = 0; yz < 4; ++yz) {
+                        const uint32_t gy = Lg.g[1] + (yz & 1), gz = Lg.g[2] + (yz >> 1);
+                        key[yz] = valid ? (int)corner_index(D, l, Lg.g[0], gy, gz) : -1;
+                        key1[yz] = (int)corner_index(D, l, Lg.g[0] + 1, gy, gz);
+                    }
+                }
+#pragma unroll
+                for (int yz = 0; yz < 4; ++yz) {
+                    const float wy = (yz & 1) ? Lg.w[1] : 1.0f - Lg.w[1];
+                    const float wz = (yz >> 1) ? Lg.w[2] : 1.0f - Lg.w[2];
+                    const float wyz = wy * wz, w1 = Lg.w[0], w0 = 1.0f - Lg.w[0];
+                    v[yz][0] = valid ? w0 * wyz * g0 : 0.0f;
+                    v[yz][1] = valid ? w0 * wyz * g1 : 0.0f;
+                    v[yz][2] = valid ? w1 * wyz * g0 : 0.0f;
+                    v[yz][3] = valid ? w1 * wyz * g1 : 0.0f;
+                    const bool cont = lane == 0 && ckey[yz] >= 0 && ckey[yz] == key[yz];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) v[yz][c] += cont ? cv[yz][c] : 0.0f;
+                    const int kp = __builtin_amdgcn_update_dpp(-2, key[yz], 0x138, 0xF, 0xF, false);  // wave_shr:1
+                    const int kn = __builtin_amdgcn_update_dpp(-2, key[yz], 0x130, 0xF, 0xF, false);  // wave_shl:1
+                    tail[yz] = lane == 63 || kn != key[yz];
+                    open[yz] = !(lane == 0 || kp != key[yz]);  // the run started in an earlier lane
+                }
+                // segmented inclusive prefix scan: run tails end with the run total
+#define MFN_SEG(CTRL, RM)                                                                          \
+    _Pragma("unroll") for (int yz = 0; yz < 4; ++yz) {                                             \
+        const int op = dppo_i<CTRL, RM>(open[yz]);                                                 \
+        _Pragma("unroll") for (int c = 0; c < 4; ++c) {                                            \
+            const float vp = dppz_f<CTRL, RM>(v[yz][c]);                                           \
+            v[yz][c] += open[yz] ? vp : 0.0f;                                                      \
+        }                                                                                          \
+        open[yz] = open[yz] ? op : 0;                                                              \
+    }
+                MFN_SEG(0x111, 0xF) MFN_SEG(0x112, 0xF) MFN_SEG(0x114, 0xF) MFN_SEG(0x118, 0xF)
+                MFN_SEG(0x142, 0xA) MFN_SEG(0x143, 0xC)
+#undef MFN_SEG
+                // closed runs -> the wave's LDS list (at most 64 tails + lane 0's flushed carry)
+#pragma unroll
+                for (int yz = 0; yz < 4; ++yz) {
+                    const bool emit = tail[yz] && lane != 63 && key[yz] >= 0;
+                    const bool flush = lane == 0 && ckey[yz] >= 0 && ckey[yz] != key[yz];
+                    const uint64_t be = __ballot(emit);
+                    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(be >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)be, 0u));
+                    const int ne = __popcll(be);
+                    auto pack = [&](float a, float b) -> long long {
+                        const int qa = (int)rintf(a * fs), qb = (int)rintf(b * fs);
+                        return (long long)((uint64_t)(uint32_t)qb << 32) + (long long)qa;
+                    };
+                    if (emit) {
+                        lk[rank][0] = key[yz];
+                        lk[rank][1] = key1[yz];
+                        lv[rank][0] = pack(v[yz][0], v[yz][1]);
+                        lv[rank][1] = pack(v[yz][2], v[yz][3]);
+                    }
+                    if (flush) {
+                        lk[ne][0] = ckey[yz];
+                        lk[ne][1] = ckey1[yz];
+                        lv[ne][0] = pack(cv[yz][0], cv[yz][1]);
+                        lv[ne][1] = pack(cv[yz][2], cv[yz][3]);
+                    }
+#if MFN_DENSE_ABLATE == 2  // experiment: no list, no atomics
+                    const int nl = 0;
+#else
+                    const int nl = ne + (__ballot(flush) ? 1 : 0);
+#endif
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    for (int b = 0; b < nl; b += 32) {  // two lanes (x-corners) per run
+                        const int j = b + (lane >> 1), c = lane & 1;
+                        if (j < nl) {
+                            const long long q = lv[j][c];
+#if MFN_DENSE_ABLATE == 1  // experiment: list built and read, no atomics
+                            if (q == 0x7fffffffffffll)
+#else
+                            if (q != 0)
+#endif
+                                __hip_atomic_fetch_add(gt + lk[j][c], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    // lane 63's run stays open
+                    ckey[yz] = __builtin_amdgcn_readlane(key[yz], 63);
+                    ckey1[yz] = __builtin_amdgcn_readlane(key1[yz], 63);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        cv[yz][c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[yz][c]), 63));
+                }
+            }
+            // the window's last open runs
+#pragma unroll
+            for (int yz = 0; yz < 4; ++yz) {
+                if (lane < 2 && ckey[yz] >= 0) {
+                    const float a = lane ? cv[yz][2] : cv[yz][0], b = lane ? cv[yz][3] : cv[yz][1];
+                    const int qa = (int)rintf(a * fs), qb = (int)rintf(b * fs);
+                    const long long q = (long long)((uint64_t)(uint32_t)qb << 32) + (long long)qa;
+                    if (q != 0)
+                        __hip_atomic_fetch_add(gt + (lane ? ckey1[yz] : ckey[yz]), q, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+    }
 }
 
 // fp16 variant (experiment / tcnn's grad_t = __half for F = 2): one lane adds BOTH features of a
@@ -484,6 +714,24 @@ __global__ __launch_bounds__(256) void fold_copies_kernel(float* __restrict__ pr
 
 // Fixed-point path: grad[p] (float) = sum_k priv[k][p] / scale for the dense prefix (copies zeroed),
 // grad[p] = int(grad[p]) / scale for the rest; scale per level from the same level_l1 as grid_bw.
+// The private copies of the fixed-point path hold each entry's two features as ONE packed integer
+// f1 * 2^32 + f0 (64-bit atomics carry both; grid_bw_dense_kernel, grid_bw_body): the sum of the
+// copies is exact in int64, and f0 = int32(low word), f1 = int32(high word) + (f0 < 0) undoes the
+// borrow of a negative f0.  Values i .. i+3 (entries i/2, i/2+1); the copies are zeroed.
+__device__ __forceinline__ int4 fold_packed_copies(int* __restrict__ priv, int64_t dense_vals, int64_t i) {
+    long long a = 0, b = 0;
+#pragma unroll
+    for (int k = 0; k < GRAD_COPIES; ++k) {
+        longlong2* q = reinterpret_cast<longlong2*>(priv + k * dense_vals + i);
+        const longlong2 c = *q;
+        a += c.x;
+        b += c.y;
+        *q = make_longlong2(0, 0);
+    }
+    const int a0 = (int)(uint32_t)(unsigned long long)a, b0 = (int)(uint32_t)(unsigned long long)b;
+    return make_int4(a0, (int)(a >> 32) + (a0 < 0), b0, (int)(b >> 32) + (b0 < 0));
+}
+
 __global__ __launch_bounds__(256) void fold_convert_kernel(float* __restrict__ grad, int* __restrict__ priv,
                                                            int64_t dense_vals, int64_t total_vals,
                                                            const mfnerf_grid_desc D,
@@ -503,14 +751,7 @@ __global__ __launch_bounds__(256) void fold_convert_kernel(float* __restrict__ g
         const float is = inv_s[l];
         int4 acc;
         if (i < dense_vals) {
-            acc = make_int4(0, 0, 0, 0);
-#pragma unroll
-            for (int k = 0; k < GRAD_COPIES; ++k) {
-                int4* q = reinterpret_cast<int4*>(priv + k * dense_vals + i);
-                const int4 v = *q;
-                acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-                *q = make_int4(0, 0, 0, 0);
-            }
+            acc = fold_packed_copies(priv, dense_vals, i);
             // the dense prefix's own entries in grad received no contributions (all went to copies)
         } else {
             acc = *reinterpret_cast<const int4*>(grad + i);
@@ -553,14 +794,7 @@ __global__ __launch_bounds__(256) void adam_fixed_kernel(float* __restrict__ p, 
             const float is = R.inv_s[l];
             int4 acc;
             if (j < dense_vals) {
-                acc = make_int4(0, 0, 0, 0);
-#pragma unroll
-                for (int k = 0; k < GRAD_COPIES; ++k) {
-                    int4* q = reinterpret_cast<int4*>(priv + k * dense_vals + j);
-                    const int4 c = *q;
-                    acc.x += c.x; acc.y += c.y; acc.z += c.z; acc.w += c.w;
-                    *q = make_int4(0, 0, 0, 0);
-                }
+                acc = fold_packed_copies(priv, dense_vals, j);
             } else {
                 acc = reinterpret_cast<const int4*>(g)[i4];
             }
@@ -645,6 +879,9 @@ int check_desc(const mfnerf_grid_desc* d, const char* what) {
 // blocks) -> scatter (records) -> accumulate.
 // partitions of 2^shift entries, shift in [MIN_BIN_SHIFT, MAX_BIN_SHIFT] chosen per layout so that
 // there are >= ~1024 partitions (4 workgroups per CU); 2^11 entries = 32 KB of int64 pairs
+#ifndef MFN_ACC32
+#define MFN_ACC32 0  // int64 LDS image at 2^32 x the scale, rounded once per entry (0), or int32 (1)
+#endif
 constexpr int MIN_BIN_SHIFT = 8, MAX_BIN_SHIFT = 11, MAX_BIN_ENTRIES = 1 << MAX_BIN_SHIFT;
 constexpr int MAX_BINS = 4096;
 
@@ -677,16 +914,19 @@ __device__ __forceinline__ int bin_table(const BinPlan& P, int b) {
 // two share a bin unless the carry reaches bit `shift` (1 x in 2^shift).  Otherwise (shared
 // MixedFeature tables, straddles) each entry gets a single record with weight sel ? fx : 1-fx.
 template <typename EMIT>
-__device__ __forceinline__ void level_records(const mfnerf_grid_desc& D, const BinPlan& P, int j, float x, float y,
-                                              float z, float g0, float g1, float fs, EMIT&& emit) {
+__device__ __forceinline__ void level_records_geo(const mfnerf_grid_desc& D, const BinPlan& P, int j,
+                                                  const LevelGeo& Lg, float g0, float g1, float fs, EMIT&& emit) {
     const int l = P.level[j];
     const int t = P.table_of[l];
     const int bin0 = P.t_bin0[t];
-    const LevelGeo Lg = level_geo(D.scale[l], x, y, z);
     const uint32_t fxq = min(32767u, (uint32_t)rintf(Lg.w[0] * 32768.0f)) << 17;
     const uint32_t ones = (uint32_t)__builtin_ctz(~Lg.g[0]);  // trailing ones of x
     const bool pair_hash = P.pairable[l] && ones < 15;
+#if MFN_ACC32
+    const float s0 = g0 * fs, s1 = g1 * fs;  // in the table's int32 fixed-point units
+#else
     const float s0 = g0 * fs * 4294967296.0f, s1 = g1 * fs * 4294967296.0f;  // exact: powers of two
+#endif
     const uint32_t mask = (1u << P.shift) - 1;
 #pragma unroll
     for (int yz = 0; yz < 4; ++yz) {
@@ -704,6 +944,12 @@ __device__ __forceinline__ void level_records(const mfnerf_grid_desc& D, const B
         emit(2 * yz, b0, make_uint3((i0 & mask) | (pair ? (ones << 11) : (1u << 15)) | fxq, a, b));
         emit(2 * yz + 1, pair ? -1 : b1, make_uint3((i1 & mask) | (1u << 15) | (1u << 16) | fxq, a, b));
     }
+}
+
+template <typename EMIT>
+__device__ __forceinline__ void level_records(const mfnerf_grid_desc& D, const BinPlan& P, int j, float x, float y,
+                                              float z, float g0, float g1, float fs, EMIT&& emit) {
+    level_records_geo(D, P, j, level_geo(D.scale[P.level[j]], x, y, z), g0, g1, fs, emit);
 }
 
 
@@ -733,15 +979,32 @@ __device__ __forceinline__ void stage_sample(const mfnerf_grid_desc& D, const Bi
     }
 }
 
-template <int MAXB, typename EMIT>
-__device__ __forceinline__ void staged_records(const mfnerf_grid_desc& D, const BinPlan& P,
-                                               const StagedSample<MAXB>& S, const float* fs_s, int j, EMIT&& emit) {
+// one sample's dL/dy pair at binned level j, selected once for both record passes (count, place)
+struct SampleLevel {
+    float g0, g1;
+    bool live;
+};
+
+template <int MAXB>
+__device__ __forceinline__ SampleLevel sample_level(const mfnerf_grid_desc& D, const BinPlan& P,
+                                                    const StagedSample<MAXB>& S, int j) {
     float g0 = 0.f, g1 = 0.f;
 #pragma unroll
-    for (int k = 0; k < MAXB; ++k)  // register-indexed select (j is uniform)
+    for (int k = 0; k < MAXB; ++k)  // register-indexed select (j is uniform: scalar compares)
         if (k == j) { g0 = S.g[2 * k]; g1 = S.g[2 * k + 1]; }
-    if (g0 == 0.0f && g1 == 0.0f) return;  // terminated samples: nothing to add
-    level_records(D, P, j, S.x, S.y, S.z, g0, g1, fs_s[P.level[j]], emit);
+    SampleLevel r;
+    r.g0 = g0;
+    r.g1 = g1;
+    r.live = !(r.g0 == 0.0f && r.g1 == 0.0f);  // terminated samples: nothing to add
+    return r;
+}
+
+template <int MAXB, typename EMIT>
+__device__ __forceinline__ void staged_records(const mfnerf_grid_desc& D, const BinPlan& P,
+                                               const StagedSample<MAXB>& S, const SampleLevel& Q, const float* fs_s,
+                                               int j, EMIT&& emit) {
+    if (!Q.live) return;
+    level_records(D, P, j, S.x, S.y, S.z, Q.g0, Q.g1, fs_s[P.level[j]], emit);
 }
 
 __device__ __forceinline__ void load_fixed_scales(const mfnerf_grid_desc& D, const float* __restrict__ level_l1,
@@ -838,6 +1101,9 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
             const int t = P.table_of[P.level[j]];
             const int b0 = P.t_bin0[t], tb = P.t_bin0[t + 1] - b0;
             for (int k = threadIdx.x; k < tb; k += SC_THREADS) thist[k] = 0;
+            SampleLevel Q[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) Q[q] = sample_level(D, P, S[q], j);
             __syncthreads();
             // the records are computed twice (ALU is cheap): once to count them per bin, once after
             // the scan to place them, each at an LDS-atomic cursor of its bin -- the order inside a
@@ -846,7 +1112,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
 #pragma unroll
             for (int q = 0; q < 2; ++q)
                 if (live[q])
-                    staged_records(D, P, S[q], fs_s, j, [&](int, int bin, uint3) {
+                    staged_records(D, P, S[q], Q[q], fs_s, j, [&](int, int bin, uint3) {
                         if (bin >= 0) atomicAdd(&thist[bin - b0], 1);
                     });
             __syncthreads();
@@ -863,7 +1129,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
 #pragma unroll
             for (int q = 0; q < 2; ++q)
                 if (live[q])
-                    staged_records(D, P, S[q], fs_s, j, [&](int, int bin, uint3 r) {
+                    staged_records(D, P, S[q], Q[q], fs_s, j, [&](int, int bin, uint3 r) {
                         if (bin < 0) return;
                         const int lb = bin - b0;
                         const int p = atomicAdd(&thist[lb], 1);
@@ -907,15 +1173,43 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
 // entries (int64 pairs, ds_add_u64) and stores it rounded to int32.
 __device__ __forceinline__ int round_shift32(long long v) { return (int)((v + 0x80000000ll) >> 32); }
 
-// float -> int64 for |v| < 2^62: below 2^31 round to nearest; above, v is an integer: its 24-bit
-// mantissa shifted into place (cheaper than the library's float -> long long)
+// float -> int64 rounded to nearest (ties to even), |v| < 2^62: below 2^31 one rint; above,
+// v = hi * 2^32 + d with hi = floor(v / 2^32), d in [0, 2^32) -- d is v's mantissa bits below 2^32
+// (ulp(v) >= 2^8 there), so the fma computing it is exact -- then d as u32.  Branch-free.
 __device__ __forceinline__ long long f2ll(float v) {
-    int e;
-    const float m = frexpf(v, &e);  // v = m * 2^e, 0.5 <= |m| < 1
-    if (e <= 30) return (long long)(int)rintf(v);
-    return (long long)(int)(m * 1073741824.0f) * (1ll << (e - 30));
+    const float hi = floorf(v * 2.3283064365386963e-10f);  // v / 2^32 (exact scaling)
+    const float d = fmaf(hi, -4294967296.0f, v);          // exact for |v| >= 2^31 (ulp(v) >= 2^8)
+    const long long big = (long long)((uint64_t)(uint32_t)(int)hi << 32) + (long long)(uint32_t)rintf(d);
+    return fabsf(v) < 2147483648.0f ? (long long)(int)rintf(v) : big;
 }
 
+#if MFN_ACC32
+// int32 image in the table's fixed-point units: each weighted contribution rounded once (as
+// grid_bw_body rounds each run-merged one), the sums exact and order-free.  One cvt per value
+// instead of the int64 path's float -> int64 conversion: the accumulate is VALU-bound.
+using acc_t = int;
+__device__ __forceinline__ void accum_record(int* img, int mask, uint3 r) {
+    const uint32_t w = r.x;
+    const float a = __uint_as_float(r.y), b = __uint_as_float(r.z);
+    if (a == 0.0f && b == 0.0f) return;
+    const float fx = (float)(w >> 17) * (1.0f / 32768.0f);
+    const int e0 = w & mask;
+    if (w & (1u << 15)) {  // single entry, weight sel ? fx : 1 - fx
+        const float wt = (w & (1u << 16)) ? fx : 1.0f - fx;
+        atomicAdd(&img[2 * e0], (int)rintf(wt * a));
+        atomicAdd(&img[2 * e0 + 1], (int)rintf(wt * b));
+    } else {
+        const int e1 = e0 ^ ((2 << ((w >> 11) & 15)) - 1);
+        const float w0 = 1.0f - fx;
+        atomicAdd(&img[2 * e0], (int)rintf(w0 * a));
+        atomicAdd(&img[2 * e0 + 1], (int)rintf(w0 * b));
+        atomicAdd(&img[2 * e1], (int)rintf(fx * a));
+        atomicAdd(&img[2 * e1 + 1], (int)rintf(fx * b));
+    }
+}
+__device__ __forceinline__ int acc_out(int v) { return v; }
+#else
+using acc_t = unsigned long long;
 __device__ __forceinline__ void accum_record(unsigned long long* img, int mask, uint3 r) {
     const uint32_t w = r.x;
     const float a = __uint_as_float(r.y), b = __uint_as_float(r.z);
@@ -937,6 +1231,9 @@ __device__ __forceinline__ void accum_record(unsigned long long* img, int mask, 
     }
 }
 
+__device__ __forceinline__ int acc_out(unsigned long long v) { return round_shift32((long long)v); }
+#endif
+
 constexpr int ACC_THREADS = 512;
 
 __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, int64_t n,
@@ -946,7 +1243,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
                                                                 const int32_t* __restrict__ ovf,
                                                                 int* __restrict__ grad, int64_t n_slots) {
     if (*ovf) return;  // a slot overflowed: bin_fallback_kernel scatters the binned levels
-    __shared__ unsigned long long img[2 * MAX_BIN_ENTRIES];
+    __shared__ acc_t img[2 * MAX_BIN_ENTRIES];
     const int bin = blockIdx.x;
     const int n_ent = 1 << P.shift, mask = n_ent - 1;
     for (int i = threadIdx.x; i < 2 * n_ent; i += blockDim.x) img[i] = 0;
@@ -979,7 +1276,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     const int64_t e_lo = (int64_t)(bin - P.t_bin0[t]) << P.shift;
     const int n_e = (int)min<int64_t>(n_ent, (int64_t)P.t_size[t] - e_lo);
     int* dst = grad + 2 * ((int64_t)P.t_offset[t] + e_lo);
-    for (int i = threadIdx.x; i < 2 * n_e; i += blockDim.x) dst[i] = round_shift32((long long)img[i]);
+    for (int i = threadIdx.x; i < 2 * n_e; i += blockDim.x) dst[i] = acc_out(img[i]);
 }
 
 // the binned levels by request-shaped int32 atomics (grid_bw_body), only if a slot overflowed (a
@@ -1046,13 +1343,12 @@ int bin_plan(const mfnerf_grid_desc* d, BinPlan* P) {
     return nb > MAX_BINS ? -1 : nb;
 }
 
-// first level routed through the bins (the dense levels before it use grid_bw_kernel)
-// The partitioned levels: the last MFNERF_BIN_LEVELS (default 6) hashed ones -- the fine levels,
-// whose rows no run merging collapses; the coarser hashed levels repeat rows along a ray and stay
-// on the run-merging atomics -- extended down to every level that shares a table with them
-// (MixedFeature), since a partition is stored whole.
+// first level routed through the bins (the dense levels before it use grid_bw_dense_kernel)
+// The partitioned levels: by default every hashed level (MFNERF_BIN_LEVELS=k: only the last k
+// hashed ones, the coarser hashed levels then staying on run-merging atomics) -- extended down to
+// every level that shares a table with them (MixedFeature), since a partition is stored whole.
 int first_binned_level(const mfnerf_grid_desc* d) {
-    static const int knob = [] { const char* e = getenv("MFNERF_BIN_LEVELS"); return e ? atoi(e) : 6; }();
+    static const int knob = [] { const char* e = getenv("MFNERF_BIN_LEVELS"); return e ? atoi(e) : MFN_MAX_LEVELS; }();
     int first_hashed = d->n_levels;
     for (int l = 0; l < d->n_levels; ++l) {
         const uint64_t r = d->res[l];
@@ -1337,7 +1633,22 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
     const int64_t cap = grid_bw_block_cap();
     const int64_t atomic_blocks = want < cap ? want : cap;
     const bool big = desc->n_levels > 16;
-    if ((parts & 1) && l_first > 0) {  // dense levels [0, l_first): request-shaped atomics, private copies
+    static const int dense_mode = [] { const char* e = getenv("MFNERF_DENSE_SCATTER"); return e ? atoi(e) : 1; }();
+    int n_dense_levels = 0;  // leading levels that are dense own tables inside the private copies
+    {
+        const int64_t de = dense_entries_of(desc);
+        while (n_dense_levels < desc->n_levels && desc->table_kind[n_dense_levels] == 0 &&
+               (int64_t)desc->offset[n_dense_levels] + desc->size[n_dense_levels] <= de)
+            ++n_dense_levels;
+    }
+    if ((parts & 1) && l_first > 0 && dense_mode && l_first <= n_dense_levels) {
+        // levels [0, l_first) all dense: one sample per lane, packed 64-bit adds into the copies
+        const int64_t wb = div_up<int64_t>(n, (int64_t)DENSE_CPW * 64 * (ENC_BLOCK / 64));
+        const size_t lds = (size_t)(ENC_BLOCK / 64) * DENSE_CPW * 64 * (2 * l_first + 1) * sizeof(float);
+        hipLaunchKernelGGL(grid_bw_dense_kernel, dim3((unsigned)(wb < cap ? wb : cap)), dim3(ENC_BLOCK), lds, stream,
+                           x, n, n_dev, x_min, x_range, *desc, dL_dout, W.priv, dense_entries_of(desc), level_l1,
+                           l_first, (parts & 2) ? W.ovf : (int32_t*)nullptr);
+    } else if ((parts & 1) && l_first > 0) {  // dense levels [0, l_first): request-shaped atomics, private copies
         auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, true> : grid_bw_kernel<0, 16, true>;
         hipLaunchKernelGGL(kern, dim3((unsigned)atomic_blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min,
                            x_range, *desc, dL_dout, grad_table, W.priv, dense_entries_of(desc), level_l1, l_first,

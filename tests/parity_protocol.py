@@ -41,11 +41,11 @@ def density_grid():
     return synthetic.ball_density_grid()
 
 
-def batch(train, step):
-    """(rays_o, rays_d, rgb) of step `step`: a random pixel of a random training view per ray
-    (datasets/base.py:22-35 'all_images'), rays as ray_utils.get_rays builds them."""
+def batch(train, step, seed=0):
+    """(rays_o, rays_d, rgb) of step `step` of run `seed`: a random pixel of a random training view
+    per ray (datasets/base.py:22-35 'all_images'), rays as ray_utils.get_rays builds them."""
     imgs, poses, dirs, _ = train
-    g = torch.Generator().manual_seed(10000 + step)
+    g = torch.Generator().manual_seed(10000 + step + 1000003 * seed)
     img = torch.randint(imgs.shape[0], (N_RAYS,), generator=g)
     pix = torch.randint(imgs.shape[1], (N_RAYS,), generator=g)
     c2w = poses[img]
@@ -54,9 +54,9 @@ def batch(train, step):
     return rays_o, rays_d, imgs[img, pix].contiguous()
 
 
-def noise(step):
-    """The march perturbation of step `step` (custom_functions.py:83, torch.rand_like)."""
-    return torch.rand(N_RAYS, generator=torch.Generator().manual_seed(20000 + step))
+def noise(step, seed=0):
+    """The march perturbation of step `step` of run `seed` (custom_functions.py:83, torch.rand_like)."""
+    return torch.rand(N_RAYS, generator=torch.Generator().manual_seed(20000 + step + 1000003 * seed))
 
 
 def init_params(cfg):

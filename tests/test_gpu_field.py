@@ -144,6 +144,44 @@ def test_grid_encode_bw_along_rays(gpu):
                 assert err < 1e-4, (binned, l, err)
 
 
+@pytest.mark.parametrize("name,args", [_layouts()[0], _layouts()[2]])
+def test_grid_encode_bw_ragged_rays(gpu, name, args):
+    """Rays of 1..300 samples packed back to back (a live count that is not a multiple of 16 or
+    64): coarse-level runs cross the 16-sample chunks and the 64-sample windows of the coarse
+    scatter, whose open runs are carried across chunk boundaries -- vs the fp64 oracle, per level,
+    bit-reproducible."""
+    lay, olay = GridLayout(*args), FO.GridLayout(*args)
+    g = torch.Generator().manual_seed(33)
+    lens = torch.randint(1, 301, (90,), generator=g)
+    lens[:6] = torch.tensor([1, 15, 16, 17, 63, 65])
+    xs = []
+    for S in lens.tolist():
+        o = torch.rand(1, 3, generator=g) * 0.6 + 0.2
+        d = torch.nn.functional.normalize(torch.randn(1, 3, generator=g), dim=-1)
+        xs.append(o + d * (torch.arange(S).view(S, 1) * (3 ** 0.5 / 1024)))
+    x = torch.cat(xs).clamp(0, 1).contiguous()
+    N = x.shape[0]
+    dy = torch.randn(N, 2 * lay.L, generator=g) * 1e-3
+    dy[N // 2: N // 2 + 77] = 0.0
+    tp = torch.zeros(lay.n_params).requires_grad_(True)
+    (FO.grid_encode(x, tp, olay).double() * dy.double()).sum().backward()
+    gref = tp.grad.double()
+    desc = lay.desc()
+    outs = []
+    for fixed, binned in ((True, False), (True, True), (True, True)):
+        gt = torch.zeros(lay.n_params, device=gpu)
+        ws = FLD.grid_bw_binned_workspace(desc, N, gpu) if binned else FLD.grid_bw_workspace(desc, gpu)
+        FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=ws, fixed_point=fixed, binned=binned)
+        got = gt.cpu().double()
+        cuts = sorted(set(2 * o for o in lay.offsets)) + [lay.n_params]  # one region per table
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            scale = float(gref[a:b].abs().max())
+            if scale > 0:  # fixed point: <= ~1e-6 of the table's largest entry (2^-30 of its L1)
+                assert float((got[a:b] - gref[a:b]).abs().max()) <= 1e-4 * scale, (name, binned, a)
+        outs.append(gt)
+    assert torch.equal(outs[1], outs[2])
+
+
 def test_grid_encode_bw_fixed_point_extreme_range(gpu):
     """No int32 overflow whatever the gradient magnitude (the scale follows the L1 bound), and an
     all-zero gradient leaves the table gradient zero."""

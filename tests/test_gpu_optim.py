@@ -149,11 +149,14 @@ def test_adam_step_fixed_matches_torch_adam(gpu):
         copies = torch.randint(-(1 << 16), 1 << 16, (8, dense_vals), generator=g0, dtype=torch.int32)
         tab = q.clone()
         tab[:dense_vals] = copies.sum(0)  # the dense prefix comes only from the copies
+        # each copy holds an entry's two features as one packed integer f1 * 2^32 + f0 (64-bit adds)
+        c64 = copies.view(8, -1, 2).long()
+        packed = (c64[..., 1] << 32) + c64[..., 0]
         g_table = tab.float() * inv
         st.grads.zero_()
         st.grads[:off] = mlp.to(gpu)
         st.grads[off:off + total].view(torch.int32).copy_(q.to(gpu))
-        ws[:8 * dense_vals].copy_(copies.reshape(-1).to(gpu))
+        ws[:8 * dense_vals].copy_(packed.reshape(-1).view(torch.int32).to(gpu))
         skip = k == 2
         if skip:
             st.finite_status[0] = 1
