@@ -302,6 +302,26 @@ int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float
 int mfnerf_field_bw_reduce(int rgb_width, const void* workspace, float* grad_xyz, float* grad_rgb,
                            int32_t* nonfinite, mfnerf_stream_t stream);
 
+/* ---------------------------------------------------------------- standalone FullyFusedMLP (MFMA)
+ * tinycudann.Network / NetworkWithInputEncoding's network as MF-NeRF configures them one module at a
+ * time (models/networks.py:36-79, tcnn FullyFusedMLP: bias-free, ReLU, output activation None or
+ * Sigmoid, fp16): what the reference's own networks.py runs when tinycudann is this library
+ * (module swap).  n_in = 32, width 64 or 128, n_hidden_layers 1 or 2, n_out <= 16
+ * (padded to 16 as tcnn does).  params: tcnn layout, row-major [out][in] per layer, f32. */
+int64_t mfnerf_mlp_n_params(int n_in, int width, int n_hidden, int n_out);
+int64_t mfnerf_mlp_packed_bytes(int n_in, int width, int n_hidden, int n_out);
+int mfnerf_mlp_pack(const float* params, int n_in, int width, int n_hidden, int n_out, void* packed,
+                    mfnerf_stream_t stream);
+/* x (n, 32) f16 -> out (n, 16) f16 (columns >= n_out hold the padded outputs). */
+int mfnerf_mlp_fw(const void* x_f16, int64_t n, const void* packed, int n_in, int width, int n_hidden, int n_out,
+                  int output_sigmoid, void* out_f16, mfnerf_stream_t stream);
+/* dout (n, 16) f16 (zero beyond n_out) -> dx (n, 32) f32 (written), grad (n_params f32, ADDED:
+ * dW = dZ^T A summed over samples in a fixed chunk order).  workspace: mfnerf_mlp_bw_workspace bytes. */
+int64_t mfnerf_mlp_bw_workspace(int64_t n, int n_in, int width, int n_hidden, int n_out);
+int mfnerf_mlp_bw(const void* x_f16, int64_t n, const void* packed, int n_in, int width, int n_hidden, int n_out,
+                  int output_sigmoid, const void* dout_f16, float* dx, float* grad, void* workspace,
+                  mfnerf_stream_t stream);
+
 /* Debug: one v_mfma_f32_32x32x16_f16 with A (32x16) and B (16x32) f16 row-major -> D (32x32) f32,
  * through the lane maps the field kernels assume (pins them on the device). */
 int mfnerf_debug_mfma_probe(const void* A, const void* B, float* D, mfnerf_stream_t stream);

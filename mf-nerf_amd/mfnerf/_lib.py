@@ -85,6 +85,12 @@ SIGNATURES = {
     "mfnerf_adam_step": (_I, [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _I, _P]),
     "mfnerf_adam_step_fixed": (_I, [_P, _P, _P, _P, _P, _I64, _I64, ctypes.POINTER(GridDesc), _P, _P, _F, _F, _F, _F, _P, _P, _P, _P]),
     "mfnerf_field_bw_reduce": (_I, [_I, _P, _P, _P, _P, _P]),
+    "mfnerf_mlp_n_params": (_I64, [_I, _I, _I, _I]),
+    "mfnerf_mlp_packed_bytes": (_I64, [_I, _I, _I, _I]),
+    "mfnerf_mlp_pack": (_I, [_P, _I, _I, _I, _I, _P, _P]),
+    "mfnerf_mlp_fw": (_I, [_P, _I64, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "mfnerf_mlp_bw_workspace": (_I64, [_I64, _I, _I, _I, _I]),
+    "mfnerf_mlp_bw": (_I, [_P, _I64, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "mfnerf_check_finite": (_I, [_P, _I64, _P, _P]),
     "mfnerf_flag_to_shards": (_I, [_P, _I64, _I64, _P, _P]),
     "mfnerf_flag_from_shard": (_I, [_P, _P, _P]),

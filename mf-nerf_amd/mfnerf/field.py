@@ -6,6 +6,7 @@ or MixedFeature grid + FullyFusedMLP 32->64->16, dir_encoder = SH4, rgb_net = Fu
 grid table], rgb_net.params = (7168), every MLP layer a row-major (out, in) block.
 """
 import math
+import weakref
 
 import torch
 
@@ -140,14 +141,17 @@ def field_weights(xyz_params, rgb_params, rgb_width):
     with the same weights."""
     key = (xyz_params.data_ptr(), rgb_params.data_ptr(), int(rgb_width))
     ver = (xyz_params._version, rgb_params._version)
+    owners = tuple(p._base if p._base is not None else p for p in (xyz_params, rgb_params))
     hit = _weights_cache.get(key)
-    if hit is not None and hit[0] == ver:
+    # the owning tensors themselves (weakly held) must match: a new model whose parameters reuse a
+    # freed model's memory and version counts must not be served the old weights
+    if hit is not None and hit[0] == ver and all(r() is o for r, o in zip(hit[3], owners)):
         return hit[1], hit[2]
     net = xyz_params[:XYZ_NET_PARAMS].detach().contiguous()
     table16 = xyz_params[XYZ_NET_PARAMS:].detach().half().contiguous()
     packed = pack_field_weights(net, rgb_params.detach().contiguous(), rgb_width)
     _weights_cache.clear()  # the current model only
-    _weights_cache[key] = (ver, packed, table16)
+    _weights_cache[key] = (ver, packed, table16, tuple(weakref.ref(o) for o in owners))
     return packed, table16
 
 

@@ -3,16 +3,24 @@
 Each module owns one flat fp32 `params` Parameter in tcnn's layout (state-dict keys
 `xyz_encoder.params`, `rgb_net.params` as in the reference), initialised like tcnn (grid
 U(-1e-4, 1e-4), MLP Xavier-uniform).  NGP (mfnerf.networks) does not call these forwards: it
-runs the fused gfx950 field kernels on the same parameters.  The standalone forwards exist for
-users who build tcnn modules directly: grids run the HIP grid kernels; the MLP standalone path
-is a plain fp16 GEMM chain (library GEMMs, not on the hot path).
+runs the fused gfx950 field kernels on the same parameters.  The standalone forwards are what the
+reference's own networks.py runs with `sys.modules["tinycudann"] = mfnerf.tcnn`:
+grids run the HIP grid kernels, the networks the MFMA FullyFusedMLP kernels of mlp.hip
+(mfnerf_mlp_fw / _bw), with tcnn's torch-binding loss scale (128) around the fp16 backward.
+There is no CPU path: a module on a CPU tensor raises.
 """
 import math
+import weakref
 
 import torch
 
+from ._lib import call, load, ptr, stream
 from .field import GridEncodeFunction
 from .grid import GridLayout
+
+# tcnn's torch binding scales the incoming gradient by 128 before its fp16 backward (half params)
+# and divides the results by it (tinycudann/modules.py: loss_scale = 128 for fp16 networks)
+MLP_LOSS_SCALE = 128.0
 
 
 def _pad16(n):
@@ -37,7 +45,72 @@ def _act(x, name):
     return {"None": lambda v: v, "ReLU": torch.relu, "Sigmoid": torch.sigmoid, "Exponential": torch.exp}[name](x)
 
 
+_packed = {}
+
+
+def _mlp_packed(params, cfg):
+    """The MFMA fragment blob of `params` (re-packed only when the parameter changed).  Keyed on
+    the storage's owner tensor itself (weakly held), its data pointer and version counter: a new
+    tensor that reuses a freed one's memory (and version count) must not hit the old blob."""
+    base = params._base if params._base is not None else params
+    key = (params.data_ptr(), params.numel(), cfg)
+    hit = _packed.get(key)
+    if hit is not None and hit[2]() is base and hit[0] == params._version:
+        return hit[1]
+    n_in, width, depth, n_out = cfg
+    nb = load().mfnerf_mlp_packed_bytes(n_in, width, depth, n_out)
+    blob = torch.empty(nb // 2, dtype=torch.float16, device=params.device)
+    call("mfnerf_mlp_pack", ptr(params.detach().float().contiguous()), n_in, width, depth, n_out, ptr(blob), stream())
+    if len(_packed) > 8:
+        _packed.clear()
+    _packed[key] = (params._version, blob, weakref.ref(base))
+    return blob
+
+
+class MLPFunction(torch.autograd.Function):
+    """tcnn FullyFusedMLP forward/backward on the MFMA kernels: x (n, 32) -> (n, n_out) f16."""
+
+    @staticmethod
+    def forward(ctx, x, params, cfg, sigmoid):
+        if not x.is_cuda:
+            raise RuntimeError("mfnerf.tcnn: the networks run on the GPU only (HIP kernels; no CPU path)")
+        n_in, width, depth, n_out = cfg
+        x16 = x.detach().half().contiguous()
+        n = x16.shape[0]
+        out = torch.empty(n, 16, dtype=torch.float16, device=x.device)
+        call("mfnerf_mlp_fw", ptr(x16), n, ptr(_mlp_packed(params, cfg)), n_in, width, depth, n_out, int(sigmoid),
+             ptr(out), stream())
+        ctx.save_for_backward(x16, params)
+        ctx.cfg, ctx.sigmoid, ctx.x_dtype = cfg, sigmoid, x.dtype
+        return out[:, :n_out]
+
+    @staticmethod
+    def backward(ctx, dout):
+        x16, params = ctx.saved_tensors
+        n_in, width, depth, n_out = ctx.cfg
+        n = x16.shape[0]
+        d16 = torch.zeros(n, 16, dtype=torch.float16, device=x16.device)
+        d16[:, :n_out] = (dout.float() * MLP_LOSS_SCALE).half()
+        dx = torch.empty(n, n_in, dtype=torch.float32, device=x16.device)
+        g = torch.zeros(params.numel(), dtype=torch.float32, device=x16.device)
+        ws = torch.empty(max(16, load().mfnerf_mlp_bw_workspace(n, n_in, width, depth, n_out)), dtype=torch.uint8,
+                         device=x16.device)
+        call("mfnerf_mlp_bw", ptr(x16), n, ptr(_mlp_packed(params, ctx.cfg)), n_in, width, depth, n_out,
+             int(ctx.sigmoid), ptr(d16), ptr(dx), ptr(g), ptr(ws), stream())
+        dx.mul_(1.0 / MLP_LOSS_SCALE)
+        g.mul_(1.0 / MLP_LOSS_SCALE)
+        return dx.to(ctx.x_dtype), g.to(params.dtype), None, None
+
+
+def mlp_forward(x, params, width, depth, n_out, activation, output_activation):
+    if activation != "ReLU" or output_activation not in ("None", "Sigmoid") or x.shape[1] != 32:
+        raise NotImplementedError(f"FullyFusedMLP({x.shape[1]} in, {activation}/{output_activation}) is outside "
+                                  "MF-NeRF's configuration")
+    return MLPFunction.apply(x, params, (32, int(width), int(depth), int(n_out)), output_activation == "Sigmoid")
+
+
 def mlp_forward_fp16(x, params, shapes, n_out, activation, output_activation):
+    """The same network as a torch fp16 GEMM chain (test reference for the MFMA kernels)."""
     h = x.half()
     off = 0
     for i, (o, k) in enumerate(shapes):
@@ -102,8 +175,8 @@ class Network(torch.nn.Module):
         self.params = torch.nn.Parameter(_xavier(self.shapes, g))
 
     def forward(self, x):
-        return mlp_forward_fp16(x, self.params, self.shapes, self.n_output_dims, self.activation,
-                                self.output_activation)
+        return mlp_forward(x, self.params, self.width, self.depth, self.n_output_dims, self.activation,
+                           self.output_activation)
 
 
 class NetworkWithInputEncoding(torch.nn.Module):
@@ -122,5 +195,5 @@ class NetworkWithInputEncoding(torch.nn.Module):
 
     def forward(self, x):
         feat = GridEncodeFunction.apply(x, self.params[self.n_net:], self.layout, self.desc)
-        return mlp_forward_fp16(feat, self.params[:self.n_net], self.shapes, self.n_output_dims, self.activation,
-                                self.output_activation)
+        return mlp_forward(feat, self.params[:self.n_net], self.width, self.depth, self.n_output_dims,
+                           self.activation, self.output_activation)

@@ -11,7 +11,7 @@ VolumeRenderer packing (vr_samples), NeRFLoss terms, TruncExp, NGP.forward's nor
 input/concat order, the test-time progressive loop, mark_invisible_cells, and the gradients the
 reference's autograd graph produces.  Only data (inputs/outputs) is written to golden_*.npz.
 
-Run from anywhere:  python tests/golden/make_golden.py [mf128]   (needs /root/reference; CPU only)
+Run from anywhere:  python tests/golden/make_golden.py [mf128|lego]   (needs /root/reference; CPU only)
 "mf128" writes golden_render_mf128.*: the same vectors for the MF benchmark field (MixedFeature
 grid with 8 shared tables, rgb_channels 128).
 """
@@ -61,10 +61,30 @@ class HPMF(HP):
     grid, N_tables, rgb_channels = "MixedFeature", 8, 128
 
 
+class HPLego(HP):
+    """The Lego training field at its real size (opt.py defaults: Hash L16 F2 T2^19, N_min 16,
+    N_max 2048 x scale 0.5 = 1024 finest resolution, rgb 64x2); the 11.4 M-entry table is not
+    stored: it is regenerated from TABLE_SEED, and its gradient is recorded per level (L1, L2, max)
+    plus on a seeded subset of entries and the largest-magnitude entries."""
+    T, N_min, N_max = 19, 16, 2048
+
+
+TABLE_SEED = 1
+N_RAYS = {"": 192, "mf128": 192, "lego": 1024}
+
+
+def table_values(n, seed=TABLE_SEED):
+    """The fixture's table: U(-0.5, 0.5) from a seeded CPU generator (reproducible anywhere)."""
+    g = torch.Generator().manual_seed(seed)
+    return torch.empty(n).uniform_(-0.5, 0.5, generator=g), g
+
+
 def main(variant=""):
     global HP
     if variant == "mf128":
         HP = HPMF
+    elif variant == "lego":
+        HP = HPLego
     install_stubs()
     import warnings
     warnings.filterwarnings("ignore")
@@ -84,15 +104,15 @@ def main(variant=""):
     thr = 0.01 * 1024 / math.sqrt(3)
     vren_oracle.packbits(grid.contiguous(), thr, model.density_bitfield)
     # parameters: larger than tcnn's init so the field is not ~constant (fixture is about semantics)
-    g = torch.Generator().manual_seed(1)
     with torch.no_grad():
         n_net = model.xyz_encoder.n_net
-        model.xyz_encoder.params[n_net:].uniform_(-0.5, 0.5, generator=g)
+        tab, g = table_values(model.xyz_encoder.params.numel() - n_net)
+        model.xyz_encoder.params[n_net:].copy_(tab)
         model.xyz_encoder.params[:n_net].mul_(3)
         model.rgb_net.params.mul_(3)
 
     poses = synthetic.camera_poses(n_cams=20, seed=2)
-    N = 192
+    N = N_RAYS[variant]
     rays_o, rays_d = synthetic.random_rays(N, poses, seed=4)
     target = torch.rand(N, 3, generator=g)
     noise = torch.rand(N, generator=g)
@@ -138,6 +158,16 @@ def main(variant=""):
     out["invisible_bits"] = torch.from_numpy(np.packbits((model.density_grid[0] < 0).numpy(), bitorder="little"))
     out["mark_K"], out["mark_poses"] = K, poses[:3]
 
+    if variant == "lego":  # the table and its gradient are too large to store whole
+        gt = out.pop("grad_xyz_params")
+        out["xyz_params"] = out["xyz_params"][:n_net].clone()
+        out["grad_xyz_net"] = gt[:n_net].clone()
+        gtab = gt[n_net:]
+        sub = torch.randperm(gtab.numel(), generator=torch.Generator().manual_seed(5))[:65536]
+        top = gtab.abs().topk(4096).indices
+        idx = torch.cat([sub, top]).unique()
+        out["grad_table_idx"], out["grad_table_val"] = idx, gtab[idx].clone()
+        out["grad_table_l1"], out["grad_table_l2"] = gtab.abs().sum(), gtab.norm()
     tag = "_" + variant if variant else ""
     np.savez_compressed(os.path.join(HERE, f"golden_render{tag}.npz"),
                         **{k: v.numpy() if isinstance(v, torch.Tensor) else np.asarray(v) for k, v in out.items()})
