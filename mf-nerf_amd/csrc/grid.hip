@@ -369,35 +369,36 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restr
                                     dense_entries, level_l1, l_end);
 }
 
-// Dense own-table levels [0, l_hi) into the private copies, one SAMPLE per lane.  The kernels above
-// give each sample 4 lanes (x-corner x feature) and issue VALU work per lane: they are VALU-bound
-// (PMC: ~58 VALU wave-instructions per 16-sample row step, the same time with the atomics
-// compiled out).  Here a lane holds its sample's whole (y,z) row -- x-pair x 2 features -- so the
-// geometry is computed once per sample and one segmented scan step serves 64 samples:
-//   * the window = DENSE_CPW chunks of 64 consecutive samples; per level and (y,z) row, runs of
-//     equal row keys are merged by a segmented prefix scan over the wave (DPP row_shr 1/2/4/8, then
-//     row_bcast:15 / :31 for the rows' open runs); lane 63's run stays open into the next chunk;
-//   * closed runs (tails; a carried run that the next chunk does not continue) are compacted into
-//     an LDS list and issued two lanes per run, one 64-bit atomic per x-corner carrying BOTH
-//     features as one packed integer hi * 2^32 + lo -- integer addition is exact, so the packed sum
-//     is (sum hi) * 2^32 + (sum lo) and the fold decodes lo = int32(low word), hi = int32(high
-//     word) + (lo < 0) (|sum| < 2^31 by the scale bound): 32 runs per instruction, one 16-B span
-//     (one request) per run.
+// Dense own-table levels [0, l_hi) into the private copies, one SAMPLE per lane.  grid_bw_body
+// gives each sample 4 lanes (x-corner x feature) and merges runs with float segmented scans: it is
+// VALU-bound (PMC: ~58 VALU wave-instructions per 16-sample row step; the same time with its
+// atomics compiled out).  Here a lane holds its sample's whole cell (4 (y,z) rows x 2 x-corners x
+// 2 features = 16 values) and a wave covers 64 consecutive samples (~ a ray):
+//   * each value is rounded to the table's int32 fixed-point unit first (one rounding per sample
+//     contribution); the run sums then come from an UNSEGMENTED integer prefix scan over the wave
+//     (DPP row_shr 1/2/4/8 + row_bcast:15/:31 -- one v_add per step and value) as
+//     P(tail) - P_excl(head): exact and order-free in two's complement;
+//   * a run = consecutive samples in one cell (the 4 rows' keys change together), so one head/tail
+//     structure serves all 16 values; heads and tails write their prefixes into a per-wave LDS
+//     list, one entry per run;
+//   * the list is issued 8 lanes per run -- (row, x-corner) -- each one 64-bit atomic carrying BOTH
+//     features as the packed integer f1 * 2^32 + f0 (the fold decodes f0 = int32(low word),
+//     f1 = int32(high word) + (f0 < 0); |sums| < 2^31 by the scale bound): a run costs 4 requests
+//     (one 16-B span per row), 8 runs per instruction.
 // Requires every level < l_hi to be a dense own table inside the private copies.
 #ifndef MFN_DENSE_ABLATE
 #define MFN_DENSE_ABLATE 0
 #endif
-constexpr int DENSE_CPW = 2;
+#ifndef MFN_DENSE_SHFL
+#define MFN_DENSE_SHFL 0
+#endif
 
 template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ float dppz_f(float v) {  // lanes without a source (or outside ROW_MASK) read 0
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
-}
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ int dppo_i(int v) {  // ... read 1 (a run flag: "still open")
-    return __builtin_amdgcn_update_dpp(1, v, CTRL, ROW_MASK, 0xF, false);
+__device__ __forceinline__ int dppz_i(int v) {  // lanes without a source (or outside ROW_MASK) read 0
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xF, false);
 }
 
+template <int NG>  // float4 groups of dL/dy held per lane: levels < 2 NG
 __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_dense_kernel(const float* __restrict__ X, int64_t n,
                                                                   const int32_t* __restrict__ n_dev, float x_min,
                                                                   float x_range, const mfnerf_grid_desc D,
@@ -406,185 +407,150 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_dense_kernel(const float* _
                                                                   const float* __restrict__ level_l1, int l_hi,
                                                                   int32_t* __restrict__ zero_flag) {
     if (zero_flag && blockIdx.x == 0 && threadIdx.x == 0) *zero_flag = 0;
-    constexpr int WS = DENSE_CPW * 64;
-    extern __shared__ float sdy_dyn[];  // per wave: WS rows of 2 l_hi + 1 floats, then the run list
     __shared__ float fs_s[MFN_MAX_LEVELS];
-    __shared__ int lkey[ENC_BLOCK / 64][66][2];
-    __shared__ long long lval[ENC_BLOCK / 64][66][2];
+    // per wave, one entry per run: the 4 rows' x0 keys, and (tail prefix, head exclusive prefix) of
+    // the 16 values, stored as 4 int4 (row r: x0f0, x0f1, x1f0, x1f1)
+    __shared__ int2 lkey[ENC_BLOCK / 64][64][4];
+    __shared__ int4 ltail[ENC_BLOCK / 64][64][4], lhead[ENC_BLOCK / 64][64][4];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if ((int)threadIdx.x < D.n_levels) fs_s[threadIdx.x] = table_fixed_scale(D, level_l1, threadIdx.x);
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     const int64_t n_waves = ((int64_t)gridDim.x * ENC_BLOCK) >> 6;
-    const int cols = 2 * l_hi, rs = 2 * l_hi + 1, row = 2 * D.n_levels;
-    float* sdy = sdy_dyn + wv * (WS * rs);
-    int(*lk)[2] = lkey[wv];
-    long long(*lv)[2] = lval[wv];
+    const int row = 2 * D.n_levels;
     __syncthreads();  // fs_s
-    for (int64_t wave = ((int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x) >> 6; wave * WS < nn; wave += n_waves) {
-        const int64_t i0 = wave * WS;
-        __builtin_amdgcn_wave_barrier();
-        float px[DENSE_CPW], py[DENSE_CPW], pz[DENSE_CPW];
+    for (int64_t w = ((int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x) >> 6; w * 64 < nn; w += n_waves) {
+        const int64_t i = w * 64 + lane;
+        const bool valid = i < nn;
+        // the sample's position and its dL/dy of levels < l_hi (float4 loads, all issued up front)
+        const float px = valid ? (X[3 * i] - x_min) / x_range : 0.0f;
+        const float py = valid ? (X[3 * i + 1] - x_min) / x_range : 0.0f;
+        const float pz = valid ? (X[3 * i + 2] - x_min) / x_range : 0.0f;
+        float4 gq[NG];
+        {
+            const float4* src = reinterpret_cast<const float4*>(dy + (valid ? i : 0) * row);
+            const int ng = (2 * l_hi + 3) >> 2;
 #pragma unroll
-        for (int k = 0; k < DENSE_CPW; ++k) {  // lane stages sample i0 + 64 k + lane: loads first
-            const int64_t i = i0 + 64 * k + lane;
-            const bool ok = i < nn;
-            const float4* src = reinterpret_cast<const float4*>(dy + (ok ? i : 0) * row);
-            float4 t[MFN_MAX_LEVELS / 2];
-            const int ng = (cols + 3) >> 2;
-#pragma unroll
-            for (int j = 0; j < MFN_MAX_LEVELS / 2; ++j)
-                t[j] = (ok && j < ng) ? src[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-            px[k] = ok ? (X[3 * i] - x_min) / x_range : 0.0f;
-            py[k] = ok ? (X[3 * i + 1] - x_min) / x_range : 0.0f;
-            pz[k] = ok ? (X[3 * i + 2] - x_min) / x_range : 0.0f;
-            float* dst = sdy + (64 * k + lane) * rs;
-#pragma unroll
-            for (int j = 0; j < MFN_MAX_LEVELS / 2; ++j) {
-                if (4 * j < cols) dst[4 * j] = t[j].x;
-                if (4 * j + 1 < cols) dst[4 * j + 1] = t[j].y;
-                if (4 * j + 2 < cols) dst[4 * j + 2] = t[j].z;
-                if (4 * j + 3 < cols) dst[4 * j + 3] = t[j].w;
-            }
+            for (int j = 0; j < NG; ++j)
+                gq[j] = (valid && j < ng) ? src[j] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
         for (int l = 0; l < l_hi; ++l) {
+            float g0 = 0.f, g1 = 0.f;
+#pragma unroll
+            for (int j = 0; j < NG; ++j) {  // uniform-index select of level l's pair
+                if (2 * j == l) { g0 = gq[j].x; g1 = gq[j].y; }
+                if (2 * j + 1 == l) { g0 = gq[j].z; g1 = gq[j].w; }
+            }
             const float fs = fs_s[l];
-            long long* gt = reinterpret_cast<long long*>(priv) +
-                            ((wave & (GRAD_COPIES - 1)) * dense_entries + (int64_t)D.offset[l]);
-            int ckey[4], ckey1[4];
-            float cv[4][4];
+            const LevelGeo Lg = level_geo(D.scale[l], px, py, pz);
+            // dense index x + y res + z res^2 with corner_index's `% size`: corners of points in
+            // [0,1]^3 stay below 2 size, where one conditional subtraction is that modulo
+            const uint32_t res = D.res[l], size = D.size[l];
+            int key[4], key1[4];
+            bool far = false;
 #pragma unroll
             for (int yz = 0; yz < 4; ++yz) {
-                ckey[yz] = -1;
-                ckey1[yz] = -1;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) cv[yz][c] = 0.0f;
+                const uint32_t gy = Lg.g[1] + (yz & 1), gz = Lg.g[2] + (yz >> 1);
+                const uint32_t k0 = Lg.g[0] + (gy + gz * res) * res, k1 = k0 + 1;
+                far |= valid && (k1 >= 2 * size || k1 < k0);
+                key[yz] = (int)(k0 >= size ? k0 - size : k0);
+                key1[yz] = (int)(k1 >= size ? k1 - size : k1);
             }
-#pragma unroll
-            for (int k = 0; k < DENSE_CPW; ++k) {
-                const bool valid = i0 + 64 * k + lane < nn;
-                const float g0 = sdy[(64 * k + lane) * rs + 2 * l], g1 = sdy[(64 * k + lane) * rs + 2 * l + 1];
-                const LevelGeo Lg = level_geo(D.scale[l], px[k], py[k], pz[k]);
-                int key[4], key1[4], open[4];
-                float v[4][4];
-                bool tail[4];
-                // dense index x + y res + z res^2 with corner_index's `% size`: the corners of points
-                // in [0,1]^3 stay below 2 size, where one conditional subtraction is that modulo
-                // (a full integer modulo per corner dominated this kernel's VALU count)
-                const uint32_t res = D.res[l], size = D.size[l];
-                bool far = false;
+            if (__builtin_expect(__ballot(far) != 0, 0)) {  // points far outside the unit cube
 #pragma unroll
                 for (int yz = 0; yz < 4; ++yz) {
                     const uint32_t gy = Lg.g[1] + (yz & 1), gz = Lg.g[2] + (yz >> 1);
-                    const uint32_t k0 = Lg.g[0] + (gy + gz * res) * res, k1 = k0 + 1;
-                    far |= valid && (k1 >= 2 * size || k1 < k0);
-                    key[yz] = valid ? (int)(k0 >= size ? k0 - size : k0) : -1;
-                    key1[yz] = (int)(k1 >= size ? k1 - size : k1);
+                    key[yz] = (int)corner_index(D, l, Lg.g[0], gy, gz);
+                    key1[yz] = (int)corner_index(D, l, Lg.g[0] + 1, gy, gz);
                 }
-                if (__builtin_expect(__ballot(far) != 0, 0)) {  // points far outside the unit cube
-#pragma unroll
-                    for (int yz = 0; yz < 4; ++yz) {
-                        const uint32_t gy = Lg.g[1] + (yz & 1), gz = Lg.g[2] + (yz >> 1);
-                        key[yz] = valid ? (int)corner_index(D, l, Lg.g[0], gy, gz) : -1;
-                        key1[yz] = (int)corner_index(D, l, Lg.g[0] + 1, gy, gz);
-                    }
-                }
+            }
+            // the 16 contributions, each rounded once to the fixed-point unit
+            int q[4][4];
+            {
+                const float a0 = g0 * fs, a1 = g1 * fs;
+                const float w1 = Lg.w[0], w0 = 1.0f - Lg.w[0];
 #pragma unroll
                 for (int yz = 0; yz < 4; ++yz) {
                     const float wy = (yz & 1) ? Lg.w[1] : 1.0f - Lg.w[1];
                     const float wz = (yz >> 1) ? Lg.w[2] : 1.0f - Lg.w[2];
-                    const float wyz = wy * wz, w1 = Lg.w[0], w0 = 1.0f - Lg.w[0];
-                    v[yz][0] = valid ? w0 * wyz * g0 : 0.0f;
-                    v[yz][1] = valid ? w0 * wyz * g1 : 0.0f;
-                    v[yz][2] = valid ? w1 * wyz * g0 : 0.0f;
-                    v[yz][3] = valid ? w1 * wyz * g1 : 0.0f;
-                    const bool cont = lane == 0 && ckey[yz] >= 0 && ckey[yz] == key[yz];
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) v[yz][c] += cont ? cv[yz][c] : 0.0f;
-                    const int kp = __builtin_amdgcn_update_dpp(-2, key[yz], 0x138, 0xF, 0xF, false);  // wave_shr:1
-                    const int kn = __builtin_amdgcn_update_dpp(-2, key[yz], 0x130, 0xF, 0xF, false);  // wave_shl:1
-                    tail[yz] = lane == 63 || kn != key[yz];
-                    open[yz] = !(lane == 0 || kp != key[yz]);  // the run started in an earlier lane
+                    const float wyz = wy * wz;
+                    const float c0 = w0 * wyz, c1 = w1 * wyz;
+                    q[yz][0] = valid ? (int)rintf(c0 * a0) : 0;
+                    q[yz][1] = valid ? (int)rintf(c0 * a1) : 0;
+                    q[yz][2] = valid ? (int)rintf(c1 * a0) : 0;
+                    q[yz][3] = valid ? (int)rintf(c1 * a1) : 0;
                 }
-                // segmented inclusive prefix scan: run tails end with the run total
-#define MFN_SEG(CTRL, RM)                                                                          \
-    _Pragma("unroll") for (int yz = 0; yz < 4; ++yz) {                                             \
-        const int op = dppo_i<CTRL, RM>(open[yz]);                                                 \
-        _Pragma("unroll") for (int c = 0; c < 4; ++c) {                                            \
-            const float vp = dppz_f<CTRL, RM>(v[yz][c]);                                           \
-            v[yz][c] += open[yz] ? vp : 0.0f;                                                      \
-        }                                                                                          \
-        open[yz] = open[yz] ? op : 0;                                                              \
-    }
-                MFN_SEG(0x111, 0xF) MFN_SEG(0x112, 0xF) MFN_SEG(0x114, 0xF) MFN_SEG(0x118, 0xF)
-                MFN_SEG(0x142, 0xA) MFN_SEG(0x143, 0xC)
-#undef MFN_SEG
-                // closed runs -> the wave's LDS list (at most 64 tails + lane 0's flushed carry)
+            }
+            // runs: consecutive samples in one cell (row 0's key identifies the cell)
+            const int cell = valid ? key[0] : -1;
+            const int cp = __builtin_amdgcn_update_dpp(-2, cell, 0x138, 0xF, 0xF, false);  // wave_shr:1
+            const int cn = __builtin_amdgcn_update_dpp(-2, cell, 0x130, 0xF, 0xF, false);  // wave_shl:1
+            const bool head = valid && (lane == 0 || cp != cell);
+            const bool tail = valid && (lane == 63 || cn != cell);
+            // inclusive prefix sums over the wave (wraparound int32: differences are exact)
+            int P[4][4];
+#pragma unroll
+            for (int yz = 0; yz < 4; ++yz)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) P[yz][c] = q[yz][c];
+#define MFN_PSTEP(CTRL, RM)                                                                   \
+    _Pragma("unroll") for (int yz = 0; yz < 4; ++yz)                                          \
+        _Pragma("unroll") for (int c = 0; c < 4; ++c) P[yz][c] += dppz_i<CTRL, RM>(P[yz][c]);
+#if MFN_DENSE_SHFL  // experiment: the scan by lane shuffles
+#pragma unroll
+            for (int dd = 1; dd < 64; dd <<= 1)
+#pragma unroll
+                for (int yz = 0; yz < 4; ++yz)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const int u = __shfl_up(P[yz][c], dd, 64);
+                        if (lane >= dd) P[yz][c] += u;
+                    }
+#else
+            MFN_PSTEP(0x111, 0xF) MFN_PSTEP(0x112, 0xF) MFN_PSTEP(0x114, 0xF) MFN_PSTEP(0x118, 0xF)
+            MFN_PSTEP(0x142, 0xA) MFN_PSTEP(0x143, 0xC)
+#endif
+#undef MFN_PSTEP
+            // run index of each lane = heads at or before it - 1; heads write the exclusive prefix,
+            // tails the inclusive one and the keys
+            const uint64_t hb = __ballot(head);
+            const int nruns = __popcll(hb);
+            const int run = __builtin_amdgcn_mbcnt_hi((uint32_t)(hb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u)) +
+                            (head ? 0 : -1);
+            if (head) {
+#pragma unroll
+                for (int yz = 0; yz < 4; ++yz)
+                    lhead[wv][run][yz] = make_int4(P[yz][0] - q[yz][0], P[yz][1] - q[yz][1], P[yz][2] - q[yz][2],
+                                                   P[yz][3] - q[yz][3]);
+            }
+            if (tail) {
 #pragma unroll
                 for (int yz = 0; yz < 4; ++yz) {
-                    const bool emit = tail[yz] && lane != 63 && key[yz] >= 0;
-                    const bool flush = lane == 0 && ckey[yz] >= 0 && ckey[yz] != key[yz];
-                    const uint64_t be = __ballot(emit);
-                    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(be >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)be, 0u));
-                    const int ne = __popcll(be);
-                    auto pack = [&](float a, float b) -> long long {
-                        const int qa = (int)rintf(a * fs), qb = (int)rintf(b * fs);
-                        return (long long)((uint64_t)(uint32_t)qb << 32) + (long long)qa;
-                    };
-                    if (emit) {
-                        lk[rank][0] = key[yz];
-                        lk[rank][1] = key1[yz];
-                        lv[rank][0] = pack(v[yz][0], v[yz][1]);
-                        lv[rank][1] = pack(v[yz][2], v[yz][3]);
-                    }
-                    if (flush) {
-                        lk[ne][0] = ckey[yz];
-                        lk[ne][1] = ckey1[yz];
-                        lv[ne][0] = pack(cv[yz][0], cv[yz][1]);
-                        lv[ne][1] = pack(cv[yz][2], cv[yz][3]);
-                    }
-#if MFN_DENSE_ABLATE == 2  // experiment: no list, no atomics
-                    const int nl = 0;
-#else
-                    const int nl = ne + (__ballot(flush) ? 1 : 0);
-#endif
-                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    for (int b = 0; b < nl; b += 32) {  // two lanes (x-corners) per run
-                        const int j = b + (lane >> 1), c = lane & 1;
-                        if (j < nl) {
-                            const long long q = lv[j][c];
-#if MFN_DENSE_ABLATE == 1  // experiment: list built and read, no atomics
-                            if (q == 0x7fffffffffffll)
-#else
-                            if (q != 0)
-#endif
-                                __hip_atomic_fetch_add(gt + lk[j][c], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        }
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    // lane 63's run stays open
-                    ckey[yz] = __builtin_amdgcn_readlane(key[yz], 63);
-                    ckey1[yz] = __builtin_amdgcn_readlane(key1[yz], 63);
-#pragma unroll
-                    for (int c = 0; c < 4; ++c)
-                        cv[yz][c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[yz][c]), 63));
+                    ltail[wv][run][yz] = make_int4(P[yz][0], P[yz][1], P[yz][2], P[yz][3]);
+                    lkey[wv][run][yz] = make_int2(key[yz], key1[yz]);
                 }
             }
-            // the window's last open runs
-#pragma unroll
-            for (int yz = 0; yz < 4; ++yz) {
-                if (lane < 2 && ckey[yz] >= 0) {
-                    const float a = lane ? cv[yz][2] : cv[yz][0], b = lane ? cv[yz][3] : cv[yz][1];
-                    const int qa = (int)rintf(a * fs), qb = (int)rintf(b * fs);
-                    const long long q = (long long)((uint64_t)(uint32_t)qb << 32) + (long long)qa;
-                    if (q != 0)
-                        __hip_atomic_fetch_add(gt + (lane ? ckey1[yz] : ckey[yz]), q, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            long long* gt = reinterpret_cast<long long*>(priv) +
+                            ((w & (GRAD_COPIES - 1)) * dense_entries + (int64_t)D.offset[l]);
+            // issue: 8 lanes per run = (row, x-corner); both features packed in one 64-bit add
+            for (int b = 0; b < nruns; b += 8) {
+                const int r = b + (lane >> 3), yz = (lane >> 1) & 3, c = lane & 1;
+                if (r < nruns) {
+                    const int4 t = ltail[wv][r][yz], h = lhead[wv][r][yz];
+                    const int f0 = c ? t.z - h.z : t.x - h.x, f1 = c ? t.w - h.w : t.y - h.y;
+                    const int2 kp = lkey[wv][r][yz];
+                    const int kk = c ? kp.y : kp.x;
+                    const long long pq = (long long)((uint64_t)(uint32_t)f1 << 32) + (long long)f0;
+#if MFN_DENSE_ABLATE == 1
+                    if (pq == 0x7fffffffffffll)
+#else
+                    if (pq != 0)
+#endif
+                        __hip_atomic_fetch_add(gt + kk, pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
+            __builtin_amdgcn_wave_barrier();  // the list is rewritten by the next level
         }
     }
 }
@@ -1643,9 +1609,9 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
     }
     if ((parts & 1) && l_first > 0 && dense_mode && l_first <= n_dense_levels) {
         // levels [0, l_first) all dense: one sample per lane, packed 64-bit adds into the copies
-        const int64_t wb = div_up<int64_t>(n, (int64_t)DENSE_CPW * 64 * (ENC_BLOCK / 64));
-        const size_t lds = (size_t)(ENC_BLOCK / 64) * DENSE_CPW * 64 * (2 * l_first + 1) * sizeof(float);
-        hipLaunchKernelGGL(grid_bw_dense_kernel, dim3((unsigned)(wb < cap ? wb : cap)), dim3(ENC_BLOCK), lds, stream,
+        const int64_t wb = div_up<int64_t>(n, (int64_t)64 * (ENC_BLOCK / 64));
+        auto dk = l_first <= 8 ? grid_bw_dense_kernel<4> : l_first <= 16 ? grid_bw_dense_kernel<8> : grid_bw_dense_kernel<16>;
+        hipLaunchKernelGGL(dk, dim3((unsigned)(wb < cap ? wb : cap)), dim3(ENC_BLOCK), 0, stream,
                            x, n, n_dev, x_min, x_range, *desc, dL_dout, W.priv, dense_entries_of(desc), level_l1,
                            l_first, (parts & 2) ? W.ovf : (int32_t*)nullptr);
     } else if ((parts & 1) && l_first > 0) {  // dense levels [0, l_first): request-shaped atomics, private copies

@@ -124,7 +124,11 @@ def test_grid_encode_bw_along_rays(gpu):
         gt = torch.zeros(lay.n_params, device=gpu)
         ws = FLD.grid_bw_binned_workspace(desc, N, gpu) if binned else FLD.grid_bw_workspace(desc, gpu)
         FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=ws, fixed_point=fixed, binned=binned)
-        assert torch.allclose(gt.cpu(), gref, rtol=1e-4, atol=1e-4 * float(gref.abs().max()))
+        # the fixed-point quantum is 2^-30 of the level's L1 (~1e-3 of one contribution here); the
+        # binned path's dense levels round every sample's contribution once (run sums are integer),
+        # ~sqrt(contributions) quanta per entry: 2e-4 of the level's largest entry
+        tol = 2e-4 if binned else 1e-4
+        assert torch.allclose(gt.cpu(), gref, rtol=1e-4, atol=tol * float(gref.abs().max()))
     # the training regime: per-sample gradients ~1e-7 of very different size per level; the
     # fixed-point resolution (2^-30 of each level's L1) stays far below fp32's relative error
     dys = dy * torch.logspace(-9, -5, 32).view(1, 32)
@@ -141,7 +145,7 @@ def test_grid_encode_bw_along_rays(gpu):
             scale = float(gref[a:b].abs().max())
             if scale > 0:
                 err = float((got[a:b] - gref[a:b]).abs().max()) / scale
-                assert err < 1e-4, (binned, l, err)
+                assert err < (2e-4 if binned else 1e-4), (binned, l, err)
 
 
 @pytest.mark.parametrize("name,args", [_layouts()[0], _layouts()[2]])
@@ -176,8 +180,9 @@ def test_grid_encode_bw_ragged_rays(gpu, name, args):
         cuts = sorted(set(2 * o for o in lay.offsets)) + [lay.n_params]  # one region per table
         for a, b in zip(cuts[:-1], cuts[1:]):
             scale = float(gref[a:b].abs().max())
-            if scale > 0:  # fixed point: <= ~1e-6 of the table's largest entry (2^-30 of its L1)
-                assert float((got[a:b] - gref[a:b]).abs().max()) <= 1e-4 * scale, (name, binned, a)
+            if scale > 0:  # fixed point: quanta of 2^-30 of the table's L1 (see test_grid_encode_bw_along_rays)
+                assert float((got[a:b] - gref[a:b]).abs().max()) <= (2e-4 if binned else 1e-4) * scale, \
+                    (name, binned, a)
         outs.append(gt)
     assert torch.equal(outs[1], outs[2])
 
