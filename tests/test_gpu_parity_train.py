@@ -101,9 +101,12 @@ def test_training_psnr_matches_reference(gpu):
               [(h["step"], round(losses[h["step"]], 5), round(h["loss"], 5)) for h in ref["history"]])
         assert skipped == 0 and got == got
         diffs.append(got - ref["test_psnr"])
-        # the loss curves agree along the way (same batches; trajectories drift apart slowly)
+        # the loss curves agree while the trajectories are still together (same batches: the first
+        # 100 steps agree to a few 1e-3; from ~150 steps on single-batch losses drift apart with the
+        # trajectories, both ways, by 10-30 %)
         rel = [abs(losses[h["step"]] - h["loss"]) / h["loss"] for h in ref["history"]]
-        assert sum(rel) / len(rel) < 0.15, (seed, rel)
+        early = rel[:len(rel) // 4]
+        assert sum(early) / len(early) < 0.02, (seed, rel)
     k = len(diffs)
     mean = sum(diffs) / k
     sd = (sum((d - mean) ** 2 for d in diffs) / (k - 1)) ** 0.5 if k > 1 else 0.0
