@@ -26,7 +26,7 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # the table-gradient scatter's kernels in the PMC summaries: the run-merging atomics (dense and coarse
 # hashed levels) and the partitioned fine levels' scatter / accumulate / (idle) fallback
-GRID_BW_KERNEL = ("grid_bw_kernel", "bin_scatter_kernel", "bin_accum_kernel", "bin_fallback_kernel")
+GRID_BW_KERNEL = ("grid_bw_dense_kernel", "grid_bw_kernel", "bin_scatter_kernel", "bin_accum_kernel", "bin_fallback_kernel")
 
 # algorithmic bytes per live sample of each per-sample kernel, as SURVEY.md 8(d) prices them (the
 # tcnn form of the op: fp16 features and fp16 gradient scatter), DESIGN.md section 5
