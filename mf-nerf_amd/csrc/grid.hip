@@ -836,17 +836,18 @@ int check_desc(const mfnerf_grid_desc* d, const char* what) {
 // 12-B record routed to its partition by a counting sort, and one workgroup per partition sums its
 // records into an LDS image with integer LDS atomics (ds_add_u32: ~4 T adds/s chip-wide at random
 // addresses, tools/lds_atomic_probe.hip -- 20x ds_add_f32), then stores the image once.  The image
-// is int64 at 2^32 x the table's int32 fixed-point scale: each contribution keeps its fp32
-// precision, the sum is exact and order-free (bit-reproducible), and the stored int32 value (the
-// format grid_bw_kernel leaves for the finish / Adam pass) is rounded ONCE per entry -- finer than
-// grid_bw_kernel's one rounding per run-merged contribution.  Passes: count (per-block bin
+// holds one 64-bit word per entry: both features' sums in the table's int32 fixed-point unit,
+// packed f1 * 2^32 + f0 (exact in two's complement, order-free: bit-reproducible), each weighted
+// contribution rounded once to the unit -- 2 LDS atomics per pair record.  (MFN_ACC32=0 keeps an
+// int64 image per feature at 2^32 x the unit, rounded once per entry: 4 atomics and a float ->
+// int64 conversion per record, 349 vs 316 us for the whole scatter.)  Passes: count (per-block bin
 // histogram; in the same launch as the dense coarse levels' scatter, which stays on grid_bw_body:
 // few hot lines, private copies, in-wave run merging -- the two overlap) -> scan (per bin over
 // blocks) -> scatter (records) -> accumulate.
 // partitions of 2^shift entries, shift in [MIN_BIN_SHIFT, MAX_BIN_SHIFT] chosen per layout so that
 // there are >= ~1024 partitions (4 workgroups per CU); 2^11 entries = 32 KB of int64 pairs
 #ifndef MFN_ACC32
-#define MFN_ACC32 0  // int64 LDS image at 2^32 x the scale, rounded once per entry (0), or int32 (1)
+#define MFN_ACC32 2  // 2: packed int32 pairs (one 64-bit LDS word per entry); 1: int32 words; 0: int64 at 2^32 x the scale
 #endif
 constexpr int MIN_BIN_SHIFT = 8, MAX_BIN_SHIFT = 11, MAX_BIN_ENTRIES = 1 << MAX_BIN_SHIFT;
 constexpr int MAX_BINS = 4096;
@@ -1035,8 +1036,10 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                                                                  const BinPlan P, const float* __restrict__ dy,
                                                                  const float* __restrict__ level_l1,
                                                                  uint3* __restrict__ rec, int32_t* __restrict__ scnt,
+                                                                 uint32_t* __restrict__ smax,
                                                                  int32_t* __restrict__ ovf, int64_t n_slots) {
     __shared__ int cursor[MAX_BINS];
+    uint32_t rmax = 0u;  // largest |a|, |b| of this thread's records (float bits order as uints)
     __shared__ int thist[MAX_TBINS], toff[MAX_TBINS], gdst[MAX_TBINS];
     __shared__ uint3 stage[SC_STAGE];
     __shared__ uint16_t sbin[SC_STAGE];
@@ -1078,8 +1081,11 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
 #pragma unroll
             for (int q = 0; q < 2; ++q)
                 if (live[q])
-                    staged_records(D, P, S[q], Q[q], fs_s, j, [&](int, int bin, uint3) {
-                        if (bin >= 0) atomicAdd(&thist[bin - b0], 1);
+                    staged_records(D, P, S[q], Q[q], fs_s, j, [&](int, int bin, uint3 r) {
+                        if (bin >= 0) {
+                            atomicAdd(&thist[bin - b0], 1);
+                            rmax = max(rmax, max(r.y & 0x7fffffffu, r.z & 0x7fffffffu));  // |float| bits order
+                        }
                     });
             __syncthreads();
             // bins -> sorted tile offsets (toff); a run's k-th record goes to its slot position gdst + k
@@ -1126,6 +1132,20 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
             __syncthreads();
         }
     }
+    // the unit's largest contribution (one word per unit: the accumulate's per-partition bound is
+    // sum over units of count x this max)
+    {
+        __shared__ uint32_t wmax[SC_THREADS / 64];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, off, 64));
+        if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = rmax;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t m = 0u;
+            for (int k = 0; k < SC_THREADS / 64; ++k) m = max(m, wmax[k]);
+            smax[u] = m;
+        }
+    }
     bool over = false;
     for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x) {
         const int c = cursor[b];
@@ -1149,7 +1169,34 @@ __device__ __forceinline__ long long f2ll(float v) {
     return fabsf(v) < 2147483648.0f ? (long long)(int)rintf(v) : big;
 }
 
-#if MFN_ACC32
+#if MFN_ACC32 == 2
+// packed image: one 64-bit word per entry holding both features' int32 sums as f1 * 2^32 + f0
+// (exact in two's complement; decoded f0 = lo, f1 = hi + (f0 < 0) at the store), 2 LDS atomics
+// per pair record.  The sums run at the PARTITION's own finer unit 2^-k of the table's: k is the
+// largest with (sum over units of the unit's record count in the partition x the unit's largest
+// |a|, |b|) * 2^k <= 2^30 -- a bound on every entry's sum, from bin_scatter's counts and maxima -- so
+// the int32 fields cannot overflow, and the stored table-unit value is rounded once per entry.
+using acc_t = unsigned long long;
+__device__ __forceinline__ unsigned long long pack2(float a, float b) {
+    return ((unsigned long long)(uint32_t)(int)rintf(b) << 32) + (unsigned long long)(long long)(int)rintf(a);
+}
+__device__ __forceinline__ void accum_record(unsigned long long* img, int mask, uint3 r, float k2) {
+    const uint32_t w = r.x;
+    const float a = __uint_as_float(r.y) * k2, b = __uint_as_float(r.z) * k2;  // exact: a power of two
+    if (a == 0.0f && b == 0.0f) return;
+    const float fx = (float)(w >> 17) * (1.0f / 32768.0f);
+    const int e0 = w & mask;
+    if (w & (1u << 15)) {  // single entry, weight sel ? fx : 1 - fx
+        const float wt = (w & (1u << 16)) ? fx : 1.0f - fx;
+        atomicAdd(&img[e0], pack2(wt * a, wt * b));
+    } else {
+        const int e1 = e0 ^ ((2 << ((w >> 11) & 15)) - 1);
+        const float w0 = 1.0f - fx;
+        atomicAdd(&img[e0], pack2(w0 * a, w0 * b));
+        atomicAdd(&img[e1], pack2(fx * a, fx * b));
+    }
+}
+#elif MFN_ACC32
 // int32 image in the table's fixed-point units: each weighted contribution rounded once (as
 // grid_bw_body rounds each run-merged one), the sums exact and order-free.  One cvt per value
 // instead of the int64 path's float -> int64 conversion: the accumulate is VALU-bound.
@@ -1206,13 +1253,19 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
                                                                 const int32_t* __restrict__ n_dev,
                                                                 const uint3* __restrict__ rec,
                                                                 const int32_t* __restrict__ scnt,
+                                                                const uint32_t* __restrict__ smax,
                                                                 const int32_t* __restrict__ ovf,
                                                                 int* __restrict__ grad, int64_t n_slots) {
     if (*ovf) return;  // a slot overflowed: bin_fallback_kernel scatters the binned levels
-    __shared__ acc_t img[2 * MAX_BIN_ENTRIES];
+#if MFN_ACC32 == 2
+    constexpr int IMG_WORDS = 1;  // per entry
+#else
+    constexpr int IMG_WORDS = 2;
+#endif
+    __shared__ acc_t img[IMG_WORDS * MAX_BIN_ENTRIES];
     const int bin = blockIdx.x;
     const int n_ent = 1 << P.shift, mask = n_ent - 1;
-    for (int i = threadIdx.x; i < 2 * n_ent; i += blockDim.x) img[i] = 0;
+    for (int i = threadIdx.x; i < IMG_WORDS * n_ent; i += blockDim.x) img[i] = 0;
     __syncthreads();
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     const int64_t slot = slot_size(min(nn, n_slots), P);  // = bin_scatter_kernel's
@@ -1221,6 +1274,29 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     const int hw = threadIdx.x >> 5, hl = threadIdx.x & 31, n_hw = ACC_THREADS / 32;
     const int32_t* cnt = scnt + (int64_t)bin * UNITS;
     const uint3* base = rec + (int64_t)bin * UNITS * slot;
+#if MFN_ACC32 == 2
+    // the partition's bound (sum over units of count x max), summed in a fixed order -> its unit 2^-k
+    __shared__ float wsum[ACC_THREADS / 64];
+    float term = 0.0f;
+    if ((int)threadIdx.x < UNITS) {
+        const int u = threadIdx.x;
+        term = (float)min(cnt[u], (int32_t)slot) * __uint_as_float(smax[u]);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) term += __shfl_xor(term, off, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = term;
+    __syncthreads();
+    float bound = 0.0f;
+#pragma unroll
+    for (int k = 0; k < ACC_THREADS / 64; ++k) bound += wsum[k];
+    int kbits = 0;
+    if (bound > 0.0f) {
+        int e;
+        frexpf(bound * 1.0001f, &e);  // bound (with margin for its own rounding) < 2^e
+        kbits = max(0, min(30, 30 - e));
+    }
+    const float k2 = ldexpf(1.0f, kbits);
+#endif
     for (int u0 = hw; u0 < UNITS; u0 += 4 * n_hw) {
         uint3 r[4];
         int c[4];
@@ -1230,19 +1306,35 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
             c[q] = u < UNITS ? cnt[u] : 0;
             r[q] = hl < c[q] ? base[(int64_t)u * slot + hl] : make_uint3(0u, 0u, 0u);
         }
+#if MFN_ACC32 == 2
+#define MFN_ACC(IMG, MASK, R) accum_record(IMG, MASK, R, k2)
+#else
+#define MFN_ACC(IMG, MASK, R) accum_record(IMG, MASK, R)
+#endif
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int u = u0 + q * n_hw;
-            accum_record(img, mask, r[q]);
-            for (int k = hl + 32; k < c[q]; k += 32) accum_record(img, mask, base[(int64_t)u * slot + k]);
+            MFN_ACC(img, mask, r[q]);
+            for (int k = hl + 32; k < c[q]; k += 32) MFN_ACC(img, mask, base[(int64_t)u * slot + k]);
         }
+#undef MFN_ACC
     }
     __syncthreads();
     const int t = bin_table(P, bin);
     const int64_t e_lo = (int64_t)(bin - P.t_bin0[t]) << P.shift;
     const int n_e = (int)min<int64_t>(n_ent, (int64_t)P.t_size[t] - e_lo);
     int* dst = grad + 2 * ((int64_t)P.t_offset[t] + e_lo);
+#if MFN_ACC32 == 2
+    const int rnd = kbits > 0 ? 1 << (kbits - 1) : 0;
+    for (int i = threadIdx.x; i < n_e; i += blockDim.x) {
+        const unsigned long long v = img[i];
+        const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32) + (lo < 0);
+        // back to the table's unit, rounded once (|fields| <= 2^30: no overflow adding rnd)
+        reinterpret_cast<int2*>(dst)[i] = make_int2((lo + rnd) >> kbits, (hi + rnd) >> kbits);
+    }
+#else
     for (int i = threadIdx.x; i < 2 * n_e; i += blockDim.x) dst[i] = acc_out(img[i]);
+#endif
 }
 
 // the binned levels by request-shaped int32 atomics (grid_bw_body), only if a slot overflowed (a
@@ -1334,6 +1426,7 @@ int first_binned_level(const mfnerf_grid_desc* d) {
 struct BinWorkspace {
     float* priv;
     int32_t *scnt, *ovf;
+    uint32_t* smax;
     uint3* rec;
 };
 
@@ -1348,6 +1441,8 @@ int64_t binned_workspace_layout(const mfnerf_grid_desc* d, int64_t n_max, char* 
     const int64_t nb = P.n_bins > 0 ? P.n_bins : 1;
     if (W) W->scnt = reinterpret_cast<int32_t*>(base + off);
     off += align256(nb * UNITS * 4);
+    if (W) W->smax = reinterpret_cast<uint32_t*>(base + off);
+    off += align256(UNITS * 4);
     if (W) W->ovf = reinterpret_cast<int32_t*>(base + off);
     off += 256;
     if (W) W->rec = reinterpret_cast<uint3*>(base + off);
@@ -1626,9 +1721,9 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
         // shared tables bin more)
         auto sk = P.n_binned <= 8 ? bin_scatter_kernel<8> : bin_scatter_kernel<MAX_BINNED>;
         hipLaunchKernelGGL(sk, dim3(UNITS), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
-                           *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.ovf, n_slots);
+                           *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.smax, W.ovf, n_slots);
         hipLaunchKernelGGL(bin_accum_kernel, dim3(P.n_bins), dim3(ACC_THREADS), 0, stream, P, n, n_dev, W.rec,
-                           W.scnt, W.ovf, (int*)grad_table, n_slots);
+                           W.scnt, W.smax, W.ovf, (int*)grad_table, n_slots);
         // levels [l_first, L) by atomics, only when a slot overflowed (exits at once otherwise)
         auto fb = big ? bin_fallback_kernel<MFN_MAX_LEVELS> : bin_fallback_kernel<16>;
         hipLaunchKernelGGL(fb, dim3(256), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc, dL_dout,
