@@ -398,6 +398,15 @@ __device__ __forceinline__ int dppz_i(int v) {  // lanes without a source (or ou
     return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xF, false);
 }
 
+// a wave's window: DENSE_WIN chunks of 64 consecutive samples; the run open at a chunk's end is
+// carried into the next chunk (per level, in LDS) instead of being issued twice
+constexpr int DENSE_WIN = 4;
+
+struct DenseIn {
+    float px, py, pz;
+    bool valid;
+};
+
 template <int NG>  // float4 groups of dL/dy held per lane: levels < 2 NG
 __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_dense_kernel(const float* __restrict__ X, int64_t n,
                                                                   const int32_t* __restrict__ n_dev, float x_min,
@@ -408,149 +417,190 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_dense_kernel(const float* _
                                                                   int32_t* __restrict__ zero_flag) {
     if (zero_flag && blockIdx.x == 0 && threadIdx.x == 0) *zero_flag = 0;
     __shared__ float fs_s[MFN_MAX_LEVELS];
-    // per wave, one entry per run: the 4 rows' x0 keys, and (tail prefix, head exclusive prefix) of
-    // the 16 values, stored as 4 int4 (row r: x0f0, x0f1, x1f0, x1f1)
-    __shared__ int2 lkey[ENC_BLOCK / 64][64][4];
-    __shared__ int4 ltail[ENC_BLOCK / 64][64][4], lhead[ENC_BLOCK / 64][64][4];
+    // per wave, one entry per run (+1 for a flushed carry): the 4 rows' (x0, x1) keys, and (tail
+    // prefix, head exclusive prefix) of the 16 values as 4 int4 (row r: x0f0, x0f1, x1f0, x1f1)
+    __shared__ int2 lkey[ENC_BLOCK / 64][65][4];
+    __shared__ int4 ltail[ENC_BLOCK / 64][65][4], lhead[ENC_BLOCK / 64][65][4];
+    // per wave and level: the run left open at the previous chunk's end (sums, keys, on/off)
+    __shared__ int4 csum[ENC_BLOCK / 64][2 * NG][4];
+    __shared__ int2 ckey[ENC_BLOCK / 64][2 * NG][4];
+    __shared__ int con[ENC_BLOCK / 64][2 * NG];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if ((int)threadIdx.x < D.n_levels) fs_s[threadIdx.x] = table_fixed_scale(D, level_l1, threadIdx.x);
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     const int64_t n_waves = ((int64_t)gridDim.x * ENC_BLOCK) >> 6;
     const int row = 2 * D.n_levels;
     __syncthreads();  // fs_s
-    for (int64_t w = ((int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x) >> 6; w * 64 < nn; w += n_waves) {
-        const int64_t i = w * 64 + lane;
-        const bool valid = i < nn;
-        // the sample's position and its dL/dy of levels < l_hi (float4 loads, all issued up front)
-        const float px = valid ? (X[3 * i] - x_min) / x_range : 0.0f;
-        const float py = valid ? (X[3 * i + 1] - x_min) / x_range : 0.0f;
-        const float pz = valid ? (X[3 * i + 2] - x_min) / x_range : 0.0f;
-        float4 gq[NG];
-        {
-            const float4* src = reinterpret_cast<const float4*>(dy + (valid ? i : 0) * row);
-            const int ng = (2 * l_hi + 3) >> 2;
+    auto load = [&](int64_t i, DenseIn& in, float4* gq) {
+        in.valid = i < nn;
+        in.px = in.valid ? (X[3 * i] - x_min) / x_range : 0.0f;
+        in.py = in.valid ? (X[3 * i + 1] - x_min) / x_range : 0.0f;
+        in.pz = in.valid ? (X[3 * i + 2] - x_min) / x_range : 0.0f;
+        const float4* src = reinterpret_cast<const float4*>(dy + (in.valid ? i : 0) * row);
+        const int ng = (2 * l_hi + 3) >> 2;
 #pragma unroll
-            for (int j = 0; j < NG; ++j)
-                gq[j] = (valid && j < ng) ? src[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        for (int l = 0; l < l_hi; ++l) {
-            float g0 = 0.f, g1 = 0.f;
+        for (int j = 0; j < NG; ++j) gq[j] = (in.valid && j < ng) ? src[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    for (int64_t w = ((int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x) >> 6; w * 64 * DENSE_WIN < nn; w += n_waves) {
+        const int64_t i0 = w * 64 * DENSE_WIN;
+        for (int l = lane; l < l_hi; l += 64) con[wv][l] = 0;
+        DenseIn in, nx;
+        float4 gq[NG], gn[NG];
+        load(i0 + lane, in, gq);
+        for (int k = 0; k < DENSE_WIN && i0 + 64 * k < nn; ++k) {
+            const bool more = k + 1 < DENSE_WIN && i0 + 64 * (k + 1) < nn;
+            if (more) load(i0 + 64 * (k + 1) + lane, nx, gn);  // in flight during this chunk's atomics
+            const bool valid = in.valid;
+            for (int l = 0; l < l_hi; ++l) {
+                float g0 = 0.f, g1 = 0.f;
 #pragma unroll
-            for (int j = 0; j < NG; ++j) {  // uniform-index select of level l's pair
-                if (2 * j == l) { g0 = gq[j].x; g1 = gq[j].y; }
-                if (2 * j + 1 == l) { g0 = gq[j].z; g1 = gq[j].w; }
-            }
-            const float fs = fs_s[l];
-            const LevelGeo Lg = level_geo(D.scale[l], px, py, pz);
-            // dense index x + y res + z res^2 with corner_index's `% size`: corners of points in
-            // [0,1]^3 stay below 2 size, where one conditional subtraction is that modulo
-            const uint32_t res = D.res[l], size = D.size[l];
-            int key[4], key1[4];
-            bool far = false;
-#pragma unroll
-            for (int yz = 0; yz < 4; ++yz) {
-                const uint32_t gy = Lg.g[1] + (yz & 1), gz = Lg.g[2] + (yz >> 1);
-                const uint32_t k0 = Lg.g[0] + (gy + gz * res) * res, k1 = k0 + 1;
-                far |= valid && (k1 >= 2 * size || k1 < k0);
-                key[yz] = (int)(k0 >= size ? k0 - size : k0);
-                key1[yz] = (int)(k1 >= size ? k1 - size : k1);
-            }
-            if (__builtin_expect(__ballot(far) != 0, 0)) {  // points far outside the unit cube
+                for (int j = 0; j < NG; ++j) {  // uniform-index select of level l's pair
+                    if (2 * j == l) { g0 = gq[j].x; g1 = gq[j].y; }
+                    if (2 * j + 1 == l) { g0 = gq[j].z; g1 = gq[j].w; }
+                }
+                const float fs = fs_s[l];
+                const LevelGeo Lg = level_geo(D.scale[l], in.px, in.py, in.pz);
+                // dense index x + y res + z res^2 with corner_index's `% size`: corners of points in
+                // [0,1]^3 stay below 2 size, where one conditional subtraction is that modulo
+                const uint32_t res = D.res[l], size = D.size[l];
+                int key[4], key1[4];
+                bool far = false;
 #pragma unroll
                 for (int yz = 0; yz < 4; ++yz) {
                     const uint32_t gy = Lg.g[1] + (yz & 1), gz = Lg.g[2] + (yz >> 1);
-                    key[yz] = (int)corner_index(D, l, Lg.g[0], gy, gz);
-                    key1[yz] = (int)corner_index(D, l, Lg.g[0] + 1, gy, gz);
+                    const uint32_t k0 = Lg.g[0] + (gy + gz * res) * res, k1 = k0 + 1;
+                    far |= valid && (k1 >= 2 * size || k1 < k0);
+                    key[yz] = (int)(k0 >= size ? k0 - size : k0);
+                    key1[yz] = (int)(k1 >= size ? k1 - size : k1);
                 }
-            }
-            // the 16 contributions, each rounded once to the fixed-point unit
-            int q[4][4];
-            {
-                const float a0 = g0 * fs, a1 = g1 * fs;
-                const float w1 = Lg.w[0], w0 = 1.0f - Lg.w[0];
+                if (__builtin_expect(__ballot(far) != 0, 0)) {  // points far outside the unit cube
 #pragma unroll
-                for (int yz = 0; yz < 4; ++yz) {
-                    const float wy = (yz & 1) ? Lg.w[1] : 1.0f - Lg.w[1];
-                    const float wz = (yz >> 1) ? Lg.w[2] : 1.0f - Lg.w[2];
-                    const float wyz = wy * wz;
-                    const float c0 = w0 * wyz, c1 = w1 * wyz;
-                    q[yz][0] = valid ? (int)rintf(c0 * a0) : 0;
-                    q[yz][1] = valid ? (int)rintf(c0 * a1) : 0;
-                    q[yz][2] = valid ? (int)rintf(c1 * a0) : 0;
-                    q[yz][3] = valid ? (int)rintf(c1 * a1) : 0;
+                    for (int yz = 0; yz < 4; ++yz) {
+                        const uint32_t gy = Lg.g[1] + (yz & 1), gz = Lg.g[2] + (yz >> 1);
+                        key[yz] = (int)corner_index(D, l, Lg.g[0], gy, gz);
+                        key1[yz] = (int)corner_index(D, l, Lg.g[0] + 1, gy, gz);
+                    }
                 }
-            }
-            // runs: consecutive samples in one cell (row 0's key identifies the cell)
-            const int cell = valid ? key[0] : -1;
-            const int cp = __builtin_amdgcn_update_dpp(-2, cell, 0x138, 0xF, 0xF, false);  // wave_shr:1
-            const int cn = __builtin_amdgcn_update_dpp(-2, cell, 0x130, 0xF, 0xF, false);  // wave_shl:1
-            const bool head = valid && (lane == 0 || cp != cell);
-            const bool tail = valid && (lane == 63 || cn != cell);
-            // inclusive prefix sums over the wave (wraparound int32: differences are exact)
-            int P[4][4];
+                // the 16 contributions, each rounded once to the fixed-point unit
+                int q[4][4];
+                {
+                    const float a0 = g0 * fs, a1 = g1 * fs;
+                    const float w1 = Lg.w[0], w0 = 1.0f - Lg.w[0];
 #pragma unroll
-            for (int yz = 0; yz < 4; ++yz)
+                    for (int yz = 0; yz < 4; ++yz) {
+                        const float wy = (yz & 1) ? Lg.w[1] : 1.0f - Lg.w[1];
+                        const float wz = (yz >> 1) ? Lg.w[2] : 1.0f - Lg.w[2];
+                        const float wyz = wy * wz;
+                        const float c0 = w0 * wyz, c1 = w1 * wyz;
+                        q[yz][0] = valid ? (int)rintf(c0 * a0) : 0;
+                        q[yz][1] = valid ? (int)rintf(c0 * a1) : 0;
+                        q[yz][2] = valid ? (int)rintf(c1 * a0) : 0;
+                        q[yz][3] = valid ? (int)rintf(c1 * a1) : 0;
+                    }
+                }
+                // runs: consecutive samples in one cell (row 0's key identifies the cell)
+                const int cell = valid ? key[0] : -1;
+                // the run left open by the previous chunk: lane 0 continues it (its sums join lane
+                // 0's values before the scan), or it is flushed as one more list entry
+                const bool carried = con[wv][l] != 0;
+                const bool cont = carried && lane == 0 && cell == ckey[wv][l][0].x;
+                if (cont) {
 #pragma unroll
-                for (int c = 0; c < 4; ++c) P[yz][c] = q[yz][c];
+                    for (int yz = 0; yz < 4; ++yz) {
+                        const int4 c = csum[wv][l][yz];
+                        q[yz][0] += c.x; q[yz][1] += c.y; q[yz][2] += c.z; q[yz][3] += c.w;
+                    }
+                }
+                const bool flush = carried && !__shfl(cont ? 1 : 0, 0, 64);
+                const int cp = __builtin_amdgcn_update_dpp(-2, cell, 0x138, 0xF, 0xF, false);  // wave_shr:1
+                const int cn = __builtin_amdgcn_update_dpp(-2, cell, 0x130, 0xF, 0xF, false);  // wave_shl:1
+                const bool head = valid && (lane == 0 || cp != cell);
+                const bool tail = valid && (lane == 63 || cn != cell);
+                // inclusive prefix sums over the wave (wraparound int32: differences are exact)
+                int P[4][4];
+#pragma unroll
+                for (int yz = 0; yz < 4; ++yz)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) P[yz][c] = q[yz][c];
 #define MFN_PSTEP(CTRL, RM)                                                                   \
     _Pragma("unroll") for (int yz = 0; yz < 4; ++yz)                                          \
         _Pragma("unroll") for (int c = 0; c < 4; ++c) P[yz][c] += dppz_i<CTRL, RM>(P[yz][c]);
-#if MFN_DENSE_SHFL  // experiment: the scan by lane shuffles
-#pragma unroll
-            for (int dd = 1; dd < 64; dd <<= 1)
-#pragma unroll
-                for (int yz = 0; yz < 4; ++yz)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        const int u = __shfl_up(P[yz][c], dd, 64);
-                        if (lane >= dd) P[yz][c] += u;
-                    }
-#else
-            MFN_PSTEP(0x111, 0xF) MFN_PSTEP(0x112, 0xF) MFN_PSTEP(0x114, 0xF) MFN_PSTEP(0x118, 0xF)
-            MFN_PSTEP(0x142, 0xA) MFN_PSTEP(0x143, 0xC)
-#endif
+                MFN_PSTEP(0x111, 0xF) MFN_PSTEP(0x112, 0xF) MFN_PSTEP(0x114, 0xF) MFN_PSTEP(0x118, 0xF)
+                MFN_PSTEP(0x142, 0xA) MFN_PSTEP(0x143, 0xC)
 #undef MFN_PSTEP
-            // run index of each lane = heads at or before it - 1; heads write the exclusive prefix,
-            // tails the inclusive one and the keys
-            const uint64_t hb = __ballot(head);
-            const int nruns = __popcll(hb);
-            const int run = __builtin_amdgcn_mbcnt_hi((uint32_t)(hb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u)) +
-                            (head ? 0 : -1);
-            if (head) {
+                // run index of each lane = heads at or before it - 1; heads write the exclusive prefix,
+                // tails the inclusive one and the keys
+                const uint64_t hb = __ballot(head);
+                const int nruns = __popcll(hb);
+                const int run = __builtin_amdgcn_mbcnt_hi((uint32_t)(hb >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u)) + (head ? 0 : -1);
+                if (head) {
 #pragma unroll
-                for (int yz = 0; yz < 4; ++yz)
-                    lhead[wv][run][yz] = make_int4(P[yz][0] - q[yz][0], P[yz][1] - q[yz][1], P[yz][2] - q[yz][2],
-                                                   P[yz][3] - q[yz][3]);
-            }
-            if (tail) {
-#pragma unroll
-                for (int yz = 0; yz < 4; ++yz) {
-                    ltail[wv][run][yz] = make_int4(P[yz][0], P[yz][1], P[yz][2], P[yz][3]);
-                    lkey[wv][run][yz] = make_int2(key[yz], key1[yz]);
+                    for (int yz = 0; yz < 4; ++yz)
+                        lhead[wv][run][yz] = make_int4(P[yz][0] - q[yz][0], P[yz][1] - q[yz][1],
+                                                       P[yz][2] - q[yz][2], P[yz][3] - q[yz][3]);
                 }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            long long* gt = reinterpret_cast<long long*>(priv) +
-                            ((w & (GRAD_COPIES - 1)) * dense_entries + (int64_t)D.offset[l]);
-            // issue: 8 lanes per run = (row, x-corner); both features packed in one 64-bit add
-            for (int b = 0; b < nruns; b += 8) {
-                const int r = b + (lane >> 3), yz = (lane >> 1) & 3, c = lane & 1;
-                if (r < nruns) {
-                    const int4 t = ltail[wv][r][yz], h = lhead[wv][r][yz];
-                    const int f0 = c ? t.z - h.z : t.x - h.x, f1 = c ? t.w - h.w : t.y - h.y;
-                    const int2 kp = lkey[wv][r][yz];
-                    const int kk = c ? kp.y : kp.x;
-                    const long long pq = (long long)((uint64_t)(uint32_t)f1 << 32) + (long long)f0;
+                if (tail) {
+#pragma unroll
+                    for (int yz = 0; yz < 4; ++yz) {
+                        ltail[wv][run][yz] = make_int4(P[yz][0], P[yz][1], P[yz][2], P[yz][3]);
+                        lkey[wv][run][yz] = make_int2(key[yz], key1[yz]);
+                    }
+                }
+                if (flush && lane < 4) {  // the carried run as entry nruns
+                    ltail[wv][nruns][lane] = csum[wv][l][lane];
+                    lhead[wv][nruns][lane] = make_int4(0, 0, 0, 0);
+                    lkey[wv][nruns][lane] = ckey[wv][l][lane];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                int nl = nruns + (flush ? 1 : 0);
+                // the run at lane 63 stays open when the window's next chunk follows: carried, and the
+                // list's last entry moves into its place
+                con[wv][l] = 0;
+                if (more && nruns > 0 && __shfl(tail ? 1 : 0, 63, 64)) {
+                    const int r = nruns - 1;
+                    if (lane < 4) {
+                        const int4 t = ltail[wv][r][lane], h = lhead[wv][r][lane];
+                        csum[wv][l][lane] = make_int4(t.x - h.x, t.y - h.y, t.z - h.z, t.w - h.w);
+                        ckey[wv][l][lane] = lkey[wv][r][lane];
+                        if (nl - 1 != r) {  // move the flushed entry into slot r
+                            ltail[wv][r][lane] = ltail[wv][nl - 1][lane];
+                            lhead[wv][r][lane] = lhead[wv][nl - 1][lane];
+                            lkey[wv][r][lane] = lkey[wv][nl - 1][lane];
+                        }
+                    }
+                    con[wv][l] = 1;
+                    nl -= 1;
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                }
+                long long* gt = reinterpret_cast<long long*>(priv) +
+                                ((w & (GRAD_COPIES - 1)) * dense_entries + (int64_t)D.offset[l]);
+                // issue: 8 lanes per run = (row, x-corner); both features packed in one 64-bit add
+                for (int b = 0; b < nl; b += 8) {
+                    const int r = b + (lane >> 3), yz = (lane >> 1) & 3, c = lane & 1;
+                    if (r < nl) {
+                        const int4 t = ltail[wv][r][yz], h = lhead[wv][r][yz];
+                        const int f0 = c ? t.z - h.z : t.x - h.x, f1 = c ? t.w - h.w : t.y - h.y;
+                        const int2 kp = lkey[wv][r][yz];
+                        const int kk = c ? kp.y : kp.x;
+                        const long long pq = (long long)((uint64_t)(uint32_t)f1 << 32) + (long long)f0;
 #if MFN_DENSE_ABLATE == 1
-                    if (pq == 0x7fffffffffffll)
+                        if (pq == 0x7fffffffffffll)
 #else
-                    if (pq != 0)
+                        if (pq != 0)
 #endif
-                        __hip_atomic_fetch_add(gt + kk, pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_fetch_add(gt + kk, pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
                 }
+                __builtin_amdgcn_wave_barrier();  // the list is rewritten by the next level
             }
-            __builtin_amdgcn_wave_barrier();  // the list is rewritten by the next level
+            if (more) {
+                in = nx;
+#pragma unroll
+                for (int j = 0; j < NG; ++j) gq[j] = gn[j];
+            }
         }
     }
 }
@@ -1704,7 +1754,7 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
     }
     if ((parts & 1) && l_first > 0 && dense_mode && l_first <= n_dense_levels) {
         // levels [0, l_first) all dense: one sample per lane, packed 64-bit adds into the copies
-        const int64_t wb = div_up<int64_t>(n, (int64_t)64 * (ENC_BLOCK / 64));
+        const int64_t wb = div_up<int64_t>(n, (int64_t)64 * DENSE_WIN * (ENC_BLOCK / 64));
         auto dk = l_first <= 8 ? grid_bw_dense_kernel<4> : l_first <= 16 ? grid_bw_dense_kernel<8> : grid_bw_dense_kernel<16>;
         hipLaunchKernelGGL(dk, dim3((unsigned)(wb < cap ? wb : cap)), dim3(ENC_BLOCK), 0, stream,
                            x, n, n_dev, x_min, x_range, *desc, dL_dout, W.priv, dense_entries_of(desc), level_l1,
