@@ -232,10 +232,28 @@ int mfnerf_grid_encode_bw_finish(const mfnerf_grid_desc* desc, float* grad_table
  * Bit-reproducible.  Replaces tcnn's hash-grid backward scatter (networks.py:36-49 encoding, half2
  * atomics there). */
 int64_t mfnerf_grid_encode_bw_binned_workspace(const mfnerf_grid_desc* desc, int64_t n_max);
+/* Adam arguments for the fused partitioned accumulate (mfnerf_grid_encode_bw_binned_adam). */
+typedef struct {
+    float* params;            /* the flat f32 master parameters, Adam m and v, and the f16 mirror */
+    float* m;
+    float* v;
+    void* p16;
+    int64_t table_offset;     /* index of the grid table's first value in those vectors */
+    float lr, beta1, beta2, eps;
+    const int32_t* step_dev;  /* as mfnerf_adam_step_fixed */
+    const float* lr_dev;
+    const mfnerf_amp_state* amp;
+} mfnerf_adam_fused;
 int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                                  const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
                                  void* workspace, int64_t n_slots, const float* level_l1, int parts,
                                  mfnerf_stream_t stream);
+/* mfnerf_grid_encode_bw_binned (parts = 3) with the partitioned tables' Adam step fused into the
+ * accumulate (adam: see mfnerf_adam_step_fixed_partial). */
+int mfnerf_grid_encode_bw_binned_adam(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                                      const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
+                                      void* workspace, int64_t n_slots, const float* level_l1,
+                                      const mfnerf_adam_fused* adam, mfnerf_stream_t stream);
 
 /* out[l] += sum over rows i < n (or *n_dev) of |dL_dout[i][2l]| + |dL_dout[i][2l+1]| (f32). */
 int mfnerf_grid_level_l1(const float* dL_dout, int64_t n, const int32_t* n_dev, int n_levels, float* out,
@@ -411,6 +429,23 @@ int mfnerf_adam_step_fixed(float* params, float* grads, float* m, float* v, void
                            int64_t table_offset, const mfnerf_grid_desc* desc, void* workspace,
                            float* level_l1, float lr, float beta1, float beta2, float eps,
                            int32_t* step_dev, const float* lr_dev, mfnerf_amp_state* amp, mfnerf_stream_t stream);
+
+/* The collective-free step's optimizer split in two (mfnerf_grid_encode_bw_binned_adam +
+ * mfnerf_adam_step_fixed_partial): the partitioned accumulate applies Adam to the partitioned
+ * tables' parameters itself, from each entry's finished int32 sum, and never writes their gradient
+ * words; the remaining pass updates [0, fused_from) only -- unless *fused_ovf is set (a record slot
+ * overflowed, the fallback scattered those levels into the gradient words), then everything, as
+ * mfnerf_adam_step_fixed does.  Same arithmetic, same bits as the unsplit pair. */
+
+int mfnerf_adam_step_fixed_partial(float* params, float* grads, float* m, float* v, void* p_f16, int64_t n,
+                                   int64_t table_offset, const mfnerf_grid_desc* desc, void* workspace,
+                                   float* level_l1, float lr, float beta1, float beta2, float eps,
+                                   int32_t* step_dev, const float* lr_dev, mfnerf_amp_state* amp, int64_t fused_from,
+                                   const int32_t* fused_ovf, mfnerf_stream_t stream);
+/* value index (within the table) where the partitioned tables start, or -1 (nothing partitioned) */
+int64_t mfnerf_grid_binned_first_value(const mfnerf_grid_desc* desc);
+/* byte offset of the slot-overflow word inside the binned workspace sized for n_slots */
+int64_t mfnerf_grid_encode_bw_binned_flag_offset(const mfnerf_grid_desc* desc, int64_t n_slots);
 
 /* status[0] (device i32) = 1 if any of x (n f32, 16-byte aligned) is inf/nan, else 0 (a full scan;
  * the training step gets the same flag from mfnerf_field_bw's nonfinite argument instead). */

@@ -120,7 +120,9 @@ extern "C" int mfnerf_adam_step(float* params, float* grads, float* m, float* v,
     if (!step_dev && step < 1) { mfn_set_error("adam_step: step must be >= 1"); return MFN_ERR_INVALID; }
     const int threads = 256;
     const int64_t want = mfn::div_up<int64_t>(mfn::div_up<int64_t>(n, 4), threads);
-    const unsigned blocks = (unsigned)(want < 4096 ? (want < 1 ? 1 : want) : 4096);
+    // 1024 workgroups at most: each takes the last-workgroup ticket (one serialised memory-side
+    // atomic on one address), grid-stride does the rest at the same bandwidth (grid.hip adam_fixed)
+    const unsigned blocks = (unsigned)(want < 1024 ? (want < 1 ? 1 : want) : 1024);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(threads), 0, stream, params, grads, m, v, (__half*)p_f16, n, lr,
                        beta1, beta2, eps, grad_scale, step, step_dev, lr_dev, amp, zero_grads);
     // with amp the last workgroup did the bookkeeping; without it only the step count remains

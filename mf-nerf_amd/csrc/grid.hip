@@ -735,14 +735,17 @@ __global__ __launch_bounds__(256) void fold_copies_kernel(float* __restrict__ pr
 // copies is exact in int64, and f0 = int32(low word), f1 = int32(high word) + (f0 < 0) undoes the
 // borrow of a negative f0.  Values i .. i+3 (entries i/2, i/2+1); the copies are zeroed.
 __device__ __forceinline__ int4 fold_packed_copies(int* __restrict__ priv, int64_t dense_vals, int64_t i) {
+    // every copy's load issued before the first zeroing store (a load-store pair per copy in turn
+    // made the fold one memory round trip per copy: ~55 us of fixed cost in the optimizer pass)
+    longlong2 c[GRAD_COPIES];
+#pragma unroll
+    for (int k = 0; k < GRAD_COPIES; ++k) c[k] = *reinterpret_cast<const longlong2*>(priv + k * dense_vals + i);
     long long a = 0, b = 0;
 #pragma unroll
     for (int k = 0; k < GRAD_COPIES; ++k) {
-        longlong2* q = reinterpret_cast<longlong2*>(priv + k * dense_vals + i);
-        const longlong2 c = *q;
-        a += c.x;
-        b += c.y;
-        *q = make_longlong2(0, 0);
+        a += c[k].x;
+        b += c[k].y;
+        *reinterpret_cast<longlong2*>(priv + k * dense_vals + i) = make_longlong2(0, 0);
     }
     const int a0 = (int)(uint32_t)(unsigned long long)a, b0 = (int)(uint32_t)(unsigned long long)b;
     return make_int4(a0, (int)(a >> 32) + (a0 < 0), b0, (int)(b >> 32) + (b0 < 0));
@@ -790,8 +793,11 @@ __global__ __launch_bounds__(256) void adam_fixed_kernel(float* __restrict__ p, 
                                                          float* __restrict__ level_l1, float lr, float b1,
                                                          float b2, float eps, int32_t* __restrict__ step_dev,
                                                          const float* __restrict__ lr_dev,
-                                                         mfnerf_amp_state* __restrict__ amp, int n_levels) {
+                                                         mfnerf_amp_state* __restrict__ amp, int n_levels,
+                                                         int64_t fused_from, const int32_t* __restrict__ fused_ovf) {
     __shared__ TableRegions R;
+    // values >= fused_from were updated by the fused partitioned accumulate, unless it overflowed
+    if (fused_ovf && *fused_ovf == 0) n = fused_from;
     R.build(D, level_l1, total_vals);
     const bool skipped = amp && amp->nonfinite;  // GradScaler: no update on a non-finite gradient, only the zeroing
     const int st = *step_dev + 1;
@@ -913,6 +919,7 @@ struct BinPlan {
     int table_of[MFN_MAX_LEVELS];    // per level: its table
     uint32_t t_offset[MFN_MAX_LEVELS], t_size[MFN_MAX_LEVELS];
     int t_bin0[MFN_MAX_LEVELS + 1];  // first bin of each table; t_bin0[n_tables] = n_bins
+    int t_level[MFN_MAX_LEVELS];     // a level of each table (its fixed-point scale)
 };
 
 __device__ __forceinline__ int bin_table(const BinPlan& P, int b) {
@@ -1131,11 +1138,8 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
 #pragma unroll
             for (int q = 0; q < 2; ++q)
                 if (live[q])
-                    staged_records(D, P, S[q], Q[q], fs_s, j, [&](int, int bin, uint3 r) {
-                        if (bin >= 0) {
-                            atomicAdd(&thist[bin - b0], 1);
-                            rmax = max(rmax, max(r.y & 0x7fffffffu, r.z & 0x7fffffffu));  // |float| bits order
-                        }
+                    staged_records(D, P, S[q], Q[q], fs_s, j, [&](int, int bin, uint3) {
+                        if (bin >= 0) atomicAdd(&thist[bin - b0], 1);
                     });
             __syncthreads();
             // bins -> sorted tile offsets (toff); a run's k-th record goes to its slot position gdst + k
@@ -1153,6 +1157,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                 if (live[q])
                     staged_records(D, P, S[q], Q[q], fs_s, j, [&](int, int bin, uint3 r) {
                         if (bin < 0) return;
+                        rmax = max(rmax, max(r.y & 0x7fffffffu, r.z & 0x7fffffffu));  // |float| bits order
                         const int lb = bin - b0;
                         const int p = atomicAdd(&thist[lb], 1);
                         stage[p] = r;
@@ -1305,7 +1310,10 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
                                                                 const int32_t* __restrict__ scnt,
                                                                 const uint32_t* __restrict__ smax,
                                                                 const int32_t* __restrict__ ovf,
-                                                                int* __restrict__ grad, int64_t n_slots) {
+                                                                int* __restrict__ grad, int64_t n_slots,
+                                                                const mfnerf_grid_desc D,
+                                                                const float* __restrict__ level_l1,
+                                                                const mfnerf_adam_fused A) {
     if (*ovf) return;  // a slot overflowed: bin_fallback_kernel scatters the binned levels
 #if MFN_ACC32 == 2
     constexpr int IMG_WORDS = 1;  // per entry
@@ -1376,6 +1384,36 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     int* dst = grad + 2 * ((int64_t)P.t_offset[t] + e_lo);
 #if MFN_ACC32 == 2
     const int rnd = kbits > 0 ? 1 << (kbits - 1) : 0;
+    if (A.params) {
+        // fused optimizer (mfnerf_adam_step_fixed_partial): the entry's finished int32 sums, converted
+        // with the table's scale exactly as adam_fixed_kernel converts them, feed the same Adam update;
+        // the gradient words are left alone (zero)
+        const float sc = table_fixed_scale(D, level_l1, P.t_level[t]);
+        const float is = sc > 0.0f ? 1.0f / sc : 0.0f;
+        if (A.amp && A.amp->nonfinite) return;  // GradScaler skip: no update (gradient words stay zero)
+        const int stp = *A.step_dev + 1;
+        const float lr = A.lr_dev ? *A.lr_dev : A.lr;
+        const float bc1 = 1.0f - powf(A.beta1, (float)stp);
+        const float bc2 = 1.0f - powf(A.beta2, (float)stp);
+        const int64_t base_v = A.table_offset + 2 * ((int64_t)P.t_offset[t] + e_lo);
+        float2* pp = reinterpret_cast<float2*>(A.params + base_v);
+        float2* mm = reinterpret_cast<float2*>(A.m + base_v);
+        float2* vv = reinterpret_cast<float2*>(A.v + base_v);
+        __half2* hh = reinterpret_cast<__half2*>(reinterpret_cast<__half*>(A.p16) + base_v);
+        for (int i = threadIdx.x; i < n_e; i += blockDim.x) {
+            const unsigned long long w = img[i];
+            const int lo = (int)(uint32_t)w, hi = (int)(uint32_t)(w >> 32) + (lo < 0);
+            const float g0 = (float)((lo + rnd) >> kbits) * is, g1 = (float)((hi + rnd) >> kbits) * is;
+            float2 p = pp[i], m = mm[i], v = vv[i];
+            mfn::adam_elem(p.x, m.x, v.x, g0, A.beta1, A.beta2, A.eps, lr, bc1, bc2);
+            mfn::adam_elem(p.y, m.y, v.y, g1, A.beta1, A.beta2, A.eps, lr, bc1, bc2);
+            pp[i] = p;
+            mm[i] = m;
+            vv[i] = v;
+            if (A.p16) hh[i] = __floats2half2_rn(p.x, p.y);
+        }
+        return;
+    }
     for (int i = threadIdx.x; i < n_e; i += blockDim.x) {
         const unsigned long long v = img[i];
         const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32) + (lo < 0);
@@ -1419,6 +1457,7 @@ int bin_plan(const mfnerf_grid_desc* d, BinPlan* P) {
         if (t == P->n_tables) {
             P->t_offset[t] = d->offset[l];
             P->t_size[t] = d->size[l];
+            P->t_level[t] = l;
             P->n_tables++;
             entries += d->size[l];
         }
@@ -1472,6 +1511,11 @@ int first_binned_level(const mfnerf_grid_desc* d) {
     }
     return l0;
 }
+
+int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table, void* workspace,
+                int64_t n_slots, const float* level_l1, int parts, const mfnerf_adam_fused* adam,
+                mfnerf_stream_t stream);
 
 struct BinWorkspace {
     float* priv;
@@ -1595,6 +1639,15 @@ int mfnerf_adam_step_fixed(float* params, float* grads, float* m, float* v, void
                            int64_t table_offset, const mfnerf_grid_desc* desc, void* workspace,
                            float* level_l1, float lr, float beta1, float beta2, float eps,
                            int32_t* step_dev, const float* lr_dev, mfnerf_amp_state* amp, mfnerf_stream_t stream) {
+    return mfnerf_adam_step_fixed_partial(params, grads, m, v, p_f16, n, table_offset, desc, workspace, level_l1, lr,
+                                          beta1, beta2, eps, step_dev, lr_dev, amp, n, nullptr, stream);
+}
+
+int mfnerf_adam_step_fixed_partial(float* params, float* grads, float* m, float* v, void* p_f16, int64_t n,
+                                   int64_t table_offset, const mfnerf_grid_desc* desc, void* workspace,
+                                   float* level_l1, float lr, float beta1, float beta2, float eps,
+                                   int32_t* step_dev, const float* lr_dev, mfnerf_amp_state* amp, int64_t fused_from,
+                                   const int32_t* fused_ovf, mfnerf_stream_t stream) {
     int st = check_desc(desc, "adam_step_fixed");
     if (st) return st;
     if (!params || !grads || !m || !v || !step_dev || !level_l1) {
@@ -1610,15 +1663,28 @@ int mfnerf_adam_step_fixed(float* params, float* grads, float* m, float* v, void
         total = e > total ? e : total;
     }
     const int64_t dense = workspace ? dense_entries_of(desc) : 0;
+    if (fused_from < 0 || fused_from > n || fused_from % 4) {
+        mfn_set_error("adam_step_fixed_partial: fused_from (%lld) must be a multiple of 4 in [0, n]",
+                      (long long)fused_from);
+        return MFN_ERR_INVALID;
+    }
     if (n % 4 || table_offset % 4 || table_offset < 0 || table_offset + total > n) {
         mfn_set_error("adam_step_fixed: n (%lld) and table_offset (%lld) must be multiples of 4 holding the table",
                       (long long)n, (long long)table_offset);
         return MFN_ERR_INVALID;
     }
-    const int64_t want = div_up<int64_t>(n / 4, 256);
-    hipLaunchKernelGGL(adam_fixed_kernel, dim3((unsigned)(want < 4096 ? (want < 1 ? 1 : want) : 4096)), dim3(256), 0,
+    // sized for the range normally updated: every workgroup takes the last-workgroup ticket (one
+    // memory-side atomic on ONE address each, serialised: ~13 ns apiece), so an idle workgroup is
+    // not free (4096 of them cost ~55 us in the fused_from case); grid-stride covers the rest
+    const int64_t want = div_up<int64_t>((fused_ovf ? fused_from : n) / 4, 256);
+#ifndef MFN_ADAM_BLOCKS
+#define MFN_ADAM_BLOCKS 1024  // measured: 4096 -> 1024 workgroups 88 -> 78 us (fewer tickets, same bandwidth)
+#endif
+    hipLaunchKernelGGL(adam_fixed_kernel,
+                       dim3((unsigned)(want < MFN_ADAM_BLOCKS ? (want < 1 ? 1 : want) : MFN_ADAM_BLOCKS)), dim3(256), 0,
                        stream, params, grads, m, v, (__half*)p_f16, n, table_offset, (int*)workspace, 2 * dense,
-                       total, *desc, level_l1, lr, beta1, beta2, eps, step_dev, lr_dev, amp, desc->n_levels);
+                       total, *desc, level_l1, lr, beta1, beta2, eps, step_dev, lr_dev, amp, desc->n_levels,
+                       fused_from, fused_ovf);
     if (!amp)  // else the kernel's last workgroup did it
         hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, amp, level_l1, desc->n_levels);
     return mfn_check_launch("adam_step_fixed");
@@ -1722,6 +1788,44 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
                                  const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
                                  void* workspace, int64_t n_slots, const float* level_l1, int parts,
                                  mfnerf_stream_t stream) {
+    return binned_impl(x, n, n_dev, x_min, x_range, desc, dL_dout, grad_table, workspace, n_slots, level_l1, parts,
+                       nullptr, stream);
+}
+
+int mfnerf_grid_encode_bw_binned_adam(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                                      const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
+                                      void* workspace, int64_t n_slots, const float* level_l1,
+                                      const mfnerf_adam_fused* adam, mfnerf_stream_t stream) {
+    if (!adam || !adam->params || !adam->m || !adam->v || !adam->step_dev ||
+        (((uintptr_t)adam->params | (uintptr_t)adam->m | (uintptr_t)adam->v) & 7) || (adam->table_offset & 1)) {
+        mfn_set_error("grid_encode_bw_binned_adam: bad Adam arguments (null or misaligned vectors, odd table_offset)");
+        return MFN_ERR_INVALID;
+    }
+    return binned_impl(x, n, n_dev, x_min, x_range, desc, dL_dout, grad_table, workspace, n_slots, level_l1, 3,
+                       adam, stream);
+}
+
+int64_t mfnerf_grid_binned_first_value(const mfnerf_grid_desc* desc) {
+    if (check_desc(desc, "grid_binned_first_value")) return -1;
+    BinPlan P;
+    if (bin_plan(desc, &P) <= 0) return -1;
+    return 2 * (int64_t)P.t_offset[0];
+}
+
+int64_t mfnerf_grid_encode_bw_binned_flag_offset(const mfnerf_grid_desc* desc, int64_t n_slots) {
+    if (check_desc(desc, "grid_encode_bw_binned_flag_offset") || n_slots <= 0) return -1;
+    BinWorkspace W;
+    if (binned_workspace_layout(desc, n_slots, nullptr, &W) < 0) return -1;
+    return (int64_t)reinterpret_cast<uintptr_t>(W.ovf);
+}
+
+}  // extern "C"
+
+namespace {
+int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table, void* workspace,
+                int64_t n_slots, const float* level_l1, int parts, const mfnerf_adam_fused* adam,
+                mfnerf_stream_t stream) {
     int st = check_desc(desc, "grid_encode_bw_binned");
     if (st) return st;
     if (n_slots <= 0 || n_slots > n) n_slots = n;
@@ -1772,8 +1876,10 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
         auto sk = P.n_binned <= 8 ? bin_scatter_kernel<8> : bin_scatter_kernel<MAX_BINNED>;
         hipLaunchKernelGGL(sk, dim3(UNITS), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
                            *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.smax, W.ovf, n_slots);
+        mfnerf_adam_fused A{};
+        if (adam) A = *adam;
         hipLaunchKernelGGL(bin_accum_kernel, dim3(P.n_bins), dim3(ACC_THREADS), 0, stream, P, n, n_dev, W.rec,
-                           W.scnt, W.smax, W.ovf, (int*)grad_table, n_slots);
+                           W.scnt, W.smax, W.ovf, (int*)grad_table, n_slots, *desc, level_l1, A);
         // levels [l_first, L) by atomics, only when a slot overflowed (exits at once otherwise)
         auto fb = big ? bin_fallback_kernel<MFN_MAX_LEVELS> : bin_fallback_kernel<16>;
         hipLaunchKernelGGL(fb, dim3(256), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc, dL_dout,
@@ -1781,5 +1887,4 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
     }
     return mfn_check_launch("grid_encode_bw_binned");
 }
-
-}  // extern "C"
+}  // namespace

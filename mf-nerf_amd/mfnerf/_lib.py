@@ -35,6 +35,16 @@ class GridDesc(ctypes.Structure):
     ]
 
 
+class AdamFused(ctypes.Structure):
+    """mfnerf_adam_fused (include/mfnerf.h)."""
+    _fields_ = [
+        ("params", ctypes.c_void_p), ("m", ctypes.c_void_p), ("v", ctypes.c_void_p), ("p16", ctypes.c_void_p),
+        ("table_offset", ctypes.c_int64),
+        ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float),
+        ("step_dev", ctypes.c_void_p), ("lr_dev", ctypes.c_void_p), ("amp", ctypes.c_void_p),
+    ]
+
+
 # name -> (restype, argtypes); mirrors include/mfnerf.h one to one
 SIGNATURES = {
     "mfnerf_last_error": (ctypes.c_char_p, []),
@@ -65,6 +75,10 @@ SIGNATURES = {
     "mfnerf_grid_encode_bw_binned_workspace": (_I64, [ctypes.POINTER(GridDesc), _I64]),
     "mfnerf_grid_encode_bw_binned": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _I64, _P, _I,
                                           _P]),
+    "mfnerf_grid_encode_bw_binned_adam": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _I64,
+                                              _P, ctypes.POINTER(AdamFused), _P]),
+    "mfnerf_grid_binned_first_value": (_I64, [ctypes.POINTER(GridDesc)]),
+    "mfnerf_grid_encode_bw_binned_flag_offset": (_I64, [ctypes.POINTER(GridDesc), _I64]),
     "mfnerf_grid_level_l1": (_I, [_P, _I64, _P, _I, _P, _P]),
     "mfnerf_debug_grid_bw_half": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _F, _P]),
     "mfnerf_debug_grid_bw_ablate": (_I, [_I, _P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P]),
@@ -84,6 +98,8 @@ SIGNATURES = {
                                      _P]),
     "mfnerf_adam_step": (_I, [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _I, _P]),
     "mfnerf_adam_step_fixed": (_I, [_P, _P, _P, _P, _P, _I64, _I64, ctypes.POINTER(GridDesc), _P, _P, _F, _F, _F, _F, _P, _P, _P, _P]),
+    "mfnerf_adam_step_fixed_partial": (_I, [_P, _P, _P, _P, _P, _I64, _I64, ctypes.POINTER(GridDesc), _P, _P, _F, _F, _F,
+                                            _F, _P, _P, _P, _I64, _P, _P]),
     "mfnerf_field_bw_reduce": (_I, [_I, _P, _P, _P, _P, _P]),
     "mfnerf_mlp_n_params": (_I64, [_I, _I, _I, _I]),
     "mfnerf_mlp_packed_bytes": (_I64, [_I, _I, _I, _I]),

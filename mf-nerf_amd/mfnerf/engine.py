@@ -19,6 +19,7 @@ so Adam is one launch and the gradient zeroing one memset; an fp16 mirror of the
 refreshed by the same Adam pass and is what the grid kernels gather from.
 Multi-GPU: run/replay(exchange=dp.allreduce_mean_) all-reduces `grads` between backward and Adam.
 """
+import ctypes
 import math
 import os
 from dataclasses import dataclass
@@ -27,7 +28,7 @@ import numpy as np
 import torch
 
 from . import synthetic
-from ._lib import call, load, ptr, stream
+from ._lib import AdamFused, call, load, ptr, stream
 from .field import XYZ_NET_PARAMS, rgb_net_params
 from .grid import GridLayout
 
@@ -444,9 +445,30 @@ class TrainStep:
         """Samples per part the binned scatter's record slots are sized for."""
         return min(self.cap_p, self.Np * max(1, self.cfg.bin_samples_per_ray))
 
-    def _grid_bw(self, mb, q):
-        """Part q's hash-table gradient scatter (the dominant kernel, alone so it can be timed)."""
+    def _fused_adam_ok(self):
+        """The collective-free replayed tail can run the partitioned tables' Adam inside the scatter's
+        accumulate (mfnerf_grid_encode_bw_binned_adam + mfnerf_adam_step_fixed_partial)."""
+        return (self._binned() and self.shard is None and os.environ.get("MFNERF_FUSED_ADAM", "1") == "1"
+                and load().mfnerf_grid_binned_first_value(self.desc) >= 0)
+
+    def _adam_fused_args(self):
+        c = self.cfg
+        amp = self._amp_ptr()
+        return AdamFused(params=self.params.data_ptr(), m=self.m.data_ptr(), v=self.v.data_ptr(),
+                         p16=self.p16.data_ptr(), table_offset=self.off_table, lr=float(c.lr), beta1=0.9,
+                         beta2=0.999, eps=float(c.eps), step_dev=self.step_dev.data_ptr(),
+                         lr_dev=self.lr_dev.data_ptr(), amp=amp.value if amp is not None else None)
+
+    def _grid_bw(self, mb, q, fuse_adam=False):
+        """Part q's hash-table gradient scatter (the dominant kernel, alone so it can be timed);
+        fuse_adam: with the partitioned tables' Adam step (then _finish_update(partial=True))."""
         t, m = self.parts[q], mb.part[q]
+        if self._binned() and fuse_adam:
+            self._fused_args = self._adam_fused_args()  # kept alive: graphs capture the call
+            call("mfnerf_grid_encode_bw_binned_adam", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min,
+                 self.x_range, self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws),
+                 self._bin_slots(), ptr(self._level_l1), ctypes.byref(self._fused_args), stream())
+            return
         if self._binned():
             # both parts in sequence on this stream: the coarse levels' atomics, then the fine levels'
             # partitioned sums (the two on separate streams inside the graphs measured 1.32 vs
@@ -479,14 +501,24 @@ class TrainStep:
              hi - lo, float(c.lr), 0.9, 0.999, c.eps, 1.0, 0, ptr(self.step_dev), ptr(self.lr_dev),
              self._amp_ptr(), int(zero_grads), stream())
 
-    def _finish_update(self):
+    def _finish_update(self, partial=False):
         """Unsharded, no exchange, fixed-point table gradient: the finish (convert) and Adam in one
-        pass (mfnerf_adam_step_fixed), then the MLP weight repack."""
+        pass (mfnerf_adam_step_fixed), then the MLP weight repack.  partial: after a fused
+        _grid_bw, only the values before the partitioned tables (all of them if a slot overflowed)."""
         c = self.cfg
-        call("mfnerf_adam_step_fixed", ptr(self.params), ptr(self.grads), ptr(self.m), ptr(self.v), ptr(self.p16),
-             self.n_alloc, self.off_table, self.desc, ptr(self.parts[0].grid_ws), ptr(self._level_l1),
-             float(c.lr), 0.9, 0.999, c.eps, ptr(self.step_dev), ptr(self.lr_dev),
-             self._amp_ptr(), stream())
+        if partial:
+            ws = self.parts[0].grid_ws
+            ovf = ctypes.c_void_p(ws.data_ptr() + load().mfnerf_grid_encode_bw_binned_flag_offset(
+                self.desc, self._bin_slots()))
+            call("mfnerf_adam_step_fixed_partial", ptr(self.params), ptr(self.grads), ptr(self.m), ptr(self.v),
+                 ptr(self.p16), self.n_alloc, self.off_table, self.desc, ptr(ws), ptr(self._level_l1),
+                 float(c.lr), 0.9, 0.999, c.eps, ptr(self.step_dev), ptr(self.lr_dev), self._amp_ptr(),
+                 self.off_table + load().mfnerf_grid_binned_first_value(self.desc), ovf, stream())
+        else:
+            call("mfnerf_adam_step_fixed", ptr(self.params), ptr(self.grads), ptr(self.m), ptr(self.v),
+                 ptr(self.p16), self.n_alloc, self.off_table, self.desc, ptr(self.parts[0].grid_ws),
+                 ptr(self._level_l1), float(c.lr), 0.9, 0.999, c.eps, ptr(self.step_dev), ptr(self.lr_dev),
+                 self._amp_ptr(), stream())
         self._pack()
 
     def _update(self):
@@ -629,8 +661,13 @@ class TrainStep:
                 tail = self._finish_update if self._fixed() else lambda: (self._grid_finish(0), self._update())
                 self.graphs["finish_update"] = cap(tail)
                 # and the scatter with it (one graph transition less again) for untimed steps
-                self.graphs["grid_bw_tail"] = [cap(lambda j=j: (self._grid_bw(self.mbuf[j], 0), tail()))
-                                               for j in range(2)]
+                if self._fixed() and self._fused_adam_ok():  # the tables' Adam inside the accumulate
+                    self.graphs["grid_bw_tail"] = [
+                        cap(lambda j=j: (self._grid_bw(self.mbuf[j], 0, fuse_adam=True),
+                                         self._finish_update(partial=True))) for j in range(2)]
+                else:
+                    self.graphs["grid_bw_tail"] = [cap(lambda j=j: (self._grid_bw(self.mbuf[j], 0), tail()))
+                                                   for j in range(2)]
         torch.cuda.synchronize()
         # the next step's march runs beside this step's grid_bw scatter, whose 4096 workgroups would
         # otherwise take every dispatch slot first (the march's small kernels then finish after the

@@ -7,6 +7,7 @@ import pytest
 import torch
 
 from mfnerf import engine, synthetic
+from mfnerf._lib import load
 
 pytestmark = pytest.mark.gpu
 
@@ -185,4 +186,46 @@ def test_fused_convert_adam_matches_finish_then_adam(gpu, kw, skip):
     if skip:
         assert torch.equal(st.params, snap["params"]) and int(st.finite_status[1]) == int(snap["finite_status"][1]) + 1
     else:
+        assert not torch.equal(st.params, snap["params"])
+
+
+@pytest.mark.parametrize("kw", [{}, {"grid": "MixedFeature", "N_tables": 8, "rgb_width": 128}],
+                         ids=["hash-rgb64", "mixedfeature-rgb128"])
+@pytest.mark.parametrize("skip", [False, True])
+def test_partitioned_accumulate_with_fused_adam_matches_unfused(gpu, kw, skip):
+    """The replayed tail with the partitioned tables' Adam fused into the accumulate
+    (mfnerf_grid_encode_bw_binned_adam + mfnerf_adam_step_fixed_partial) == the scatter followed by
+    the one-pass convert + Adam (mfnerf_adam_step_fixed), bit for bit: params, m, v, the fp16 mirror,
+    the step counter, the zeroed gradient words, copies and level_l1 -- also on a skipped step."""
+    st = _make(gpu, 1, **kw)
+    assert st._fused_adam_ok()
+    batches = st.make_batches(2, seed=5)
+    st.run(batches[0])  # m, v non-zero
+    mb, nomark = st.mbuf[0], (lambda name: None)
+    st._use(mb)
+    st._march(batches[1], mb, nomark)
+    st._chain(batches[1], mb, 0, nomark)
+    if skip:
+        st.finite_status[0] = 1
+    torch.cuda.synchronize()
+    names = ("params", "grads", "m", "v", "p16", "step_dev", "finite_status", "_level_l1")
+    snap = {k: getattr(st, k).clone() for k in names}
+    ws = st.parts[0].grid_ws
+    snap_ws = ws.clone()
+    st._grid_bw(mb, 0)
+    st._finish_update()
+    torch.cuda.synchronize()
+    ref = {k: getattr(st, k).clone() for k in names}
+    ref_ws = ws.clone()
+    for k in names:
+        getattr(st, k).copy_(snap[k])
+    ws.copy_(snap_ws)
+    st._grid_bw(mb, 0, fuse_adam=True)
+    st._finish_update(partial=True)
+    torch.cuda.synchronize()
+    for k in names:
+        assert torch.equal(getattr(st, k), ref[k]), k
+    nc = load().mfnerf_grid_encode_bw_workspace(st.desc) // 4  # the private copies: zeroed by both
+    assert not bool(ws[:nc].any()) and not bool(ref_ws[:nc].any()) and not bool(st.grads.any())
+    if not skip:
         assert not torch.equal(st.params, snap["params"])

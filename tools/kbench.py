@@ -80,6 +80,8 @@ def main():
         "check": lambda: call("mfnerf_check_finite", ptr(step.grads), step.grads.numel(), ptr(step.finite_status), s()),
         "adam": lambda: step._adam(step.grads, 0, step.n_alloc, False),
         "adam_fixed": step._finish_update,  # fused convert + Adam + repack (state changes: timing only)
+        "grid_bw_fused": lambda: step._grid_bw(mb, 0, fuse_adam=True),  # + the partitioned tables' Adam
+        "adam_partial": lambda: step._finish_update(partial=True),
         "pack": step._pack,
         "march": lambda: step._march(batch, mb, lambda _n: None),
     }
