@@ -458,6 +458,14 @@ int mfnerf_check_finite(const float* x, int64_t n, int32_t* status, mfnerf_strea
 int mfnerf_flag_to_shards(float* grads, int64_t world, int64_t shard_len, const int32_t* flag, mfnerf_stream_t stream);
 int mfnerf_flag_from_shard(const float* g_shard, int32_t* flag, mfnerf_stream_t stream);
 
+/* A soft gate between two streams' captured graphs (no reference counterpart: it replaces the host
+ * event the reference's PyTorch loop never needed, train.py:129-150 running one stream).  gate =
+ * device int32[2], zeroed once.  mfnerf_gate_signal adds a signal; mfnerf_gate_wait (one thread)
+ * waits for the signal matching its own ticket, at most timeout_us, then absorbs signals nobody
+ * waited for.  Ordering only: data hazards must still be covered by stream events. */
+int mfnerf_gate_signal(int32_t* gate, mfnerf_stream_t stream);
+int mfnerf_gate_wait(int32_t* gate, int64_t timeout_us, mfnerf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

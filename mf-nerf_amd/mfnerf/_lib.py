@@ -110,6 +110,8 @@ SIGNATURES = {
     "mfnerf_check_finite": (_I, [_P, _I64, _P, _P]),
     "mfnerf_flag_to_shards": (_I, [_P, _I64, _I64, _P, _P]),
     "mfnerf_flag_from_shard": (_I, [_P, _P, _P]),
+    "mfnerf_gate_signal": (_I, [_P, _P]),
+    "mfnerf_gate_wait": (_I, [_P, _I64, _P]),
 }
 
 _lib = None

@@ -33,6 +33,7 @@ from .field import XYZ_NET_PARAMS, rgb_net_params
 from .grid import GridLayout
 
 MAX_SAMPLES = 1024
+GATE_TIMEOUT_US = 2000  # a gated march starts anyway after this long (gate.hip)
 NEAR_DISTANCE = 0.01
 SQRT3 = 3 ** 0.5
 
@@ -451,6 +452,10 @@ class TrainStep:
         return (self._binned() and self.shard is None and os.environ.get("MFNERF_FUSED_ADAM", "1") == "1"
                 and load().mfnerf_grid_binned_first_value(self.desc) >= 0)
 
+    def _gated_ok(self):
+        """The collective-free single-part step can be one graph with a device-gated side march."""
+        return self.n_parts == 1 and self.shard is None and os.environ.get("MFNERF_GATED_MARCH", "1") == "1"
+
     def _adam_fused_args(self):
         c = self.cfg
         amp = self._amp_ptr()
@@ -668,6 +673,27 @@ class TrainStep:
                 else:
                     self.graphs["grid_bw_tail"] = [cap(lambda j=j: (self._grid_bw(self.mbuf[j], 0), tail()))
                                                    for j in range(2)]
+                if self._gated_ok():
+                    # the whole step as ONE graph: the chain signals a device gate where the host
+                    # used to record the event that starts the next march (gate.hip); the side
+                    # stream's march graph begins by waiting on that gate
+                    self._gate = torch.zeros(2, dtype=torch.int32, device=self.dev)
+                    gp = ptr(self._gate)
+                    fuse = self._fixed() and self._fused_adam_ok()
+
+                    def step(j):
+                        self._chain(self._static[j], self.mbuf[j], 0, nomark)
+                        call("mfnerf_gate_signal", gp, stream())
+                        if fuse:
+                            self._grid_bw(self.mbuf[j], 0, fuse_adam=True)
+                            self._finish_update(partial=True)
+                        else:
+                            self._grid_bw(self.mbuf[j], 0)
+                            tail()
+                    self.graphs["step"] = [cap(lambda j=j: step(j)) for j in range(2)]
+                    self.graphs["march_gated"] = [
+                        cap(lambda j=j: (call("mfnerf_gate_wait", gp, GATE_TIMEOUT_US, stream()), march(j)),
+                            rng=True) for j in range(2)]
         torch.cuda.synchronize()
         # the next step's march runs beside this step's grid_bw scatter, whose 4096 workgroups would
         # otherwise take every dispatch slot first (the march's small kernels then finish after the
@@ -692,14 +718,15 @@ class TrainStep:
             for d, s_ in zip((dst.rays_o, dst.rays_d, dst.rgb), (batch.rays_o, batch.rays_d, batch.rgb)):
                 d.copy_(s_)
 
-    def _march_on_side(self, j, batch, after):
+    def _march_on_side(self, j, batch, after, gated=False):
         """Copy batch into static set j and march it on the side stream once `after` (an event on
-        the main stream) has passed: set j's buffers were last read two steps back."""
+        the main stream) has passed: set j's buffers were last read two steps back.  gated: the
+        march graph first waits for the step graph's gate signal (placement only)."""
         self._side.wait_event(after)
         with torch.cuda.stream(self._side):
             if batch is not None:
                 self._stage_batch(j, batch)
-            self.graphs["march"][j].replay()
+            self.graphs["march_gated" if gated else "march"][j].replay()
             self._ev_march[j].record(self._side)
 
     def replay(self, batch: Batch = None, exchange=None, grid_bw_events=None, next_batch=None, prefetch=None):
@@ -724,6 +751,18 @@ class TrainStep:
         self._ev_start.record(main)
         if not self._primed:
             self._march_on_side(j, batch, self._ev_start)
+        if fuse_tail and grid_bw_events is None and g.get("step") is not None and prefetch and not self.march_early:
+            # one graph for the step; the next march (side stream) starts when its gate sees the
+            # chain's signal -- set 1-j was last read by the previous step, all before _ev_start
+            main.wait_event(self._ev_march[j])
+            self._use(self.mbuf[j])
+            self.last_batch = self._static[j]
+            self.adam_step += 1
+            g["step"][j].replay()
+            self._march_on_side(1 - j, next_batch, self._ev_start, gated=True)
+            self._parity = 1 - j
+            self._primed = True
+            return
         early = prefetch and self.march_early
         if early:  # set 1-j was last read by the previous step, all of which precedes _ev_start
             self._march_on_side(1 - j, next_batch, self._ev_start)

@@ -44,9 +44,33 @@ def test_timed_and_fused_tail_replays_match_eager(gpu):
             torch.cuda.synchronize()
             assert ev[0].elapsed_time(ev[1][0]) > 0
     torch.cuda.synchronize()
+    # steps 1, 2, 4, 5 ran as one graph with a gated march (gate.hip); every signal was waited for
+    assert a.graphs.get("step") is not None and a._gate.tolist() == [4, 4]
     assert a.adam_step == b.adam_step
     assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
     assert torch.equal(a.p16, b.p16) and int(a.step_dev) == int(b.step_dev)
+
+
+def test_gate_waits_times_out_and_absorbs_unwaited_signals(gpu):
+    """gate.hip: a wait with no signal gives up after its timeout; a wait behind several signals
+    passes at once and absorbs the ones nobody waited for (the pair is back in step)."""
+    from mfnerf._lib import call, ptr, stream
+    gate = torch.zeros(2, dtype=torch.int32, device=gpu)
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    call("mfnerf_gate_wait", ptr(gate), 3000, stream())
+    t1.record()
+    torch.cuda.synchronize()
+    assert 2.5 <= t0.elapsed_time(t1) <= 50.0 and gate.tolist() == [0, 1]
+    for _ in range(3):
+        call("mfnerf_gate_signal", ptr(gate), stream())
+    t0.record()
+    call("mfnerf_gate_wait", ptr(gate), 100000, stream())
+    t1.record()
+    torch.cuda.synchronize()
+    assert t0.elapsed_time(t1) < 5.0 and gate.tolist() == [3, 3]
+    with pytest.raises(RuntimeError):
+        call("mfnerf_gate_wait", ptr(gate), -1, stream())
 
 
 @pytest.mark.parametrize("parts", [1, 2, 4])
