@@ -14,6 +14,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "mfma_pack.hpp"
 #include "../../include/mfnerf.h"
 
 using namespace mfn;
@@ -127,25 +128,6 @@ __global__ void pack_kernel(const TP* __restrict__ px, const TP* __restrict__ pr
 
 __device__ __forceinline__ f32x16 mfma(const half8& a, const half8& b, const f32x16& c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-}
-
-template <int BASE, bool RELU>
-__device__ __forceinline__ half8 pack8(const f32x16& a) {
-    half8 r;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        float v = a[BASE + j];
-        if (RELU) v = fmaxf(v, 0.0f);
-        r[j] = (_Float16)v;
-    }
-    return r;
-}
-
-// zero dY where the forward activation (stored f16, post-ReLU) is not positive
-template <int BASE>
-__device__ __forceinline__ void relu_mask(f32x16& d, const half8& y) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) d[BASE + j] = ((float)y[j] > 0.0f) ? d[BASE + j] : 0.0f;
 }
 
 __device__ __forceinline__ half8 lds_frag(const _Float16* lds, int f, int lane) {
@@ -544,8 +526,8 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
             f32x16 a = mfma(bw_frag<W, NW>(lds, pk, G::B5 + mt, lane), dOb, z);
-            relu_mask<0>(a, T.r2[mt][0]); relu_mask<8>(a, T.r2[mt][1]);
-            dr2p[mt][0] = pack8<0, false>(a); dr2p[mt][1] = pack8<8, false>(a);
+            dr2p[mt][0] = relu_mask8(pack8<0, false>(a), T.r2[mt][0]);
+            dr2p[mt][1] = relu_mask8(pack8<8, false>(a), T.r2[mt][1]);
         }
         if constexpr (!C::R2_SPLIT) {   // -- rgb layer 2: dWr2 (WxW) += dR2^T R1
             SOp x[MT];
@@ -569,8 +551,8 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
 #pragma unroll
                 for (int q = 0; q < 2; ++q)
                     a = mfma(bw_frag<W, NW>(lds, pk, G::B4 + mt * G::KC + t * 2 + q, lane), dr2p[t][q], a);
-            relu_mask<0>(a, T.r1[mt][0]); relu_mask<8>(a, T.r1[mt][1]);
-            dr1p[mt][0] = pack8<0, false>(a); dr1p[mt][1] = pack8<8, false>(a);
+            dr1p[mt][0] = relu_mask8(pack8<0, false>(a), T.r1[mt][0]);
+            dr1p[mt][1] = relu_mask8(pack8<8, false>(a), T.r1[mt][1]);
         }
         {   // -- rgb layer 1: dWr1 (Wx32) += dR1^T [SH;h]   (SH natural order, h perm order)
             const SOp x = to_s(lds, lane, T.sh, ID_N0, T.hb, ID_P16);
@@ -604,10 +586,10 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
         {
             f32x16 a0 = mfma(bw_frag<W, NW>(lds, pk, G::B2 + 0, lane), dhb, z);
             f32x16 a1 = mfma(bw_frag<W, NW>(lds, pk, G::B2 + 1, lane), dhb, z);
-            relu_mask<0>(a0, T.y1[0][0]); relu_mask<8>(a0, T.y1[0][1]);
-            relu_mask<0>(a1, T.y1[1][0]); relu_mask<8>(a1, T.y1[1][1]);
-            dy1p[0][0] = pack8<0, false>(a0); dy1p[0][1] = pack8<8, false>(a0);
-            dy1p[1][0] = pack8<0, false>(a1); dy1p[1][1] = pack8<8, false>(a1);
+            dy1p[0][0] = relu_mask8(pack8<0, false>(a0), T.y1[0][0]);
+            dy1p[0][1] = relu_mask8(pack8<8, false>(a0), T.y1[0][1]);
+            dy1p[1][0] = relu_mask8(pack8<0, false>(a1), T.y1[1][0]);
+            dy1p[1][1] = relu_mask8(pack8<8, false>(a1), T.y1[1][1]);
         }
         {   // -- xyz layer 1: dW1 (64x32) += dY1^T X   (X natural order)
             const SOp x = to_s(lds, lane, T.x[0], ID_N0, T.x[1], ID_N16);
@@ -792,8 +774,8 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_wr2_kernel(
 #pragma unroll
         for (int o = 0; o < MT; ++o) {
             f32x16 a = mfma(lds_frag(lds, G::B5 + o, lane), dOb, z);
-            relu_mask<0>(a, T.r2[o][0]); relu_mask<8>(a, T.r2[o][1]);
-            const SOp d = to_s(lds, lane, pack8<0, false>(a), ID_P0, pack8<8, false>(a), ID_P16);
+            const SOp d = to_s(lds, lane, relu_mask8(pack8<0, false>(a), T.r2[o][0]), ID_P0,
+                               relu_mask8(pack8<8, false>(a), T.r2[o][1]), ID_P16);
 #pragma unroll
             for (int i = 0; i < MT; ++i) dw_acc_agpr(acc[o][i], d, x[i]);
         }

@@ -15,6 +15,7 @@
 //             (K = samples in both operands' registers, no transpose needed), partial tiles summed
 //             over chunks in a fixed order: deterministic.
 #include "common.hpp"
+#include "mfma_pack.hpp"
 #include "../../include/mfnerf.h"
 
 using namespace mfn;
@@ -87,19 +88,6 @@ __device__ __forceinline__ f32x16 mfma(const half8& a, const half8& b, const f32
 __device__ __forceinline__ half8 frag(const _Float16* lds, int f, int lane) {
     return *reinterpret_cast<const half8*>(lds + (f * 64 + lane) * 8);
 }
-template <int BASE, bool RELU>
-__device__ __forceinline__ half8 pack8(const f32x16& a) {
-    half8 r;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = (_Float16)(RELU ? fmaxf(a[BASE + j], 0.0f) : a[BASE + j]);
-    return r;
-}
-template <int BASE>
-__device__ __forceinline__ void relu_mask(f32x16& d, const half8& y) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) d[BASE + j] = ((float)y[j] > 0.0f) ? d[BASE + j] : 0.0f;
-}
-
 // the forward of one 32-sample tile: the layer inputs as B operands (kept for the backward) and
 // the output layer's accumulator (rows 0..15)
 template <int W, int NH>
@@ -235,10 +223,8 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_bw_kernel(const _Float16* __res
 #pragma unroll
         for (int mt = 0; mt < G::MT; ++mt) {
             f32x16 a = mfma(frag(lds, G::BO + mt, lane), d, z);
-            relu_mask<0>(a, T.a[NH - 1][2 * mt]);
-            relu_mask<8>(a, T.a[NH - 1][2 * mt + 1]);
-            dzc[2 * mt] = pack8<0, false>(a);
-            dzc[2 * mt + 1] = pack8<8, false>(a);
+            dzc[2 * mt] = relu_mask8(pack8<0, false>(a), T.a[NH - 1][2 * mt]);
+            dzc[2 * mt + 1] = relu_mask8(pack8<8, false>(a), T.a[NH - 1][2 * mt + 1]);
         }
 #pragma unroll
         for (int l = NH - 1; l >= 1; --l) {
@@ -250,10 +236,8 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_bw_kernel(const _Float16* __res
                 f32x16 a = z;
 #pragma unroll
                 for (int c = 0; c < G::KC; ++c) a = mfma(frag(lds, G::BH + ((l - 1) * G::MT + mt) * G::KC + c, lane), dzc[c], a);
-                relu_mask<0>(a, T.a[l - 1][2 * mt]);
-                relu_mask<8>(a, T.a[l - 1][2 * mt + 1]);
-                nx[2 * mt] = pack8<0, false>(a);
-                nx[2 * mt + 1] = pack8<8, false>(a);
+                nx[2 * mt] = relu_mask8(pack8<0, false>(a), T.a[l - 1][2 * mt]);
+                nx[2 * mt + 1] = relu_mask8(pack8<8, false>(a), T.a[l - 1][2 * mt + 1]);
             }
 #pragma unroll
             for (int c = 0; c < G::KC; ++c) dzc[c] = nx[c];
