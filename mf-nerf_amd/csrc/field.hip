@@ -64,6 +64,7 @@ struct BwCfg {
     static constexpr bool RGB_LDS = XYZ_LDS;              // dWr1, dWr2, dWr3
     static constexpr bool R2_SPLIT = (W == 128);          // dWr2 by field_bw_wr2_kernel
     static constexpr bool B4_GLOBAL = false;              // Wr2^T from global memory (unused variant)
+    static constexpr bool PAIR = false;                   // two sample tiles per loop trip (spills: slower)
     static constexpr int SKIP = B4_GLOBAL ? G::MT * G::KC : 0;
     static constexpr int LDS_FRAGS = G::N - SKIP + 4;  // + 4 identity fragments
     static constexpr int ID_BASE = LDS_FRAGS - 4;
@@ -209,68 +210,122 @@ __device__ __forceinline__ void load_tile_in(const _Float16* __restrict__ feat, 
     }
 }
 
-template <int W, bool DENSITY_ONLY>
-__device__ __forceinline__ void forward_tile(const _Float16* lds, int lane, const TileIn& I, bool valid,
-                                             FwdTile<W>& T) {
+// The forward of P independent tiles, stage by stage: each layer's MFMAs for every tile, then the
+// next layer.  The scheduler keeps this source order at one wave per SIMD, so a tile's packing
+// (VALU) overlaps the next tile's MFMAs, and one fragment read from LDS serves all P tiles.
+template <int W, bool DENSITY_ONLY, int P>
+__device__ __forceinline__ void forward_tiles(const _Float16* lds, int lane, const TileIn* I, const bool* valid,
+                                              FwdTile<W>* T) {
     using G = Geo<W>;
     constexpr int MT = G::MT;
     const int h = lane >> 5;
     const f32x16 z = {};
-    T.x[0] = I.x[0];
-    T.x[1] = I.x[1];
     // xyz layer 1: Y1^T = W1 X^T
-    f32x16 y1a = mfma(lds_frag(lds, G::F1 + 0, lane), T.x[0], z);
-    y1a = mfma(lds_frag(lds, G::F1 + 1, lane), T.x[1], y1a);
-    f32x16 y1b = mfma(lds_frag(lds, G::F1 + 2, lane), T.x[0], z);
-    y1b = mfma(lds_frag(lds, G::F1 + 3, lane), T.x[1], y1b);
-    T.y1[0][0] = pack8<0, true>(y1a); T.y1[0][1] = pack8<8, true>(y1a);
-    T.y1[1][0] = pack8<0, true>(y1b); T.y1[1][1] = pack8<8, true>(y1b);
-    // xyz layer 2: H^T = W2 relu(Y1)^T (rows 0..15 valid)
-    f32x16 ha = mfma(lds_frag(lds, G::F2 + 0, lane), T.y1[0][0], z);
-    ha = mfma(lds_frag(lds, G::F2 + 1, lane), T.y1[0][1], ha);
-    ha = mfma(lds_frag(lds, G::F2 + 2, lane), T.y1[1][0], ha);
-    ha = mfma(lds_frag(lds, G::F2 + 3, lane), T.y1[1][1], ha);
-    T.hb = pack8<0, false>(ha);   // the fp16 network output of tcnn
-    T.h0 = (float)T.hb[0];        // row 0 on lanes h==0
-    if (DENSITY_ONLY) return;
-    float shv[16];
-    if (valid) sh4(I.d[0], I.d[1], I.d[2], shv);
-    else {
+    {
+        const half8 f0 = lds_frag(lds, G::F1 + 0, lane), f1 = lds_frag(lds, G::F1 + 1, lane);
+        const half8 f2 = lds_frag(lds, G::F1 + 2, lane), f3 = lds_frag(lds, G::F1 + 3, lane);
+        f32x16 y1a[P], y1b[P];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) shv[i] = 0.0f;
+        for (int q = 0; q < P; ++q) {
+            T[q].x[0] = I[q].x[0];
+            T[q].x[1] = I[q].x[1];
+            y1a[q] = mfma(f0, T[q].x[0], z);
+            y1a[q] = mfma(f1, T[q].x[1], y1a[q]);
+            y1b[q] = mfma(f2, T[q].x[0], z);
+            y1b[q] = mfma(f3, T[q].x[1], y1b[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            T[q].y1[0][0] = pack8<0, true>(y1a[q]); T[q].y1[0][1] = pack8<8, true>(y1a[q]);
+            T[q].y1[1][0] = pack8<0, true>(y1b[q]); T[q].y1[1][1] = pack8<8, true>(y1b[q]);
+        }
     }
+    // xyz layer 2: H^T = W2 relu(Y1)^T (rows 0..15 valid)
+    {
+        half8 f[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        // select the loaded VALUES (a conditional of the two array lvalues is an lvalue: a load
-        // through a selected pointer, which kept shv in scratch memory)
-        const float lo = shv[j], hi = shv[8 + j];
-        T.sh[j] = (_Float16)(h ? hi : lo);
+        for (int i = 0; i < 4; ++i) f[i] = lds_frag(lds, G::F2 + i, lane);
+        f32x16 ha[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            ha[q] = mfma(f[0], T[q].y1[0][0], z);
+            ha[q] = mfma(f[1], T[q].y1[0][1], ha[q]);
+            ha[q] = mfma(f[2], T[q].y1[1][0], ha[q]);
+            ha[q] = mfma(f[3], T[q].y1[1][1], ha[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            T[q].hb = pack8<0, false>(ha[q]);   // the fp16 network output of tcnn
+            T[q].h0 = (float)T[q].hb[0];        // row 0 on lanes h==0
+        }
+    }
+    if (DENSITY_ONLY) return;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        float shv[16];
+        sh4(I[q].d[0], I[q].d[1], I[q].d[2], shv);  // (0/0 on invalid lanes, selected away: no branch)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) shv[i] = valid[q] ? shv[i] : 0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            // select the loaded VALUES (a conditional of the two array lvalues is an lvalue: a load
+            // through a selected pointer, which kept shv in scratch memory)
+            const float lo = shv[j], hi = shv[8 + j];
+            T[q].sh[j] = (_Float16)(h ? hi : lo);
+        }
     }
     // rgb layer 1
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-        f32x16 a = mfma(lds_frag(lds, G::F3 + 2 * mt, lane), T.sh, z);
-        a = mfma(lds_frag(lds, G::F3 + 2 * mt + 1, lane), T.hb, a);
-        T.r1[mt][0] = pack8<0, true>(a); T.r1[mt][1] = pack8<8, true>(a);
+        const half8 f0 = lds_frag(lds, G::F3 + 2 * mt, lane), f1 = lds_frag(lds, G::F3 + 2 * mt + 1, lane);
+        f32x16 a[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            a[q] = mfma(f0, T[q].sh, z);
+            a[q] = mfma(f1, T[q].hb, a[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < P; ++q) { T[q].r1[mt][0] = pack8<0, true>(a[q]); T[q].r1[mt][1] = pack8<8, true>(a[q]); }
     }
     // rgb layer 2
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-        f32x16 a = z;
+        f32x16 a[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) a[q] = z;
 #pragma unroll
         for (int t = 0; t < MT; ++t)
 #pragma unroll
-            for (int q = 0; q < 2; ++q) a = mfma(lds_frag(lds, G::F4 + mt * G::KC + t * 2 + q, lane), T.r1[t][q], a);
-        T.r2[mt][0] = pack8<0, true>(a); T.r2[mt][1] = pack8<8, true>(a);
+            for (int k = 0; k < 2; ++k) {
+                const half8 f = lds_frag(lds, G::F4 + mt * G::KC + t * 2 + k, lane);
+#pragma unroll
+                for (int q = 0; q < P; ++q) a[q] = mfma(f, T[q].r1[t][k], a[q]);
+            }
+#pragma unroll
+        for (int q = 0; q < P; ++q) { T[q].r2[mt][0] = pack8<0, true>(a[q]); T[q].r2[mt][1] = pack8<8, true>(a[q]); }
     }
     // rgb layer 3 (rows 0..2 = rgb logits on lanes h==0)
-    f32x16 o = z;
+    f32x16 o[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) o[q] = z;
 #pragma unroll
     for (int t = 0; t < MT; ++t)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) o = mfma(lds_frag(lds, G::F5 + t * 2 + q, lane), T.r2[t][q], o);
+        for (int k = 0; k < 2; ++k) {
+            const half8 f = lds_frag(lds, G::F5 + t * 2 + k, lane);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) T.rgb[c] = 1.0f / (1.0f + __expf(-o[c]));
+            for (int q = 0; q < P; ++q) o[q] = mfma(f, T[q].r2[t][k], o[q]);
+        }
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) T[q].rgb[c] = 1.0f / (1.0f + __expf(-o[q][c]));
+}
+
+template <int W, bool DENSITY_ONLY>
+__device__ __forceinline__ void forward_tile(const _Float16* lds, int lane, const TileIn& I, bool valid,
+                                             FwdTile<W>& T) {
+    forward_tiles<W, DENSITY_ONLY, 1>(lds, lane, &I, &valid, &T);
 }
 
 __device__ __forceinline__ void load_frags(_Float16* lds, const _Float16* __restrict__ packed, int n_frags) {
@@ -474,154 +529,230 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     const int64_t tiles = div_up<int64_t>(nn, 32);
     const int64_t stride = (int64_t)gridDim.x * NW;
-    // the next tile's inputs are loaded while this tile computes
-    TileIn nI;
-    float ngs = 0.f, ng0 = 0.f, ng1 = 0.f, ng2 = 0.f;
-    auto fetch = [&](int64_t tile) {
+    // P sample tiles per loop trip (tile, tile + stride, ...), computed in one basic block so the
+    // scheduler overlaps one tile's MFMA chain with the other's VALU packing and LDS waits (one wave
+    // per SIMD hides no latency otherwise).  Each accumulator still takes the tiles in the order
+    // tile, tile + stride, ...: the sums are the same as with one tile per trip, bit for bit.
+    constexpr int P = C::PAIR ? 2 : 1;
+    // the next trip's inputs are loaded while this trip computes
+    struct BwIn { TileIn I; float gs, g0, g1, g2; };
+    BwIn nx[P];
+    auto fetch = [&](int64_t tile, BwIn& o) {
         const int64_t s = tile * 32 + r;
         const bool v = s < nn;
-        load_tile_in(feat, plane_stride, dirs, s, v, h, true, nI);
-        ngs = ng0 = ng1 = ng2 = 0.0f;
+        load_tile_in(feat, plane_stride, dirs, s, v, h, true, o.I);
+        o.gs = o.g0 = o.g1 = o.g2 = 0.0f;
         if (v && h == 0) {
-            ngs = dL_dsigma[s];
-            ng0 = dL_drgb[3 * s]; ng1 = dL_drgb[3 * s + 1]; ng2 = dL_drgb[3 * s + 2];
+            o.gs = dL_dsigma[s];
+            o.g0 = dL_drgb[3 * s]; o.g1 = dL_drgb[3 * s + 1]; o.g2 = dL_drgb[3 * s + 2];
         }
     };
     const int64_t tile0 = (int64_t)blockIdx.x * NW + wid;
-    if (tile0 < tiles) fetch(tile0);
+    if (tile0 < tiles) {
+#pragma unroll
+        for (int q = 0; q < P; ++q) fetch(tile0 + q * stride, nx[q]);
+    }
     // per-level L1 of dL/dfeat (the fixed-point table-gradient scales): this lane's 8 levels are
     // 4g + 2h (features 8g+4h, +1) and 4g + 2h + 1 (features 8g+4h+2, +3), g = 0..3
     float l1a[4] = {0.f, 0.f, 0.f, 0.f}, l1b[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t tile = tile0; tile < tiles; tile += stride) {
+    // one trip: the P tiles' forward + backward stage by stage (see forward_tiles); dW into the
+    // accumulators (tile 0's contribution before tile 1's), dX^T (scaled by S) into dx[]
+    auto trip_bw = [&](const _Float16* lds, const _Float16* pk, const BwIn* in, const bool* valid, f32x16* dx) {
+        FwdTile<W> T[P];
+        {
+            TileIn I[P];
+#pragma unroll
+            for (int q = 0; q < P; ++q) I[q] = in[q].I;
+            forward_tiles<W, false, P>(lds, lane, I, valid, T);
+        }
+        // -- rgb layer 3: dO (rows 0..2 on lanes h==0) = dL/drgb * sigmoid' (the grads are 0 on
+        //    lanes h == 1: no branch)
+        half8 dOb[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            f32x16 dO = z;
+            dO[0] = in[q].g0 * S * T[q].rgb[0] * (1.0f - T[q].rgb[0]);
+            dO[1] = in[q].g1 * S * T[q].rgb[1] * (1.0f - T[q].rgb[1]);
+            dO[2] = in[q].g2 * S * T[q].rgb[2] * (1.0f - T[q].rgb[2]);
+            dOb[q] = pack8<0, false>(dO);
+        }
+        //    dR2 = Wr3^T dO, masked by R2 > 0 (the data-gradient chain first, the dW products after)
+        half8 dr2p[P][MT][2];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const half8 f = bw_frag<W, NW>(lds, pk, G::B5 + mt, lane);
+            f32x16 a[P];
+#pragma unroll
+            for (int q = 0; q < P; ++q) a[q] = mfma(f, dOb[q], z);
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                dr2p[q][mt][0] = relu_mask8(pack8<0, false>(a[q]), T[q].r2[mt][0]);
+                dr2p[q][mt][1] = relu_mask8(pack8<8, false>(a[q]), T[q].r2[mt][1]);
+            }
+        }
+        // dWr3 (16 x W, rows 0..2 non-zero) += dO^T R2
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const SOp d = to_s16(lds, lane, dOb[q], ID_P0);
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+                acc_tile<RL>(dwr3[RL ? 0 : t], i_r3, 3, W, d,
+                             to_s(lds, lane, T[q].r2[t][0], ID_P0, T[q].r2[t][1], ID_P16), 0, t, lane);
+        }
+        //    dR1 = Wr2^T dR2, masked by R1 > 0
+        half8 dr1p[P][MT][2];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            f32x16 a[P];
+#pragma unroll
+            for (int q = 0; q < P; ++q) a[q] = z;
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const half8 f = bw_frag<W, NW>(lds, pk, G::B4 + mt * G::KC + t * 2 + k, lane);
+#pragma unroll
+                    for (int q = 0; q < P; ++q) a[q] = mfma(f, dr2p[q][t][k], a[q]);
+                }
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                dr1p[q][mt][0] = relu_mask8(pack8<0, false>(a[q]), T[q].r1[mt][0]);
+                dr1p[q][mt][1] = relu_mask8(pack8<8, false>(a[q]), T[q].r1[mt][1]);
+            }
+        }
+        if constexpr (!C::R2_SPLIT) {   // -- rgb layer 2: dWr2 (WxW) += dR2^T R1
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                SOp x[MT];
+#pragma unroll
+                for (int i = 0; i < MT; ++i) x[i] = to_s(lds, lane, T[q].r1[i][0], ID_P0, T[q].r1[i][1], ID_P16);
+#pragma unroll
+                for (int o = 0; o < MT; ++o) {
+                    const SOp d = to_s(lds, lane, dr2p[q][o][0], ID_P0, dr2p[q][o][1], ID_P16);
+#pragma unroll
+                    for (int i = 0; i < MT; ++i)
+                        acc_tile<RL>(dwr2[RL ? 0 : o][RL ? 0 : i], i_r2, W, W, d, x[i], o, i, lane);
+                }
+            }
+        }
+        //    d[SH;h] = Wr1^T dR1 (rows 16..31 = dh) + TruncExp backward into h[0]
+        half8 dhb[P];
+        {
+            f32x16 dsh[P];
+#pragma unroll
+            for (int q = 0; q < P; ++q) dsh[q] = z;
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const half8 f = bw_frag<W, NW>(lds, pk, G::B3 + t * 2 + k, lane);
+#pragma unroll
+                    for (int q = 0; q < P; ++q) dsh[q] = mfma(f, dr1p[q][t][k], dsh[q]);
+                }
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                // row 16 = reg 8 on lanes h==0: g * exp(clamp(h0,-15,15)) (custom_functions.py:170-173)
+                const float dh0 = in[q].gs * S * __expf(fminf(fmaxf(T[q].h0, -15.0f), 15.0f));
+                dsh[q][8] = h == 0 ? dsh[q][8] + dh0 : dsh[q][8];
+                dhb[q] = pack8<8, false>(dsh[q]);
+            }
+        }
+        // -- rgb layer 1: dWr1 (Wx32) += dR1^T [SH;h]   (SH natural order, h perm order)
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const SOp x = to_s(lds, lane, T[q].sh, ID_N0, T[q].hb, ID_P16);
+#pragma unroll
+            for (int o = 0; o < MT; ++o)
+                acc_tile<RL>(dwr1[RL ? 0 : o], i_r1, W, 32,
+                             to_s(lds, lane, dr1p[q][o][0], ID_P0, dr1p[q][o][1], ID_P16), x, o, 0, lane);
+        }
+        //    dY1 = W2^T dh, masked by Y1 > 0
+        half8 dy1p[P][2][2];
+        {
+            const half8 f0 = bw_frag<W, NW>(lds, pk, G::B2 + 0, lane), f1 = bw_frag<W, NW>(lds, pk, G::B2 + 1, lane);
+            f32x16 a0[P], a1[P];
+#pragma unroll
+            for (int q = 0; q < P; ++q) { a0[q] = mfma(f0, dhb[q], z); a1[q] = mfma(f1, dhb[q], z); }
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                dy1p[q][0][0] = relu_mask8(pack8<0, false>(a0[q]), T[q].y1[0][0]);
+                dy1p[q][0][1] = relu_mask8(pack8<8, false>(a0[q]), T[q].y1[0][1]);
+                dy1p[q][1][0] = relu_mask8(pack8<0, false>(a1[q]), T[q].y1[1][0]);
+                dy1p[q][1][1] = relu_mask8(pack8<8, false>(a1[q]), T[q].y1[1][1]);
+            }
+        }
+        //    dX = W1^T dY1
+        {
+            half8 f[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) f[i] = bw_frag<W, NW>(lds, pk, G::B1 + i, lane);
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                dx[q] = z;
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) dx[q] = mfma(f[t * 2 + k], dy1p[q][t][k], dx[q]);
+            }
+        }
+        // -- xyz layer 2: dW2 (16x64) += dh^T Y1
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const SOp d = to_s16(lds, lane, dhb[q], ID_P0);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+                acc_tile<XL>(dw2[XL ? 0 : t], i_w2, 16, 64, d,
+                             to_s(lds, lane, T[q].y1[t][0], ID_P0, T[q].y1[t][1], ID_P16), 0, t, lane);
+        }
+        // -- xyz layer 1: dW1 (64x32) += dY1^T X   (X natural order)
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const SOp x = to_s(lds, lane, T[q].x[0], ID_N0, T[q].x[1], ID_N16);
+#pragma unroll
+            for (int o = 0; o < 2; ++o)
+                acc_tile<XL>(dw1[XL ? 0 : o], i_w1, 64, 32,
+                             to_s(lds, lane, dy1p[q][o][0], ID_P0, dy1p[q][o][1], ID_P16), x, o, 0, lane);
+        }
+    };
+    for (int64_t tile = tile0; tile < tiles; tile += P * stride) {
         // the fragment reads are loop-invariant; an opaque base keeps the compiler from hoisting
         // all of them (4 registers each) out of the loop
         int opaque = 0;
         asm volatile("" : "+s"(opaque));
         const _Float16* lds = lds_base + opaque;
         const _Float16* pk = packed + opaque;  // B4 from global memory (W = 128): not hoisted either
-        const int64_t s = tile * 32 + r;
-        const bool valid = s < nn;
-        const TileIn I = nI;
-        const float gs = ngs, g0 = ng0, g1 = ng1, g2 = ng2;
-        if (tile + stride < tiles) fetch(tile + stride);
-        FwdTile<W> T;
-        forward_tile<W, false>(lds, lane, I, valid, T);
-        // -- rgb layer 3: dO (rows 0..2 on lanes h==0) = dL/drgb * sigmoid'
-        f32x16 dO = z;
-        if (h == 0) {
-            dO[0] = g0 * S * T.rgb[0] * (1.0f - T.rgb[0]);
-            dO[1] = g1 * S * T.rgb[1] * (1.0f - T.rgb[1]);
-            dO[2] = g2 * S * T.rgb[2] * (1.0f - T.rgb[2]);
+        BwIn in[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) in[q] = nx[q];
+        if (tile + P * stride < tiles) {
+#pragma unroll
+            for (int q = 0; q < P; ++q) fetch(tile + (P + q) * stride, nx[q]);
         }
-        const half8 dOb = pack8<0, false>(dO);
-        {   // dWr3 (16 x W, rows 0..2 non-zero) += dO^T R2
-            const SOp d = to_s16(lds, lane, dOb, ID_P0);
+        f32x16 dx[P];
+        bool valid[P];
 #pragma unroll
-            for (int t = 0; t < MT; ++t)
-                acc_tile<RL>(dwr3[RL ? 0 : t], i_r3, 3, W, d, to_s(lds, lane, T.r2[t][0], ID_P0, T.r2[t][1], ID_P16),
-                             0, t, lane);
-        }
-        //    dR2 = Wr3^T dO, masked by R2 > 0
-        half8 dr2p[MT][2];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-            f32x16 a = mfma(bw_frag<W, NW>(lds, pk, G::B5 + mt, lane), dOb, z);
-            dr2p[mt][0] = relu_mask8(pack8<0, false>(a), T.r2[mt][0]);
-            dr2p[mt][1] = relu_mask8(pack8<8, false>(a), T.r2[mt][1]);
-        }
-        if constexpr (!C::R2_SPLIT) {   // -- rgb layer 2: dWr2 (WxW) += dR2^T R1
-            SOp x[MT];
-#pragma unroll
-            for (int i = 0; i < MT; ++i) x[i] = to_s(lds, lane, T.r1[i][0], ID_P0, T.r1[i][1], ID_P16);
-#pragma unroll
-            for (int o = 0; o < MT; ++o) {
-                const SOp d = to_s(lds, lane, dr2p[o][0], ID_P0, dr2p[o][1], ID_P16);
-#pragma unroll
-                for (int i = 0; i < MT; ++i)
-                    acc_tile<RL>(dwr2[RL ? 0 : o][RL ? 0 : i], i_r2, W, W, d, x[i], o, i, lane);
-            }
-        }
-        //    dR1 = Wr2^T dR2, masked by R1 > 0
-        half8 dr1p[MT][2];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-            f32x16 a = z;
-#pragma unroll
-            for (int t = 0; t < MT; ++t)
-#pragma unroll
-                for (int q = 0; q < 2; ++q)
-                    a = mfma(bw_frag<W, NW>(lds, pk, G::B4 + mt * G::KC + t * 2 + q, lane), dr2p[t][q], a);
-            dr1p[mt][0] = relu_mask8(pack8<0, false>(a), T.r1[mt][0]);
-            dr1p[mt][1] = relu_mask8(pack8<8, false>(a), T.r1[mt][1]);
-        }
-        {   // -- rgb layer 1: dWr1 (Wx32) += dR1^T [SH;h]   (SH natural order, h perm order)
-            const SOp x = to_s(lds, lane, T.sh, ID_N0, T.hb, ID_P16);
-#pragma unroll
-            for (int o = 0; o < MT; ++o)
-                acc_tile<RL>(dwr1[RL ? 0 : o], i_r1, W, 32, to_s(lds, lane, dr1p[o][0], ID_P0, dr1p[o][1], ID_P16), x,
-                             o, 0, lane);
-        }
-        //    d[SH;h] = Wr1^T dR1 (rows 16..31 = dh) + TruncExp backward into h[0]
-        half8 dhb;
-        {
-            f32x16 dsh = z;
-#pragma unroll
-            for (int t = 0; t < MT; ++t)
-#pragma unroll
-                for (int q = 0; q < 2; ++q)
-                    dsh = mfma(bw_frag<W, NW>(lds, pk, G::B3 + t * 2 + q, lane), dr1p[t][q], dsh);
-            // row 16 = reg 8 on lanes h==0: g * exp(clamp(h0,-15,15)) (custom_functions.py:170-173)
-            if (h == 0) dsh[8] += gs * S * __expf(fminf(fmaxf(T.h0, -15.0f), 15.0f));
-            dhb = pack8<8, false>(dsh);
-        }
-        {   // -- xyz layer 2: dW2 (16x64) += dh^T Y1
-            const SOp d = to_s16(lds, lane, dhb, ID_P0);
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-                acc_tile<XL>(dw2[XL ? 0 : t], i_w2, 16, 64, d, to_s(lds, lane, T.y1[t][0], ID_P0, T.y1[t][1], ID_P16),
-                             0, t, lane);
-        }
-        //    dY1 = W2^T dh, masked by Y1 > 0
-        half8 dy1p[2][2];
-        {
-            f32x16 a0 = mfma(bw_frag<W, NW>(lds, pk, G::B2 + 0, lane), dhb, z);
-            f32x16 a1 = mfma(bw_frag<W, NW>(lds, pk, G::B2 + 1, lane), dhb, z);
-            dy1p[0][0] = relu_mask8(pack8<0, false>(a0), T.y1[0][0]);
-            dy1p[0][1] = relu_mask8(pack8<8, false>(a0), T.y1[0][1]);
-            dy1p[1][0] = relu_mask8(pack8<0, false>(a1), T.y1[1][0]);
-            dy1p[1][1] = relu_mask8(pack8<8, false>(a1), T.y1[1][1]);
-        }
-        {   // -- xyz layer 1: dW1 (64x32) += dY1^T X   (X natural order)
-            const SOp x = to_s(lds, lane, T.x[0], ID_N0, T.x[1], ID_N16);
-#pragma unroll
-            for (int o = 0; o < 2; ++o)
-                acc_tile<XL>(dw1[XL ? 0 : o], i_w1, 64, 32, to_s(lds, lane, dy1p[o][0], ID_P0, dy1p[o][1], ID_P16), x,
-                             o, 0, lane);
-        }
+        for (int q = 0; q < P; ++q) valid[q] = (tile + q * stride) * 32 + r < nn;
+        trip_bw(lds, pk, in, valid, dx);
         //    dX = W1^T dY1 -> global fp32 (features (i&3)+8(i>>2)+4h)
-        {
-            f32x16 dx = z;
+        bool bad = false;
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int q = 0; q < 2; ++q)
-                    dx = mfma(bw_frag<W, NW>(lds, pk, G::B1 + t * 2 + q, lane), dy1p[t][q], dx);
-            bool bad = false;
-            if (valid) {
+        for (int q = 0; q < P; ++q) {
+            const int64_t s = (tile + q * stride) * 32 + r;
+            if (s < nn) {
                 float4* dst = reinterpret_cast<float4*>(dL_dfeat + s * 32);
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const float4 o = make_float4(dx[4 * g] * invS, dx[4 * g + 1] * invS, dx[4 * g + 2] * invS,
-                                                 dx[4 * g + 3] * invS);
+                    const float4 o = make_float4(dx[q][4 * g] * invS, dx[q][4 * g + 1] * invS,
+                                                 dx[q][4 * g + 2] * invS, dx[q][4 * g + 3] * invS);
                     bad |= !(isfinite(o.x) && isfinite(o.y) && isfinite(o.z) && isfinite(o.w));
                     dst[2 * g + h] = o;
                     l1a[g] += fabsf(o.x) + fabsf(o.y);
                     l1b[g] += fabsf(o.z) + fabsf(o.w);
                 }
             }
-            // the table gradient is sum(weight * dL/dfeat): non-finite only if some dL/dfeat is
-            if (nonfinite && __any(bad) && lane == 0) atomicOr(nonfinite, 1);
         }
+        // the table gradient is sum(weight * dL/dfeat): non-finite only if some dL/dfeat is
+        if (nonfinite && __any(bad) && lane == 0) atomicOr(nonfinite, 1);
     }
 
     // ---- epilogue: the workgroup's dW (and the level L1 partials) -> one slab row
