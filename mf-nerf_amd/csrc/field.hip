@@ -64,7 +64,10 @@ struct BwCfg {
     static constexpr bool RGB_LDS = XYZ_LDS;              // dWr1, dWr2, dWr3
     static constexpr bool R2_SPLIT = (W == 128);          // dWr2 by field_bw_wr2_kernel
     static constexpr bool B4_GLOBAL = false;              // Wr2^T from global memory (unused variant)
-    static constexpr bool PAIR = false;                   // two sample tiles per loop trip (spills: slower)
+#ifndef MFN_FIELD_PAIR
+#define MFN_FIELD_PAIR 0
+#endif
+    static constexpr bool PAIR = MFN_FIELD_PAIR && W == 64 && NW == 4;  // two sample tiles per loop trip
     static constexpr int SKIP = B4_GLOBAL ? G::MT * G::KC : 0;
     static constexpr int LDS_FRAGS = G::N - SKIP + 4;  // + 4 identity fragments
     static constexpr int ID_BASE = LDS_FRAGS - 4;
@@ -487,7 +490,7 @@ __device__ __forceinline__ void acc_tile(f32x16& reg, float* img, int rows, int 
     }
 }
 
-template <int W, int NW>
+template <int W, int NW, bool PLANAR>
 __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
     const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n,
     const int32_t* __restrict__ n_dev, const _Float16* __restrict__ packed, const float* __restrict__ dL_dsigma,
@@ -510,7 +513,7 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
     float* i_r1 = limg + (XL ? oR1 : 0);
     float* i_r2 = i_r1 + W * 32;
     float* i_r3 = i_r2 + W * W;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform)
     const int r = lane & 31, h = lane >> 5;
     const float S = scale_dev ? *scale_dev : grad_scale, invS = 1.0f / S;  // the (dynamic) loss scale
     const f32x16 z = {};
@@ -535,23 +538,50 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
     // tile, tile + stride, ...: the sums are the same as with one tile per trip, bit for bit.
     constexpr int P = C::PAIR ? 2 : 1;
     // the next trip's inputs are loaded while this trip computes
-    struct BwIn { TileIn I; float gs, g0, g1, g2; };
+    struct BwIn { TileIn I; float gs, g0, g1, g2; bool live; };
     BwIn nx[P];
+    // Branch-free: every lane loads (a sample index clamped into [0, nn)) and only the incoming
+    // gradients are zeroed where the sample is out of range or on the lanes h == 1.  An out-of-range
+    // lane then carries finite activations with a zero data gradient, so its dW products are zero
+    // (a NaN there would poison the K = samples sums), and the loop has one path: the compiler's
+    // vmcnt bookkeeping does not merge paths into a vmcnt(0) that waits for the dL/dfeat stores.
     auto fetch = [&](int64_t tile, BwIn& o) {
         const int64_t s = tile * 32 + r;
-        const bool v = s < nn;
-        load_tile_in(feat, plane_stride, dirs, s, v, h, true, o.I);
-        o.gs = o.g0 = o.g1 = o.g2 = 0.0f;
-        if (v && h == 0) {
-            o.gs = dL_dsigma[s];
-            o.g0 = dL_drgb[3 * s]; o.g1 = dL_drgb[3 * s + 1]; o.g2 = dL_drgb[3 * s + 2];
+        const bool v = s < nn && h == 0;
+        const int64_t sc = min<int64_t>(s, nn - 1);
+        if constexpr (PLANAR) {
+            // x[0] element j = feature 8h+j = level 4h + j/2; x[1]: level 8 + 4h + j/2
+            const uint32_t* Pp = reinterpret_cast<const uint32_t*>(feat);
+            uint32_t u[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                u[k] = Pp[(int64_t)(4 * h + k) * plane_stride + sc];
+                u[4 + k] = Pp[(int64_t)(8 + 4 * h + k) * plane_stride + sc];
+            }
+            o.I.x[0] = *reinterpret_cast<const half8*>(&u[0]);
+            o.I.x[1] = *reinterpret_cast<const half8*>(&u[4]);
+        } else {
+            const half8* row = reinterpret_cast<const half8*>(feat + sc * 32);
+            o.I.x[0] = row[h];
+            o.I.x[1] = row[2 + h];
         }
+        o.I.d[0] = dirs[3 * sc]; o.I.d[1] = dirs[3 * sc + 1]; o.I.d[2] = dirs[3 * sc + 2];
+        // raw: the select waits for the load, so it happens where the values are used (zero_grads)
+        o.gs = dL_dsigma[sc]; o.g0 = dL_drgb[3 * sc]; o.g1 = dL_drgb[3 * sc + 1]; o.g2 = dL_drgb[3 * sc + 2];
+        o.live = v;
+    };
+    auto zero_grads = [&](BwIn& o) {
+        o.gs = o.live ? o.gs : 0.0f;
+        o.g0 = o.live ? o.g0 : 0.0f;
+        o.g1 = o.live ? o.g1 : 0.0f;
+        o.g2 = o.live ? o.g2 : 0.0f;
     };
     const int64_t tile0 = (int64_t)blockIdx.x * NW + wid;
     if (tile0 < tiles) {
 #pragma unroll
         for (int q = 0; q < P; ++q) fetch(tile0 + q * stride, nx[q]);
     }
+    bool bad = false;  // a non-finite dL/dfeat on this lane, reported once after the loop
     // per-level L1 of dL/dfeat (the fixed-point table-gradient scales): this lane's 8 levels are
     // 4g + 2h (features 8g+4h, +1) and 4g + 2h + 1 (features 8g+4h+2, +3), g = 0..3
     float l1a[4] = {0.f, 0.f, 0.f, 0.f}, l1b[4] = {0.f, 0.f, 0.f, 0.f};
@@ -723,37 +753,32 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
         const _Float16* pk = packed + opaque;  // B4 from global memory (W = 128): not hoisted either
         BwIn in[P];
 #pragma unroll
-        for (int q = 0; q < P; ++q) in[q] = nx[q];
-        if (tile + P * stride < tiles) {
+        for (int q = 0; q < P; ++q) { in[q] = nx[q]; zero_grads(in[q]); }
 #pragma unroll
-            for (int q = 0; q < P; ++q) fetch(tile + (P + q) * stride, nx[q]);
-        }
+        for (int q = 0; q < P; ++q) fetch(tile + (P + q) * stride, nx[q]);  // (clamped past the end)
         f32x16 dx[P];
         bool valid[P];
 #pragma unroll
         for (int q = 0; q < P; ++q) valid[q] = (tile + q * stride) * 32 + r < nn;
         trip_bw(lds, pk, in, valid, dx);
         //    dX = W1^T dY1 -> global fp32 (features (i&3)+8(i>>2)+4h)
-        bool bad = false;
 #pragma unroll
         for (int q = 0; q < P; ++q) {
             const int64_t s = (tile + q * stride) * 32 + r;
-            if (s < nn) {
-                float4* dst = reinterpret_cast<float4*>(dL_dfeat + s * 32);
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float4 o = make_float4(dx[q][4 * g] * invS, dx[q][4 * g + 1] * invS,
-                                                 dx[q][4 * g + 2] * invS, dx[q][4 * g + 3] * invS);
-                    bad |= !(isfinite(o.x) && isfinite(o.y) && isfinite(o.z) && isfinite(o.w));
-                    dst[2 * g + h] = o;
-                    l1a[g] += fabsf(o.x) + fabsf(o.y);
-                    l1b[g] += fabsf(o.z) + fabsf(o.w);
-                }
+            for (int g = 0; g < 4; ++g) {
+                const float4 o = make_float4(dx[q][4 * g] * invS, dx[q][4 * g + 1] * invS,
+                                             dx[q][4 * g + 2] * invS, dx[q][4 * g + 3] * invS);
+                bad |= !(isfinite(o.x) && isfinite(o.y) && isfinite(o.z) && isfinite(o.w));
+                if (s < nn) reinterpret_cast<float4*>(dL_dfeat + s * 32)[2 * g + h] = o;
+                // (an out-of-range lane's dX is exactly zero: its data gradient is)
+                l1a[g] += fabsf(o.x) + fabsf(o.y);
+                l1b[g] += fabsf(o.z) + fabsf(o.w);
             }
         }
-        // the table gradient is sum(weight * dL/dfeat): non-finite only if some dL/dfeat is
-        if (nonfinite && __any(bad) && lane == 0) atomicOr(nonfinite, 1);
     }
+    // the table gradient is sum(weight * dL/dfeat): non-finite only if some dL/dfeat is
+    if (nonfinite && __any(bad) && lane == 0) atomicOr(nonfinite, 1);
 
     // ---- epilogue: the workgroup's dW (and the level L1 partials) -> one slab row
     float* row = slab + (int64_t)blockIdx.x * G::N_DW;
@@ -1035,16 +1060,26 @@ int launch_bw(const void* feat, int64_t ps, const float* dirs, int64_t n, const 
               mfnerf_stream_t stream) {
     using C = BwCfg<W, NW>;
     if constexpr (C::LDS > 65536) {  // more than the default dynamic-LDS limit
-        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_kernel<W, NW>),
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
+        static const hipError_t attr = [] {
+            const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_kernel<W, NW, false>),
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
+            const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_kernel<W, NW, true>),
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
+            return a0 != hipSuccess ? a0 : a1;
+        }();
         if (attr != hipSuccess) {
             mfn_set_error("field_bw: cannot raise the LDS limit to %d bytes", (int)C::LDS);
             return MFN_ERR_INVALID;
         }
     }
-    hipLaunchKernelGGL((field_bw_kernel<W, NW>), dim3(BW_BLOCKS), dim3(64 * NW), C::LDS, stream,
-                       (const _Float16*)feat, ps, dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb,
-                       grad_scale, scale_dev, dL_dfeat, (float*)workspace, nonfinite, level_l1);
+    if (ps > 0)
+        hipLaunchKernelGGL((field_bw_kernel<W, NW, true>), dim3(BW_BLOCKS), dim3(64 * NW), C::LDS, stream,
+                           (const _Float16*)feat, ps, dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb,
+                           grad_scale, scale_dev, dL_dfeat, (float*)workspace, nonfinite, level_l1);
+    else
+        hipLaunchKernelGGL((field_bw_kernel<W, NW, false>), dim3(BW_BLOCKS), dim3(64 * NW), C::LDS, stream,
+                           (const _Float16*)feat, ps, dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb,
+                           grad_scale, scale_dev, dL_dfeat, (float*)workspace, nonfinite, level_l1);
     if constexpr (C::R2_SPLIT)
         hipLaunchKernelGGL(field_bw_wr2_kernel<W>, dim3(BW_BLOCKS), dim3(FIELD_BLOCK),
                            (size_t)(Geo<W>::B4 + 4) * FRAG_HALFS * 2, stream, (const _Float16*)feat, ps, dirs, n, n_dev,
