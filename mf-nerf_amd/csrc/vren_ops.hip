@@ -140,7 +140,10 @@ __global__ void march_count_kernel(MarchParams p, int64_t n_rays, int32_t* __res
 }
 
 // One-workgroup exclusive scan of the per-ray counts -> rays_a rows and counter (device resident).
-constexpr int SCAN_THREADS = 1024;
+// 512 threads, few registers: the scan runs on the side stream while the scatter's 1024-thread workgroups hold
+// 16 waves of every CU; a 1024-thread workgroup found no CU until the scatter ended (~115 us later)
+constexpr int SCAN_THREADS = 512;
+constexpr int SCAN_K = 32;  // counts per thread held in registers (n_rays <= 16384)
 __global__ __launch_bounds__(SCAN_THREADS) void march_scan_kernel(const int32_t* __restrict__ counts, int64_t n_rays,
                                                                  int64_t capacity, int64_t* __restrict__ rays_a,
                                                                  int32_t* __restrict__ counter) {
@@ -148,8 +151,24 @@ __global__ __launch_bounds__(SCAN_THREADS) void march_scan_kernel(const int32_t*
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int64_t chunk = div_up<int64_t>(n_rays, SCAN_THREADS);
     const int64_t b = tid * chunk, e = min(n_rays, b + chunk);
+    // up to SCAN_K counts per thread (8192 rays: 16, 16384: 32) are loaded together: one memory round
+    // trip instead of chunk dependent ones (this kernel runs on the side stream beside the
+    // table-gradient scatter, where every load waits behind its traffic)
+    const bool staged = chunk <= SCAN_K;
+    int32_t cr[SCAN_K];
     int64_t local = 0;
-    for (int64_t i = b; i < e; ++i) local += counts[i];
+    if (staged) {
+#pragma unroll
+        for (int k = 0; k < SCAN_K; ++k) {
+            const int64_t i = b + k;
+            const int32_t c = counts[i < e ? i : 0];
+            cr[k] = i < e ? c : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < SCAN_K; ++k) local += cr[k];
+    } else {
+        for (int64_t i = b; i < e; ++i) local += counts[i];
+    }
     // inclusive wave scan
     int64_t v = local;
     for (int off = 1; off < 64; off <<= 1) {
@@ -168,12 +187,17 @@ __global__ __launch_bounds__(SCAN_THREADS) void march_scan_kernel(const int32_t*
     }
     __syncthreads();
     int64_t run = (v - local) + (wid > 0 ? wave_tot[wid - 1] : 0);  // exclusive start of this chunk
-    for (int64_t i = b; i < e; ++i) {
-        const int64_t c = counts[i];
-        const int64_t s = min(run, capacity);
-        const int64_t cc = max<int64_t>(0, min(c, capacity - run));
-        rays_a[3 * i] = i; rays_a[3 * i + 1] = s; rays_a[3 * i + 2] = cc;
-        run += c;
+    {
+        // the write pass re-reads the counts (cache hits now) rather than keep SCAN_K registers live
+        // through it: the kernel must stay small to fit beside the scatter's waves
+#pragma unroll 4
+        for (int64_t i = b; i < e; ++i) {
+            const int64_t c = counts[i];
+            const int64_t s = min(run, capacity);
+            const int64_t cc = max<int64_t>(0, min(c, capacity - run));
+            rays_a[3 * i] = i; rays_a[3 * i + 1] = s; rays_a[3 * i + 2] = cc;
+            run += c;
+        }
     }
     if (tid == SCAN_THREADS - 1) {
         counter[0] = (int32_t)min(run, capacity);
