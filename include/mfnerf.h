@@ -254,6 +254,22 @@ int mfnerf_grid_encode_bw_binned_adam(const float* x, int64_t n, const int32_t* 
                                       const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
                                       void* workspace, int64_t n_slots, const float* level_l1,
                                       const mfnerf_adam_fused* adam, mfnerf_stream_t stream);
+/* The collective-free step's whole table-gradient + optimizer tail in three launches: the binned
+ * scatter (parts = 3), an accumulate launch whose partitions apply Adam to the partitioned tables
+ * (as mfnerf_grid_encode_bw_binned_adam) while its leading workgroups run mfnerf_adam_step_fixed's
+ * update over [0, the partitioned tables' first value) -- the MLPs and the dense levels, whose
+ * gradients are final before the scatter -- and, after the overflow fallback, a pass that updates
+ * the partitioned values only if a record slot overflowed and does the step's bookkeeping (step
+ * count, GradScaler, level_l1 zeroed).  grads: the flat gradient of n_params values (the table's
+ * at adam->table_offset), zero for the table on entry; step_dev / amp: adam's, writable.  Same bits
+ * as mfnerf_grid_encode_bw_binned_adam + mfnerf_adam_step_fixed_partial (and as the unfused
+ * mfnerf_grid_encode_bw_binned + mfnerf_adam_step_fixed).  Replaces tcnn's hash-grid backward +
+ * apex FusedAdam's step over the whole model (train.py:136). */
+int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                                          const mfnerf_grid_desc* desc, const float* dL_dout, float* grads,
+                                          int64_t n_params, void* workspace, int64_t n_slots, float* level_l1,
+                                          const mfnerf_adam_fused* adam, int32_t* step_dev, mfnerf_amp_state* amp,
+                                          mfnerf_stream_t stream);
 
 /* out[l] += sum over rows i < n (or *n_dev) of |dL_dout[i][2l]| + |dL_dout[i][2l+1]| (f32). */
 int mfnerf_grid_level_l1(const float* dL_dout, int64_t n, const int32_t* n_dev, int n_levels, float* out,

@@ -785,28 +785,15 @@ __global__ __launch_bounds__(256) void fold_convert_kernel(float* __restrict__ g
 // prefix's in GRAD_COPIES private copies); each value is converted exactly as fold_convert_kernel
 // does, fed to the same Adam update as adam_kernel, and its gradient word (and copies) zeroed for
 // the next step -- one pass over the gradient instead of a convert pass + a read in Adam.
-__global__ __launch_bounds__(256) void adam_fixed_kernel(float* __restrict__ p, float* __restrict__ g,
-                                                         float* __restrict__ m, float* __restrict__ v,
-                                                         __half* __restrict__ p16, int64_t n, int64_t off,
-                                                         int* __restrict__ priv, int64_t dense_vals,
-                                                         int64_t total_vals, const mfnerf_grid_desc D,
-                                                         float* __restrict__ level_l1, float lr, float b1,
-                                                         float b2, float eps, int32_t* __restrict__ step_dev,
-                                                         const float* __restrict__ lr_dev,
-                                                         mfnerf_amp_state* __restrict__ amp, int n_levels,
-                                                         int64_t fused_from, const int32_t* __restrict__ fused_ovf) {
-    __shared__ TableRegions R;
-    // values >= fused_from were updated by the fused partitioned accumulate, unless it overflowed
-    if (fused_ovf && *fused_ovf == 0) n = fused_from;
-    R.build(D, level_l1, total_vals);
-    const bool skipped = amp && amp->nonfinite;  // GradScaler: no update on a non-finite gradient, only the zeroing
-    const int st = *step_dev + 1;
-    if (lr_dev) lr = *lr_dev;
-    const float bc1 = 1.0f - powf(b1, (float)st);
-    const float bc2 = 1.0f - powf(b2, (float)st);
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+// The float4 groups [i4_first, i4_end) step `stride` (a grid-stride loop over the caller's threads).
+__device__ __forceinline__ void adam_fixed_body(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                                                float* __restrict__ v, __half* __restrict__ p16, int64_t off,
+                                                int* __restrict__ priv, int64_t dense_vals, int64_t total_vals,
+                                                const TableRegions& R, float lr, float b1, float b2, float eps,
+                                                float bc1, float bc2, bool skipped, int64_t i4_first,
+                                                int64_t i4_end, int64_t stride) {
     int l = 0;
-    for (int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; 4 * i4 < n; i4 += stride) {
+    for (int64_t i4 = i4_first; i4 < i4_end; i4 += stride) {
         const int64_t i = 4 * i4, j = i - off;  // off, dense_vals, region bounds: multiples of 4
         float4 gg;
         if (j < 0 || j >= total_vals) {
@@ -840,6 +827,41 @@ __global__ __launch_bounds__(256) void adam_fixed_kernel(float* __restrict__ p, 
             reinterpret_cast<uint2*>(p16)[i4] = u;
         }
     }
+}
+
+// tail_mode 0: values [0, n), or [0, fused_from) when the fused partitioned accumulate updated the
+// rest (fused_ovf clear).  tail_mode 1 (mfnerf_grid_encode_bw_binned_adam_all, whose accumulate
+// launch also updated [0, fused_from)): [fused_from, n) only if a slot overflowed, else nothing but
+// the step's bookkeeping.
+__global__ __launch_bounds__(256) void adam_fixed_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v,
+                                                         __half* __restrict__ p16, int64_t n, int64_t off,
+                                                         int* __restrict__ priv, int64_t dense_vals,
+                                                         int64_t total_vals, const mfnerf_grid_desc D,
+                                                         float* __restrict__ level_l1, float lr, float b1,
+                                                         float b2, float eps, int32_t* __restrict__ step_dev,
+                                                         const float* __restrict__ lr_dev,
+                                                         mfnerf_amp_state* __restrict__ amp, int n_levels,
+                                                         int64_t fused_from, const int32_t* __restrict__ fused_ovf,
+                                                         int tail_mode) {
+    __shared__ TableRegions R;
+    int64_t lo = 0;
+    if (tail_mode == 1) {
+        lo = fused_from;
+        if (*fused_ovf == 0) n = lo;
+    } else if (fused_ovf && *fused_ovf == 0) {
+        // values >= fused_from were updated by the fused partitioned accumulate
+        n = fused_from;
+    }
+    R.build(D, level_l1, total_vals);
+    const bool skipped = amp && amp->nonfinite;  // GradScaler: no update on a non-finite gradient, only the zeroing
+    const int st = *step_dev + 1;
+    if (lr_dev) lr = *lr_dev;
+    const float bc1 = 1.0f - powf(b1, (float)st);
+    const float bc2 = 1.0f - powf(b2, (float)st);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    adam_fixed_body(p, g, m, v, p16, off, priv, dense_vals, total_vals, R, lr, b1, b2, eps, bc1, bc2, skipped,
+                    lo / 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x, n / 4, stride);
     // step count / skip count / loss scale, and level_l1 zeroed for the next step's field_bw, by the
     // last workgroup (every workgroup has read level_l1, step_dev and the flag by now)
     if (amp) mfn::amp_step_end_last_block(step_dev, amp, level_l1, n_levels);
@@ -1304,6 +1326,17 @@ __device__ __forceinline__ int acc_out(unsigned long long v) { return round_shif
 
 constexpr int ACC_THREADS = 512;
 
+// The rest of the optimizer step carried by the accumulate's launch (mfnerf_grid_encode_bw_binned_adam_all):
+// its first n_blocks workgroups run adam_fixed_body over the float4 groups [0, end4) -- the MLPs and
+// the dense levels, whose gradients are final before the scatter -- beside the partitions' workgroups.
+struct AdamRest {
+    float* g;            // the flat gradient (MLP floats, then the table's int32 sums)
+    int* priv;           // the dense levels' private copies
+    int64_t dense_vals, total_vals, end4;
+    int n_blocks;        // 0: none
+    int first;           // 1: the grid's first n_blocks workgroups (dispatched early), 0: its last
+};
+
 __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, int64_t n,
                                                                 const int32_t* __restrict__ n_dev,
                                                                 const uint3* __restrict__ rec,
@@ -1313,7 +1346,22 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
                                                                 int* __restrict__ grad, int64_t n_slots,
                                                                 const mfnerf_grid_desc D,
                                                                 const float* __restrict__ level_l1,
-                                                                const mfnerf_adam_fused A) {
+                                                                const mfnerf_adam_fused A, const AdamRest X) {
+    const int rest_b = X.first ? (int)blockIdx.x : (int)blockIdx.x - P.n_bins;
+    if (rest_b >= 0 && rest_b < X.n_blocks) {
+        // independent of the slot-overflow flag: these values never go through the partitions
+        __shared__ TableRegions TR;
+        TR.build(D, level_l1, X.total_vals);
+        const bool skipped = A.amp && A.amp->nonfinite;
+        const int stp = *A.step_dev + 1;
+        const float lr = A.lr_dev ? *A.lr_dev : A.lr;
+        const float bc1 = 1.0f - powf(A.beta1, (float)stp);
+        const float bc2 = 1.0f - powf(A.beta2, (float)stp);
+        adam_fixed_body(A.params, X.g, A.m, A.v, reinterpret_cast<__half*>(A.p16), A.table_offset, X.priv,
+                        X.dense_vals, X.total_vals, TR, lr, A.beta1, A.beta2, A.eps, bc1, bc2, skipped,
+                        (int64_t)rest_b * blockDim.x + threadIdx.x, X.end4, (int64_t)X.n_blocks * blockDim.x);
+        return;
+    }
     if (*ovf) return;  // a slot overflowed: bin_fallback_kernel scatters the binned levels
 #if MFN_ACC32 == 2
     constexpr int IMG_WORDS = 1;  // per entry
@@ -1321,7 +1369,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     constexpr int IMG_WORDS = 2;
 #endif
     __shared__ acc_t img[IMG_WORDS * MAX_BIN_ENTRIES];
-    const int bin = blockIdx.x;
+    const int bin = (int)blockIdx.x - (X.first ? X.n_blocks : 0);
     const int n_ent = 1 << P.shift, mask = n_ent - 1;
     for (int i = threadIdx.x; i < IMG_WORDS * n_ent; i += blockDim.x) img[i] = 0;
     __syncthreads();
@@ -1515,7 +1563,7 @@ int first_binned_level(const mfnerf_grid_desc* d) {
 int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                 const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table, void* workspace,
                 int64_t n_slots, const float* level_l1, int parts, const mfnerf_adam_fused* adam,
-                mfnerf_stream_t stream);
+                mfnerf_stream_t stream, const AdamRest* rest = nullptr);
 
 struct BinWorkspace {
     float* priv;
@@ -1684,7 +1732,7 @@ int mfnerf_adam_step_fixed_partial(float* params, float* grads, float* m, float*
                        dim3((unsigned)(want < MFN_ADAM_BLOCKS ? (want < 1 ? 1 : want) : MFN_ADAM_BLOCKS)), dim3(256), 0,
                        stream, params, grads, m, v, (__half*)p_f16, n, table_offset, (int*)workspace, 2 * dense,
                        total, *desc, level_l1, lr, beta1, beta2, eps, step_dev, lr_dev, amp, desc->n_levels,
-                       fused_from, fused_ovf);
+                       fused_from, fused_ovf, 0);
     if (!amp)  // else the kernel's last workgroup did it
         hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, amp, level_l1, desc->n_levels);
     return mfn_check_launch("adam_step_fixed");
@@ -1805,6 +1853,58 @@ int mfnerf_grid_encode_bw_binned_adam(const float* x, int64_t n, const int32_t* 
                        adam, stream);
 }
 
+int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                                          const mfnerf_grid_desc* desc, const float* dL_dout, float* grads,
+                                          int64_t n_params, void* workspace, int64_t n_slots, float* level_l1,
+                                          const mfnerf_adam_fused* adam, int32_t* step_dev, mfnerf_amp_state* amp,
+                                          mfnerf_stream_t stream) {
+    if (!adam || !adam->params || !adam->m || !adam->v || !grads || !step_dev || adam->step_dev != step_dev ||
+        adam->amp != amp || (((uintptr_t)adam->params | (uintptr_t)adam->m | (uintptr_t)adam->v |
+                              (uintptr_t)grads) & 15) || (adam->p16 && ((uintptr_t)adam->p16 & 7)) ||
+        adam->table_offset % 4 || n_params % 4 || adam->table_offset < 0) {
+        mfn_set_error("grid_encode_bw_binned_adam_all: bad Adam arguments (null or misaligned vectors, "
+                      "table_offset / n_params not multiples of 4, step_dev / amp differing from adam's)");
+        return MFN_ERR_INVALID;
+    }
+    int st = check_desc(desc, "grid_encode_bw_binned_adam_all");
+    if (st) return st;
+    int64_t total = 0;
+    for (int l = 0; l < desc->n_levels; ++l) {
+        const int64_t e = 2 * ((int64_t)desc->offset[l] + desc->size[l]);
+        total = e > total ? e : total;
+    }
+    BinPlan P;
+    if (bin_plan(desc, &P) <= 0 || adam->table_offset + total > n_params) {
+        mfn_set_error("grid_encode_bw_binned_adam_all: nothing partitioned, or the table outside [table_offset, n_params)");
+        return MFN_ERR_INVALID;
+    }
+    const int64_t fused_from = adam->table_offset + 2 * (int64_t)P.t_offset[0];  // the partitioned tables' first value
+    if (fused_from % 4) { mfn_set_error("grid_encode_bw_binned_adam_all: partitions not float4-aligned"); return MFN_ERR_INVALID; }
+    BinWorkspace W;
+    binned_workspace_layout(desc, n_slots <= 0 || n_slots > n ? n : n_slots, (char*)workspace, &W);
+    // [0, fused_from) by the accumulate launch's leading workgroups (one float4 per thread, <= 256 of them)
+    AdamRest X{grads, (int*)workspace, 2 * dense_entries_of(desc), total, fused_from / 4, 0, 1};
+    static const int knobs[2] = {
+        [] { const char* e = getenv("MFNERF_ADAM_REST_BLOCKS"); return e ? atoi(e) : 256; }(),
+        [] { const char* e = getenv("MFNERF_ADAM_REST_FIRST"); return e ? atoi(e) : 1; }()};
+    const int64_t want = div_up<int64_t>(fused_from / 4, ACC_THREADS);
+    X.n_blocks = (int)(want < 1 ? 1 : (want < knobs[0] ? want : knobs[0]));
+    X.first = knobs[1];
+    st = binned_impl(x, n, n_dev, x_min, x_range, desc, dL_dout, grads + adam->table_offset, workspace, n_slots,
+                     level_l1, 3, adam, stream, &X);
+    if (st) return st;
+    // after the overflow fallback: the partitioned tables' values if a slot overflowed (else
+    // nothing), then the step's bookkeeping (step count, loss scale, level_l1 zeroed) by the last
+    // workgroup -- after every workgroup of the accumulate has read them
+    hipLaunchKernelGGL(adam_fixed_kernel, dim3(64), dim3(256), 0, stream, adam->params, grads, adam->m, adam->v,
+                       (__half*)adam->p16, n_params, adam->table_offset, (int*)workspace, 2 * dense_entries_of(desc),
+                       total, *desc, level_l1, adam->lr, adam->beta1, adam->beta2, adam->eps, step_dev, adam->lr_dev,
+                       amp, desc->n_levels, fused_from, (const int32_t*)W.ovf, 1);
+    if (!amp)
+        hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, amp, level_l1, desc->n_levels);
+    return mfn_check_launch("grid_encode_bw_binned_adam_all");
+}
+
 int64_t mfnerf_grid_binned_first_value(const mfnerf_grid_desc* desc) {
     if (check_desc(desc, "grid_binned_first_value")) return -1;
     BinPlan P;
@@ -1825,7 +1925,7 @@ namespace {
 int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                 const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table, void* workspace,
                 int64_t n_slots, const float* level_l1, int parts, const mfnerf_adam_fused* adam,
-                mfnerf_stream_t stream) {
+                mfnerf_stream_t stream, const AdamRest* rest) {
     int st = check_desc(desc, "grid_encode_bw_binned");
     if (st) return st;
     if (n_slots <= 0 || n_slots > n) n_slots = n;
@@ -1878,8 +1978,10 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
                            *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.smax, W.ovf, n_slots);
         mfnerf_adam_fused A{};
         if (adam) A = *adam;
-        hipLaunchKernelGGL(bin_accum_kernel, dim3(P.n_bins), dim3(ACC_THREADS), 0, stream, P, n, n_dev, W.rec,
-                           W.scnt, W.smax, W.ovf, (int*)grad_table, n_slots, *desc, level_l1, A);
+        AdamRest X{};
+        if (rest) X = *rest;
+        hipLaunchKernelGGL(bin_accum_kernel, dim3(P.n_bins + X.n_blocks), dim3(ACC_THREADS), 0, stream, P, n, n_dev,
+                           W.rec, W.scnt, W.smax, W.ovf, (int*)grad_table, n_slots, *desc, level_l1, A, X);
         // levels [l_first, L) by atomics, only when a slot overflowed (exits at once otherwise)
         auto fb = big ? bin_fallback_kernel<MFN_MAX_LEVELS> : bin_fallback_kernel<16>;
         hipLaunchKernelGGL(fb, dim3(256), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc, dL_dout,

@@ -466,8 +466,17 @@ class TrainStep:
 
     def _grid_bw(self, mb, q, fuse_adam=False):
         """Part q's hash-table gradient scatter (the dominant kernel, alone so it can be timed);
-        fuse_adam: with the partitioned tables' Adam step (then _finish_update(partial=True))."""
+        fuse_adam: with the partitioned tables' Adam step (then _finish_update(partial=True));
+        fuse_adam="all": with the whole optimizer step (then only _pack())."""
         t, m = self.parts[q], mb.part[q]
+        if self._binned() and fuse_adam == "all":
+            self._fused_args = self._adam_fused_args()  # kept alive: graphs capture the call
+            amp = self._amp_ptr()
+            call("mfnerf_grid_encode_bw_binned_adam_all", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min,
+                 self.x_range, self.desc, ptr(t.dfeat), ptr(self.grads), self.n_alloc, ptr(t.grid_ws),
+                 self._bin_slots(), ptr(self._level_l1), ctypes.byref(self._fused_args), ptr(self.step_dev),
+                 amp, stream())
+            return
         if self._binned() and fuse_adam:
             self._fused_args = self._adam_fused_args()  # kept alive: graphs capture the call
             call("mfnerf_grid_encode_bw_binned_adam", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min,
@@ -485,6 +494,18 @@ class TrainStep:
         call("mfnerf_grid_encode_bw_scatter", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min, self.x_range,
              self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws),
              ptr(self._level_l1) if self._fixed() else None, stream())
+
+    def _fused_tail(self, j):
+        """The replayed collective-free tail: scatter + every Adam update, then the MLP repack.  By
+        default the MLPs' and dense levels' update rides the accumulate's launch
+        (mfnerf_grid_encode_bw_binned_adam_all); MFNERF_FUSED_ADAM_ALL=0 keeps it a pass of its own
+        after the scatter (mfnerf_adam_step_fixed_partial).  Same bits either way."""
+        if os.environ.get("MFNERF_FUSED_ADAM_ALL", "1") == "1":
+            self._grid_bw(self.mbuf[j], 0, fuse_adam="all")
+            self._pack()
+        else:
+            self._grid_bw(self.mbuf[j], 0, fuse_adam=True)
+            self._finish_update(partial=True)
 
     def _grid_finish(self, q):
         """Fold part q's private copies of the coarse levels / convert the fixed-point sums."""
@@ -667,9 +688,7 @@ class TrainStep:
                 self.graphs["finish_update"] = cap(tail)
                 # and the scatter with it (one graph transition less again) for untimed steps
                 if self._fixed() and self._fused_adam_ok():  # the tables' Adam inside the accumulate
-                    self.graphs["grid_bw_tail"] = [
-                        cap(lambda j=j: (self._grid_bw(self.mbuf[j], 0, fuse_adam=True),
-                                         self._finish_update(partial=True))) for j in range(2)]
+                    self.graphs["grid_bw_tail"] = [cap(lambda j=j: self._fused_tail(j)) for j in range(2)]
                 else:
                     self.graphs["grid_bw_tail"] = [cap(lambda j=j: (self._grid_bw(self.mbuf[j], 0), tail()))
                                                    for j in range(2)]
@@ -685,8 +704,7 @@ class TrainStep:
                         self._chain(self._static[j], self.mbuf[j], 0, nomark)
                         call("mfnerf_gate_signal", gp, stream())
                         if fuse:
-                            self._grid_bw(self.mbuf[j], 0, fuse_adam=True)
-                            self._finish_update(partial=True)
+                            self._fused_tail(j)
                         else:
                             self._grid_bw(self.mbuf[j], 0)
                             tail()

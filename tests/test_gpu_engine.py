@@ -216,12 +216,23 @@ def test_fused_convert_adam_matches_finish_then_adam(gpu, kw, skip):
 @pytest.mark.parametrize("kw", [{}, {"grid": "MixedFeature", "N_tables": 8, "rgb_width": 128}],
                          ids=["hash-rgb64", "mixedfeature-rgb128"])
 @pytest.mark.parametrize("skip", [False, True])
-def test_partitioned_accumulate_with_fused_adam_matches_unfused(gpu, kw, skip):
+@pytest.mark.parametrize("mode", ["partial", "all", "all-overflow"])
+def test_partitioned_accumulate_with_fused_adam_matches_unfused(gpu, kw, skip, mode):
     """The replayed tail with the partitioned tables' Adam fused into the accumulate
-    (mfnerf_grid_encode_bw_binned_adam + mfnerf_adam_step_fixed_partial) == the scatter followed by
-    the one-pass convert + Adam (mfnerf_adam_step_fixed), bit for bit: params, m, v, the fp16 mirror,
-    the step counter, the zeroed gradient words, copies and level_l1 -- also on a skipped step."""
-    st = _make(gpu, 1, **kw)
+    (partial: mfnerf_grid_encode_bw_binned_adam + mfnerf_adam_step_fixed_partial; all:
+    mfnerf_grid_encode_bw_binned_adam_all, the MLPs' and dense levels' update riding the accumulate's
+    launch; all-overflow: the same with record slots sized far below the live count, so the atomic
+    fallback and the overflow pass run) == the scatter followed by the one-pass convert + Adam
+    (mfnerf_adam_step_fixed), bit for bit: params, m, v, the fp16 mirror, the step counter, the
+    zeroed gradient words, copies and level_l1 -- also on a skipped step."""
+    if mode == "all-overflow":
+        # small tables (few partitions) and a full batch: ~480 records per (partition, unit) slot
+        # against slots sized for 256 samples (112 records)
+        st = engine.TrainStep(engine.StepConfig(n_rays=8192, log2_T=12, n_parts=1, **kw), device=gpu, seed=0)
+        st.set_occupancy(synthetic.ball_density_grid())
+        st._bin_slots = lambda: 256
+    else:
+        st = _make(gpu, 1, **kw)
     assert st._fused_adam_ok()
     batches = st.make_batches(2, seed=5)
     st.run(batches[0])  # m, v non-zero
@@ -244,9 +255,16 @@ def test_partitioned_accumulate_with_fused_adam_matches_unfused(gpu, kw, skip):
     for k in names:
         getattr(st, k).copy_(snap[k])
     ws.copy_(snap_ws)
-    st._grid_bw(mb, 0, fuse_adam=True)
-    st._finish_update(partial=True)
+    if mode == "partial":
+        st._grid_bw(mb, 0, fuse_adam=True)
+        st._finish_update(partial=True)
+    else:
+        st._grid_bw(mb, 0, fuse_adam="all")
+        st._pack()
     torch.cuda.synchronize()
+    if mode == "all-overflow":
+        ovf = load().mfnerf_grid_encode_bw_binned_flag_offset(st.desc, st._bin_slots()) // 4
+        assert int(ws[ovf].view(torch.int32)) == 1  # the fallback path really ran
     for k in names:
         assert torch.equal(getattr(st, k), ref[k]), k
     nc = load().mfnerf_grid_encode_bw_workspace(st.desc) // 4  # the private copies: zeroed by both
