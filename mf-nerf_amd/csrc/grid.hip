@@ -1371,15 +1371,32 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     __shared__ acc_t img[IMG_WORDS * MAX_BIN_ENTRIES];
     const int bin = (int)blockIdx.x - (X.first ? X.n_blocks : 0);
     const int n_ent = 1 << P.shift, mask = n_ent - 1;
-    for (int i = threadIdx.x; i < IMG_WORDS * n_ent; i += blockDim.x) img[i] = 0;
-    __syncthreads();
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     const int64_t slot = slot_size(min(nn, n_slots), P);  // = bin_scatter_kernel's
-    // one unit's slot per half-wave (32 lanes; ~30 records per slot at the Lego config), 4 slots
+    // one unit's slot per half-wave (32 lanes; ~30 records per slot at the Lego config), QF slots
     // in flight per half-wave
     const int hw = threadIdx.x >> 5, hl = threadIdx.x & 31, n_hw = ACC_THREADS / 32;
     const int32_t* cnt = scnt + (int64_t)bin * UNITS;
     const uint3* base = rec + (int64_t)bin * UNITS * slot;
+#ifndef MFN_ACC_INFLIGHT
+#define MFN_ACC_INFLIGHT 8  // slots per half-wave whose first 32 records are loaded together (16: all; 8 measured best)
+#endif
+    constexpr int QF = MFN_ACC_INFLIGHT;
+    uint3 r[QF];
+    int c[QF];
+    auto prefetch = [&](int u0) {
+#pragma unroll
+        for (int q = 0; q < QF; ++q) {
+            const int u = u0 + q * n_hw;
+            c[q] = u < UNITS ? cnt[u] : 0;
+            // unconditional (a slot holds >= 96 records, so lane hl < 32 stays inside it): the count
+            // and the records are in flight together; records past the count are dropped below
+            r[q] = base[(int64_t)(u < UNITS ? u : 0) * slot + hl];
+        }
+    };
+    prefetch(hw);  // the first round's loads overlap the image zeroing and the partition's bound
+    for (int i = threadIdx.x; i < IMG_WORDS * n_ent; i += blockDim.x) img[i] = 0;
+    __syncthreads();
 #if MFN_ACC32 == 2
     // the partition's bound (sum over units of count x max), summed in a fixed order -> its unit 2^-k
     __shared__ float wsum[ACC_THREADS / 64];
@@ -1403,24 +1420,17 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     }
     const float k2 = ldexpf(1.0f, kbits);
 #endif
-    for (int u0 = hw; u0 < UNITS; u0 += 4 * n_hw) {
-        uint3 r[4];
-        int c[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int u = u0 + q * n_hw;
-            c[q] = u < UNITS ? cnt[u] : 0;
-            r[q] = hl < c[q] ? base[(int64_t)u * slot + hl] : make_uint3(0u, 0u, 0u);
-        }
+    for (int u0 = hw; u0 < UNITS; u0 += QF * n_hw) {
+        if (u0 != hw) prefetch(u0);
 #if MFN_ACC32 == 2
 #define MFN_ACC(IMG, MASK, R) accum_record(IMG, MASK, R, k2)
 #else
 #define MFN_ACC(IMG, MASK, R) accum_record(IMG, MASK, R)
 #endif
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < QF; ++q) {
             const int u = u0 + q * n_hw;
-            MFN_ACC(img, mask, r[q]);
+            if (hl < c[q]) MFN_ACC(img, mask, r[q]);
             for (int k = hl + 32; k < c[q]; k += 32) MFN_ACC(img, mask, base[(int64_t)u * slot + k]);
         }
 #undef MFN_ACC
