@@ -700,9 +700,19 @@ class TrainStep:
                     gp = ptr(self._gate)
                     fuse = self._fixed() and self._fused_adam_ok()
 
+                    # where in the chain the gate opens: after the stage named.  Default "composite":
+                    # the next draw + march start beside field_bw, whose one wave per SIMD (384 of
+                    # 512 registers) leaves room and issue cycles for the march's waves -- 0.687 ->
+                    # 0.672 ms/step against opening after the whole chain ("field_bw"); "field_fw"
+                    # (beside compositing too) 0.677
+                    gate_at = os.environ.get("MFNERF_GATE_AT", "composite")
+
+                    def signal_at(name):
+                        if name == gate_at:
+                            call("mfnerf_gate_signal", gp, stream())
+
                     def step(j):
-                        self._chain(self._static[j], self.mbuf[j], 0, nomark)
-                        call("mfnerf_gate_signal", gp, stream())
+                        self._chain(self._static[j], self.mbuf[j], 0, signal_at)
                         if fuse:
                             self._fused_tail(j)
                         else:
