@@ -853,15 +853,17 @@ __global__ __launch_bounds__(256) void adam_fixed_kernel(float* __restrict__ p, 
         // values >= fused_from were updated by the fused partitioned accumulate
         n = fused_from;
     }
-    R.build(D, level_l1, total_vals);
-    const bool skipped = amp && amp->nonfinite;  // GradScaler: no update on a non-finite gradient, only the zeroing
-    const int st = *step_dev + 1;
-    if (lr_dev) lr = *lr_dev;
-    const float bc1 = 1.0f - powf(b1, (float)st);
-    const float bc2 = 1.0f - powf(b2, (float)st);
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    adam_fixed_body(p, g, m, v, p16, off, priv, dense_vals, total_vals, R, lr, b1, b2, eps, bc1, bc2, skipped,
-                    lo / 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x, n / 4, stride);
+    if (n > lo) {  // (uniform; the overflow-only pass has nothing to update unless a slot overflowed)
+        R.build(D, level_l1, total_vals);
+        const bool skipped = amp && amp->nonfinite;  // GradScaler: no update on a non-finite gradient, only the zeroing
+        const int st = *step_dev + 1;
+        if (lr_dev) lr = *lr_dev;
+        const float bc1 = 1.0f - powf(b1, (float)st);
+        const float bc2 = 1.0f - powf(b2, (float)st);
+        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+        adam_fixed_body(p, g, m, v, p16, off, priv, dense_vals, total_vals, R, lr, b1, b2, eps, bc1, bc2, skipped,
+                        lo / 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x, n / 4, stride);
+    }
     // step count / skip count / loss scale, and level_l1 zeroed for the next step's field_bw, by the
     // last workgroup (every workgroup has read level_l1, step_dev and the flag by now)
     if (amp) mfn::amp_step_end_last_block(step_dev, amp, level_l1, n_levels);
