@@ -62,7 +62,7 @@ def test_fully_fused_mlp_vs_fp16_oracle(gpu, width, depth, n_out, out_act):
     ref = mlp16(x64, p64, tcnn.mlp_shapes(32, n_out, width, depth), n_out, out_act)
     # fp32 accumulation of fp16 products vs exact sums, then one fp16 rounding: <= ~2 fp16 ulps
     err = (y.detach().cpu().double() - ref.detach()).abs()
-    assert float(err.max()) <= 2e-3 * max(1.0, float(ref.abs().max())), float(err.max())
+    assert float(err.max()) <= 2e-3 * max(1.0, float(ref.detach().abs().max())), float(err.max())
     (y.float() * dout.to(gpu)).sum().backward()
     (ref * dout.double()).sum().backward()
     # backward: fp16 operands (the loss-scaled dL/dout, activations, weights) with fp32 sums
