@@ -2022,7 +2022,12 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
         if (!((parts & 1) && l_first > 0)) (void)hipMemsetAsync(W.ovf, 0, sizeof(int32_t), stream);
         // the staged dL/dy rows sized for the binned levels (8 at the Lego layout; MixedFeature's
         // shared tables bin more)
-        auto sk = P.n_binned <= 8 ? bin_scatter_kernel<8> : bin_scatter_kernel<MAX_BINNED>;
+#ifndef MFN_SCATTER_MAXB12
+#define MFN_SCATTER_MAXB12 1
+#endif
+        auto sk = P.n_binned <= 8                          ? bin_scatter_kernel<8>
+                  : (MFN_SCATTER_MAXB12 && P.n_binned <= 12) ? bin_scatter_kernel<12>
+                                                             : bin_scatter_kernel<MAX_BINNED>;
         hipLaunchKernelGGL(sk, dim3(UNITS), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
                            *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.smax, W.ovf, n_slots);
         mfnerf_adam_fused A{};
