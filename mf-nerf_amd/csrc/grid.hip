@@ -2025,7 +2025,13 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
 #ifndef MFN_SCATTER_MAXB12
 #define MFN_SCATTER_MAXB12 1
 #endif
+#ifndef MFN_SCATTER_MAXB10
+#define MFN_SCATTER_MAXB10 1
+#endif
+        // the smallest staging that holds the partitioned levels: fewer registers leave room on each
+        // CU for the side stream's march kernels
         auto sk = P.n_binned <= 8                          ? bin_scatter_kernel<8>
+                  : (MFN_SCATTER_MAXB10 && P.n_binned <= 10) ? bin_scatter_kernel<10>
                   : (MFN_SCATTER_MAXB12 && P.n_binned <= 12) ? bin_scatter_kernel<12>
                                                              : bin_scatter_kernel<MAX_BINNED>;
         hipLaunchKernelGGL(sk, dim3(UNITS), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
