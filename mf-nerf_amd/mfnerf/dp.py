@@ -32,9 +32,15 @@ def _host_staged(fn, *ts):
         t.copy_(h)
 
 
+def _on():
+    """A process group is up (world size 1 included: the collectives then still run through the
+    backend -- RCCL's single-rank path is what tests/test_gpu_dp.py drives on the one-GPU box)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def allreduce_mean_(flat):
     """In-place mean over ranks of one flat gradient tensor (one collective per step)."""
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _on():
         return flat
     if dist.get_backend() == "nccl":
         dist.all_reduce(flat, op=dist.ReduceOp.AVG)
@@ -47,14 +53,14 @@ def allreduce_mean_(flat):
 
 
 def _world():
-    if not dist.is_available() or not dist.is_initialized():
+    if not _on():
         return 1
     return dist.get_world_size()
 
 
 def reduce_scatter_mean_(shard, flat):
     """shard (flat.numel()/world,) <- this rank's slice of the mean over ranks of flat."""
-    if _world() == 1:
+    if not _on():
         shard.copy_(flat)
         return shard
     if dist.get_backend() == "nccl":
@@ -69,9 +75,9 @@ def reduce_scatter_mean_(shard, flat):
 
 def all_gather_(full, rank):
     """full = concat over ranks of each rank's slice full[rank*k:(rank+1)*k] (in place)."""
-    w = _world()
-    if w == 1:
+    if not _on():
         return full
+    w = _world()
     k = full.numel() // w
     _host_staged(lambda x: dist.all_gather_into_tensor(x, x[rank * k:(rank + 1) * k].clone()), full)
     return full
@@ -86,10 +92,10 @@ def sharded_update(grads, g_shard, p16, rank, adam_shard, flag=None):
     sees the union of the flags without another collective."""
     from ._lib import call, ptr, stream
     w = _world()
-    if flag is not None and w > 1:
+    if flag is not None and _on():
         call("mfnerf_flag_to_shards", ptr(grads), w, g_shard.numel(), ptr(flag), stream())
     reduce_scatter_mean_(g_shard, grads)
-    if flag is not None and w > 1:
+    if flag is not None and _on():
         call("mfnerf_flag_from_shard", ptr(g_shard), ptr(flag), stream())
     adam_shard(g_shard)
     all_gather_(p16, rank)
@@ -97,7 +103,7 @@ def sharded_update(grads, g_shard, p16, rank, adam_shard, flag=None):
 
 def allreduce_max_(t):
     """In-place elementwise max over ranks (the non-finite-gradient flag)."""
-    if _world() == 1:
+    if not _on():
         return t
     if dist.get_backend() == "nccl":
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

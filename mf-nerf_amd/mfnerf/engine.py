@@ -241,8 +241,6 @@ class TrainStep:
         t.field_ws = torch.empty(load().mfnerf_field_bw_workspace(cap, c.rgb_width) // 4, **f32)
         if self._binned():
             nb = load().mfnerf_grid_encode_bw_binned_workspace(self.desc, self._bin_slots())
-            if nb < 0:
-                raise ValueError("grid layout unsupported by the binned table-gradient scatter")
         else:
             nb = load().mfnerf_grid_encode_bw_workspace(self.desc)
         t.grid_ws = torch.zeros(max(16, nb) // 4, **f32)
@@ -330,11 +328,12 @@ class TrainStep:
         call("mfnerf_field_pack_weights_f16", ptr(self.p16), ptr(self.p16[self.off_rgb:]), self.cfg.rgb_width,
              ptr(self.packed), stream())
 
-    def shard_optimizer(self, rank, world):
+    def shard_optimizer(self, rank, world, force=False):
         """Data parallel with a sharded optimizer (mfnerf.dp.sharded_update): this rank keeps Adam
         state only for its 1/world slice of the flat parameters; the step reduce-scatters the
-        gradient, updates the slice and all-gathers the fp16 compute copy."""
-        if world <= 1:
+        gradient, updates the slice and all-gathers the fp16 compute copy.  world 1 is a no-op
+        unless force (a one-rank process group running the sharded path, for tests)."""
+        if world <= 1 and not force:
             return
         if self.n_alloc % (64 * world):
             raise ValueError(f"world size {world} does not divide the padded parameter count {self.n_alloc}")
@@ -439,8 +438,14 @@ class TrainStep:
         return self.n_parts == 1 and self.cfg.fixed_point_grid
 
     def _binned(self):
-        """The fixed-point table gradient by table partitions (one part only, like _fixed)."""
-        return self.cfg.n_parts == 1 and self.cfg.fixed_point_grid and self.cfg.binned_grid
+        """The fixed-point table gradient by table partitions (one part only, like _fixed), for the
+        layouts the partitioned scatter supports; any other layout the reference accepts (opt.py:78,
+        e.g. --T 21) keeps the request-shaped fixed-point atomic scatter."""
+        if not (self.cfg.n_parts == 1 and self.cfg.fixed_point_grid and self.cfg.binned_grid):
+            return False
+        if getattr(self, "_bin_supported", None) is None:
+            self._bin_supported = load().mfnerf_grid_encode_bw_binned_workspace(self.desc, self._bin_slots()) >= 0
+        return self._bin_supported
 
     def _bin_slots(self):
         """Samples per part the binned scatter's record slots are sized for."""
@@ -451,10 +456,6 @@ class TrainStep:
         accumulate (mfnerf_grid_encode_bw_binned_adam + mfnerf_adam_step_fixed_partial)."""
         return (self._binned() and self.shard is None and os.environ.get("MFNERF_FUSED_ADAM", "1") == "1"
                 and load().mfnerf_grid_binned_first_value(self.desc) >= 0)
-
-    def _gated_ok(self):
-        """The collective-free single-part step can be one graph with a device-gated side march."""
-        return self.n_parts == 1 and self.shard is None and os.environ.get("MFNERF_GATED_MARCH", "1") == "1"
 
     def _adam_fused_args(self):
         c = self.cfg
@@ -638,19 +639,27 @@ class TrainStep:
         self.run(batch)
 
     # ---------------------------------------------------------------- HIP graphs
-    def capture(self):
-        """Capture the step as HIP graphs over two alternating march buffer sets j = 0, 1:
-        march[j] (AABB + noise + per-part march of static batch j), chain[j][q] and grid_bw[j][q]
-        per part, reduce (parts' MLP grads) and update (Adam + repack).  replay() orchestrates them
-        on streams: part q's chain+grid_bw on stream q, the chain of part q+1 starting when part q's
-        chain ends (so it overlaps part q's grid_bw), and the NEXT step's march on a side stream
-        (it needs neither this step's gradients nor its update).  Splitting at grid_bw also lets the
-        caller time it and run the data-parallel all-reduce between graphs.  Call after at least one
-        eager step (lazy library init happens outside capture)."""
+    def capture(self, host_noise=False):
+        """Capture the step as HIP graphs over two alternating march buffer sets j = 0, 1.
+
+        One part, no collective (the default N=1 step): ONE graph per step ("step": chain -> scatter
+        with the whole optimizer in its launches -> repack); the next step's batch draw + march is a
+        graph of its own on a high-priority side stream, started by a device gate the step graph
+        opens after compositing (gate.hip).  Data parallel (one part): TWO graphs per step around
+        the collective ("dp_pre": repack -> chain -> scatter -> float gradient -> non-finite flag
+        into the shards; "dp_post": flag back -> Adam on this rank's shard (sharded) or everywhere
+        (all-reduce)), the collectives issued stream-ordered between them, the march gated the same
+        way.  The per-stage graphs (march[j], chain[j][q], grid_bw[j][q], finish, update / adam +
+        pack) serve several parts and the steps whose scatter is timed by events (bench).
+        host_noise: the march perturbation is copied from a buffer replay(noise=...) fills instead of
+        drawn from the step's generator (parity tests driving several processes with one draw).
+        Call after at least one eager step (lazy library init happens outside capture)."""
         N = self.cfg.n_rays
         if len(self.mbuf) == 1:
             self.mbuf.append(self._march_buffers())
         self._static = [_packed_batch(torch.zeros(3, N, 3, device=self.dev)) for _ in range(2)]
+        self._host_noise = bool(host_noise)
+        self._static_noise = [torch.zeros(N, device=self.dev) for _ in range(2)] if host_noise else None
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
         nomark = lambda _n: None  # noqa: E731
@@ -667,7 +676,8 @@ class TrainStep:
         def march(j):
             if self.dataset is not None:
                 self._draw(self._static[j], self.mbuf[j])
-            self._march(self._static[j], self.mbuf[j], nomark, prepped=self.dataset is not None)
+            self._march(self._static[j], self.mbuf[j], nomark, prepped=self.dataset is not None,
+                        noise=self._static_noise[j] if host_noise else None)
 
         self.graphs = {
             "march": [cap(lambda j=j: march(j), rng=True) for j in range(2)],
@@ -677,51 +687,69 @@ class TrainStep:
             "finish": [cap(lambda q=q: self._grid_finish(q)) for q in range(P)],
             "reduce": cap(self._reduce_parts) if P > 1 else None,
         }
+        gated = P == 1 and os.environ.get("MFNERF_GATED_MARCH", "1") == "1"
+        signal_at = self._gate_signaller() if gated else None
+        if gated:
+            gp = ptr(self._gate)
+            self.graphs["march_gated"] = [
+                cap(lambda j=j: (call("mfnerf_gate_wait", gp, GATE_TIMEOUT_US, stream()), march(j)), rng=True)
+                for j in range(2)]
+        amp = self._amp_on()
+        self.graphs["pack"] = cap(self._pack)
         if self.shard is not None:
             rank, lo, hi = self.shard
             self.graphs["adam"] = cap(lambda: self._adam(self.g_shard, lo, hi, False))
-            self.graphs["pack"] = cap(self._pack)
         else:
             self.graphs["update"] = cap(self._update)
-            if P == 1:  # no collective between them: one graph, one launch gap less
-                tail = self._finish_update if self._fixed() else lambda: (self._grid_finish(0), self._update())
-                self.graphs["finish_update"] = cap(tail)
-                # and the scatter with it (one graph transition less again) for untimed steps
-                if self._fixed() and self._fused_adam_ok():  # the tables' Adam inside the accumulate
-                    self.graphs["grid_bw_tail"] = [cap(lambda j=j: self._fused_tail(j)) for j in range(2)]
+        if P == 1:
+            # data parallel: the step up to the exchange, then the update after it
+            w = self.shard[2] - self.shard[1] if self.shard is not None else self.n_alloc
+            n_sh = self.n_alloc // w
+
+            def dp_pre(j, mark):
+                self._pack()  # the previous step's all-gathered / updated fp16 weights
+                self._chain(self._static[j], self.mbuf[j], 0, mark)
+                self._grid_bw(self.mbuf[j], 0)
+                self._grid_finish(0)
+                if amp:  # the non-finite flag rides the collective: NaN into every shard's first value
+                    call("mfnerf_flag_to_shards", ptr(self.grads), n_sh, w, ptr(self.finite_status), stream())
+
+            def dp_post():
+                if self.shard is not None:
+                    if amp:
+                        call("mfnerf_flag_from_shard", ptr(self.g_shard), ptr(self.finite_status), stream())
+                    self._adam(self.g_shard, self.shard[1], self.shard[2], False)
                 else:
-                    self.graphs["grid_bw_tail"] = [cap(lambda j=j: (self._grid_bw(self.mbuf[j], 0), tail()))
-                                                   for j in range(2)]
-                if self._gated_ok():
-                    # the whole step as ONE graph: the chain signals a device gate where the host
-                    # used to record the event that starts the next march (gate.hip); the side
-                    # stream's march graph begins by waiting on that gate
-                    self._gate = torch.zeros(2, dtype=torch.int32, device=self.dev)
-                    gp = ptr(self._gate)
-                    fuse = self._fixed() and self._fused_adam_ok()
-
-                    # where in the chain the gate opens: after the stage named.  Default "composite":
-                    # the next draw + march start beside field_bw, whose one wave per SIMD (384 of
-                    # 512 registers) leaves room and issue cycles for the march's waves -- 0.687 ->
-                    # 0.672 ms/step against opening after the whole chain ("field_bw"); "field_fw"
-                    # (beside compositing too) 0.677
-                    gate_at = os.environ.get("MFNERF_GATE_AT", "composite")
-
-                    def signal_at(name):
-                        if name == gate_at:
-                            call("mfnerf_gate_signal", gp, stream())
-
-                    def step(j):
-                        self._chain(self._static[j], self.mbuf[j], 0, signal_at)
-                        if fuse:
-                            self._fused_tail(j)
-                        else:
-                            self._grid_bw(self.mbuf[j], 0)
-                            tail()
-                    self.graphs["step"] = [cap(lambda j=j: step(j)) for j in range(2)]
-                    self.graphs["march_gated"] = [
-                        cap(lambda j=j: (call("mfnerf_gate_wait", gp, GATE_TIMEOUT_US, stream()), march(j)),
-                            rng=True) for j in range(2)]
+                    if amp:
+                        call("mfnerf_flag_from_shard", ptr(self.grads), ptr(self.finite_status), stream())
+                    self._adam(self.grads, 0, self.n_alloc, True)
+            self.graphs["dp_pre"] = [cap(lambda j=j: dp_pre(j, signal_at or nomark)) for j in range(2)]
+            self.graphs["dp_post"] = cap(dp_post)
+        if self.shard is None and P == 1:
+            tail = self._finish_update if self._fixed() else lambda: (self._grid_finish(0), self._update())
+            self.graphs["finish_update"] = cap(tail)
+            fuse = self._fixed() and self._fused_adam_ok()
+            # the scatter with the optimizer (one graph transition less) for untimed steps
+            if fuse:  # the tables' Adam inside the accumulate
+                self.graphs["grid_bw_tail"] = [cap(lambda j=j: self._fused_tail(j)) for j in range(2)]
+            else:
+                self.graphs["grid_bw_tail"] = [cap(lambda j=j: (self._grid_bw(self.mbuf[j], 0), tail()))
+                                               for j in range(2)]
+            if gated:
+                # the whole step as ONE graph: the chain signals the device gate where the host used
+                # to record the event that starts the next march
+                def step(j):
+                    self._chain(self._static[j], self.mbuf[j], 0, signal_at)
+                    if fuse:
+                        self._fused_tail(j)
+                    else:
+                        self._grid_bw(self.mbuf[j], 0)
+                        tail()
+                self.graphs["step"] = [cap(lambda j=j: step(j)) for j in range(2)]
+        if gated and signal_at.count != (4 if self.shard is None else 2):
+            # every gated graph must open the gate exactly once, or each gated march would spin for
+            # GATE_TIMEOUT_US before starting
+            raise RuntimeError(f"gated graphs signalled {signal_at.count} times")
         torch.cuda.synchronize()
         # the next step's march runs beside this step's grid_bw scatter, whose 4096 workgroups would
         # otherwise take every dispatch slot first (the march's small kernels then finish after the
@@ -735,8 +763,30 @@ class TrainStep:
         self._ev_part = [torch.cuda.Event() for _ in range(P)]
         self._parity = 0
         self._primed = False
+        self._stale_pack = False  # a dp_pre step left the repack to the next step's graph
         # where the next step's march starts: under this step's grid_bw (default) or at its start
         self.march_early = os.environ.get("MFNERF_MARCH_EARLY", "0") == "1"
+
+    def _gate_signaller(self):
+        """mark() for the gated graphs: signals the device gate after the chain stage named by
+        MFNERF_GATE_AT (default "composite": the next draw + march start beside field_bw, whose one
+        wave per SIMD leaves room and issue cycles for the march's waves -- 0.687 -> 0.672 ms/step
+        against opening after the whole chain ("field_bw"); "field_fw" 0.677); counts its signals."""
+        self._gate = torch.zeros(2, dtype=torch.int32, device=self.dev)
+        gp = ptr(self._gate)
+        gate_at = os.environ.get("MFNERF_GATE_AT", "composite")
+        if gate_at not in ("grid_fw", "field_fw", "composite", "field_bw"):
+            raise ValueError(f"MFNERF_GATE_AT={gate_at!r}: one of grid_fw, field_fw, composite, field_bw")
+        # with the distortion loss the chain composites in two stages: the gate opens after the
+        # second ("composite_bw"), the same place as after the fused kernel
+        name_ = "composite_bw" if gate_at == "composite" and self.cfg.lambda_distortion > 0 else gate_at
+
+        def signal_at(name):
+            if name == name_:
+                call("mfnerf_gate_signal", gp, stream())
+                signal_at.count += 1
+        signal_at.count = 0
+        return signal_at
 
     def _stage_batch(self, j, batch):
         dst = self._static[j]
@@ -746,27 +796,36 @@ class TrainStep:
             for d, s_ in zip((dst.rays_o, dst.rays_d, dst.rgb), (batch.rays_o, batch.rays_d, batch.rgb)):
                 d.copy_(s_)
 
-    def _march_on_side(self, j, batch, after, gated=False):
-        """Copy batch into static set j and march it on the side stream once `after` (an event on
-        the main stream) has passed: set j's buffers were last read two steps back.  gated: the
-        march graph first waits for the step graph's gate signal (placement only)."""
+    def _march_on_side(self, j, batch, after, gated=False, noise=None):
+        """Copy batch (and, captured with host_noise, its perturbation) into static set j and march
+        it on the side stream once `after` (an event on the main stream) has passed: set j's buffers
+        were last read two steps back.  gated: the march graph first waits for the step graph's
+        gate signal (placement only)."""
         self._side.wait_event(after)
         with torch.cuda.stream(self._side):
             if batch is not None:
                 self._stage_batch(j, batch)
+            if self._host_noise:
+                if noise is None:
+                    raise ValueError("captured with host_noise: pass noise= / next_noise= to replay()")
+                self._static_noise[j].copy_(noise)
             self.graphs["march_gated" if gated else "march"][j].replay()
             self._ev_march[j].record(self._side)
 
-    def replay(self, batch: Batch = None, exchange=None, grid_bw_events=None, next_batch=None, prefetch=None):
+    def replay(self, batch: Batch = None, exchange=None, grid_bw_events=None, next_batch=None, prefetch=None,
+               noise=None, next_noise=None):
         """One training step from the captured graphs (the kernels of run()).  With next_batch (or,
         with an attached dataset, prefetch=True, its default), the next step's march is issued on
         the side stream to overlap this step; the next replay() must then be called with that batch
         (or, with a dataset, the next replay() trains on the batch already drawn).  Pass
         prefetch=False before anything that must precede the next march (an occupancy refresh).
+        Data parallel: sharded (shard_optimizer) or exchange=dp.allreduce_mean_.
         grid_bw_events: optional (start, [end per part]) timing events -- start before part 0's
-        grid_bw, end after each part's grid_bw."""
+        grid_bw, end after each part's grid_bw (that step runs the per-stage graphs).
+        noise / next_noise: the perturbations of batch / next_batch (capture(host_noise=True))."""
+        from . import dp
         g, j, P = self.graphs, self._parity, self.n_parts
-        fuse_tail = g.get("finish_update") is not None and exchange is None
+        dp_mode = self.shard is not None or exchange is not None
         if self.dataset is not None:
             batch = None
             if prefetch is None:
@@ -778,22 +837,40 @@ class TrainStep:
         main = torch.cuda.current_stream()
         self._ev_start.record(main)
         if not self._primed:
-            self._march_on_side(j, batch, self._ev_start)
-        if fuse_tail and grid_bw_events is None and g.get("step") is not None and prefetch and not self.march_early:
-            # one graph for the step; the next march (side stream) starts when its gate sees the
-            # chain's signal -- set 1-j was last read by the previous step, all before _ev_start
+            self._march_on_side(j, batch, self._ev_start, noise=noise)
+        one_graph = (P == 1 and grid_bw_events is None and prefetch and not self.march_early
+                     and g.get("march_gated") is not None)
+        if one_graph and (dp_mode or g.get("step") is not None):
+            # set 1-j was last read by the previous step, all of which precedes _ev_start
             main.wait_event(self._ev_march[j])
             self._use(self.mbuf[j])
             self.last_batch = self._static[j]
             self.adam_step += 1
-            g["step"][j].replay()
-            self._march_on_side(1 - j, next_batch, self._ev_start, gated=True)
+            if not dp_mode:  # one graph for the step; the next march starts at its gate signal
+                g["step"][j].replay()
+                self._march_on_side(1 - j, next_batch, self._ev_start, gated=True, noise=next_noise)
+            else:
+                # [repack] chain, scatter, float gradient, flag -> collective -> Adam -> (all-gather)
+                g["dp_pre"][j].replay()
+                self._march_on_side(1 - j, next_batch, self._ev_start, gated=True, noise=next_noise)
+                if self.shard is not None:
+                    dp.reduce_scatter_mean_(self.g_shard, self.grads)
+                    g["dp_post"].replay()
+                    dp.all_gather_(self.p16, self.shard[0])
+                else:
+                    exchange(self.grads)
+                    g["dp_post"].replay()
+                self._stale_pack = True  # the next step's dp_pre (or the pack graph) repacks
             self._parity = 1 - j
             self._primed = True
             return
+        fuse_tail = g.get("finish_update") is not None and not dp_mode
+        if self._stale_pack:
+            g["pack"].replay()
+            self._stale_pack = False
         early = prefetch and self.march_early
         if early:  # set 1-j was last read by the previous step, all of which precedes _ev_start
-            self._march_on_side(1 - j, next_batch, self._ev_start)
+            self._march_on_side(1 - j, next_batch, self._ev_start, noise=next_noise)
         main.wait_event(self._ev_march[j])
         self._use(self.mbuf[j])
         self.last_batch = self._static[j]
@@ -807,7 +884,7 @@ class TrainStep:
                 if q == P - 1 and prefetch and not early:
                     # set 1-j was last read by the previous step, which this chain follows; waiting
                     # for the last chain puts the march under the grid_bw scatters, not the chains
-                    self._march_on_side(1 - j, next_batch, self._ev_chain[q])
+                    self._march_on_side(1 - j, next_batch, self._ev_chain[q], noise=next_noise)
                 if fuse_tail and grid_bw_events is None:
                     # P == 1: scatter + convert/Adam + repack as one graph (no event needed between)
                     self.adam_step += 1

@@ -8,7 +8,11 @@ the step.
   1000 steps (train.py:136-142, datasets/base.py:17-20), held on the device (Adam reads it);
 * fp16 loss scaling -- PL precision=16 (train.py:287) = torch GradScaler: the MLP backward runs in
   fp16 at the dynamic loss scale (init 2^16, x2 after 2000 clean steps, x0.5 on an overflow) and
-  un-scales inside the kernel; a step whose gradient is not finite is skipped.  All of it on the
+  un-scales inside the kernel; a step whose gradient is not finite is skipped.  Deviation: tcnn
+  also multiplies the MLP backward by its own fixed loss_scale of 128, so the reference's fp16
+  backward runs at 128x the GradScaler's scale; here field_bw runs at the GradScaler's scale alone,
+  so overflow/backoff dynamics start from a 128x lower effective scale (skip-count parity is
+  unpinned: the parity fixtures come from an fp32 reference and assert zero skips).  All of it on the
   device (mfnerf_field_bw's non-finite flag and device scale, the optimizer pass's last workgroup
   running GradScaler.update(); mfnerf_amp_state) -- no host synchronisation;
 * metrics -- train loss / PSNR / rm_s (train.py:178-189), test PSNR with the test-time renderer
@@ -216,6 +220,9 @@ class Trainer:
         st.v.zero_()
         st.step_dev.zero_()
         st.adam_step = 0
+        # ... and a fresh GradScaler (PL precision=16 builds it at init 2^16, train.py:287): the
+        # loss scale, growth tracker and skip count do not carry over
+        st.reset_loss_scale()
         if "model.density_grid" in sd:
             st.density_grid.copy_(sd["model.density_grid"].to(st.dev))
         if "model.density_bitfield" in sd:

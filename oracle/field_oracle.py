@@ -126,30 +126,62 @@ def grid_index(layout, l, gx, gy, gz):
     return index % size
 
 
-def grid_encode(x, params, layout):
-    """x: (N,3) fp32 in [0,1]; params: (n_params,) fp32 table -> (N, L*F) fp32.
-    Per level: pos = fmaf(scale, x, 0.5); g = floor(pos); w = pos - g (Linear);
-    out = sum over the 8 corners of prod_d (bit_d ? w_d : 1-w_d) * table[index]."""
-    N = x.shape[0]
-    F = layout.F
-    table = params.view(-1, F)
-    outs = []
+def _corners(x, layout):
+    """Per (level, corner): (flat table row index (N,) i64, trilinear weight (N,) f32)."""
+    out = []
     for l in range(layout.L):
         # fmaf(scale, x, 0.5) in fp32: evaluate in fp64 and round once
         pos = (x.double() * float(layout.scales[l]) + 0.5).float()
         g = torch.floor(pos)
         w = pos - g
         gi = g.to(torch.int64)
-        acc = torch.zeros(N, F, dtype=torch.float32, device=x.device)
+        lv = []
         for c in range(8):
             gc = [gi[:, d] + ((c >> d) & 1) for d in range(3)]
-            wt = torch.ones(N, dtype=torch.float32, device=x.device)
+            wt = torch.ones(x.shape[0], dtype=torch.float32, device=x.device)
             for d in range(3):
                 wt = wt * (w[:, d] if (c >> d) & 1 else (1 - w[:, d]))
-            idx = grid_index(layout, l, gc[0], gc[1], gc[2]) + layout.offsets[l]
-            acc = acc + wt[:, None] * table[idx]
-        outs.append(acc)
-    return torch.cat(outs, 1)
+            lv.append((grid_index(layout, l, gc[0], gc[1], gc[2]) + layout.offsets[l], wt))
+        out.append(lv)
+    return out
+
+
+class _GridEncode(torch.autograd.Function):
+    """The encoding with the table gradient scattered into ONE buffer (index_add_ per level and
+    corner).  Autograd through `table[idx]` would materialise a zero table-sized gradient for each of
+    the L*8 gathers (128 x 45 MB per backward at the Lego layout) and sum them."""
+
+    @staticmethod
+    def forward(ctx, params, x, layout):
+        F = layout.F
+        table = params.view(-1, F)
+        cs = _corners(x, layout)
+        outs = []
+        for lv in cs:
+            acc = torch.zeros(x.shape[0], F, dtype=torch.float32, device=x.device)
+            for idx, wt in lv:
+                acc = acc + wt[:, None] * table[idx]
+            outs.append(acc)
+        ctx.cs, ctx.F, ctx.n, ctx.dtype = cs, F, params.numel(), params.dtype
+        return torch.cat(outs, 1)
+
+    @staticmethod
+    def backward(ctx, dout):
+        F = ctx.F
+        grad = torch.zeros(ctx.n // F, F, dtype=ctx.dtype, device=dout.device)
+        for l, lv in enumerate(ctx.cs):
+            dl = dout[:, l * F:(l + 1) * F]
+            for idx, wt in lv:
+                grad.index_add_(0, idx, (wt[:, None] * dl).to(ctx.dtype))
+        return grad.view(-1), None, None
+
+
+def grid_encode(x, params, layout):
+    """x: (N,3) fp32 in [0,1]; params: (n_params,) fp32 table -> (N, L*F) fp32.
+    Per level: pos = fmaf(scale, x, 0.5); g = floor(pos); w = pos - g (Linear);
+    out = sum over the 8 corners of prod_d (bit_d ? w_d : 1-w_d) * table[index].
+    Differentiable in params (not in x: the encoding's input needs no gradient here)."""
+    return _GridEncode.apply(params, x.detach(), layout)
 
 
 def sh4(d01):

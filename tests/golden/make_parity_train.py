@@ -9,8 +9,9 @@ tests/test_gpu_parity_train.py trains this repo's fused MI355X step from the sam
 perturbations and checks the held-out PSNR against these numbers (north_star: within 0.2 dB).
 
 Only data is written (numbers); the reference never leaves this container.
-    python tests/golden/make_parity_train.py          (needs /root/reference; CPU, ~7 minutes)
+    python tests/golden/make_parity_train.py          (needs /root/reference; CPU, ~15 minutes on 1 thread)
     python tests/golden/make_parity_train.py --seed 3 (batch/perturbation seed 3 -> parity_train_s3.json)
+    MFNERF_PARITY_THREADS=1 runs the 8 seeds side by side on an 8-core host
 """
 import json
 import os
@@ -42,7 +43,7 @@ def main(seed=0):
     from models import rendering
     from models.networks import NGP
 
-    torch.set_num_threads(os.cpu_count() or 1)
+    torch.set_num_threads(int(os.environ.get("MFNERF_PARITY_THREADS", os.cpu_count() or 1)))
     cfg = PP.config()
     model = NGP(scale=cfg.scale, hparams=HP)
     xyz0, rgb0 = PP.init_params(cfg)
@@ -58,6 +59,9 @@ def main(seed=0):
     t0 = time.time()
     real_rand_like = torch.rand_like
     for step in range(PP.STEPS):
+        if step % PP.STEPS_PER_EPOCH == 0:  # train.py:140-142: the scheduler steps once per epoch
+            for grp in opt.param_groups:
+                grp["lr"] = PP.lr_at(step)
         o, d, rgb = PP.batch(train, step, seed)
         nz = PP.noise(step, seed)
         torch.rand_like = lambda t, *a, **k: nz.clone() if t.shape == nz.shape else real_rand_like(t, *a, **k)
@@ -83,7 +87,8 @@ def main(seed=0):
             rt = rendering.render(model, o, dd, test_time=True)
             views.append(PP.psnr(rt["rgb"], img))
     out = {"protocol": {"W": PP.W, "n_train": PP.N_TRAIN, "n_test": PP.N_TEST, "n_rays": PP.N_RAYS,
-                        "steps": PP.STEPS, "lr": PP.LR, "init_seed": PP.INIT_SEED, "run_seed": seed,
+                        "steps": PP.STEPS, "epochs": PP.EPOCHS, "steps_per_epoch": PP.STEPS_PER_EPOCH,
+                        "lr": PP.LR, "lr_schedule": "cosine per epoch, eta_min lr/100 (train.py:136-142)", "init_seed": PP.INIT_SEED, "run_seed": seed,
                         "field": "Hash L16 F2 T2^19 rgb64x2",
                         "occupancy": "fixed ball union", "precision": "fp32 (reference on CPU, oracle kernels)"},
            "history": hist, "test_psnr_views": views, "test_psnr": sum(views) / len(views),

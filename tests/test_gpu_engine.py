@@ -271,3 +271,53 @@ def test_partitioned_accumulate_with_fused_adam_matches_unfused(gpu, kw, skip, m
     assert not bool(ws[:nc].any()) and not bool(ref_ws[:nc].any()) and not bool(st.grads.any())
     if not skip:
         assert not torch.equal(st.params, snap["params"])
+
+
+def test_gated_replay_with_distortion_loss_keeps_the_gate_in_step(gpu):
+    """--distortion_loss_w > 0 composites in two stages (composite_fw / composite_bw, no fused
+    kernel): the step graph must still open the gate once per step, else every gated march would spin
+    for GATE_TIMEOUT_US (2 ms) first.  Replays stay bit-identical to eager steps."""
+    K = 5
+    a, b = _make(gpu, 1, lambda_distortion=1e-3), _make(gpu, 1, lambda_distortion=1e-3)
+    batches = a.make_batches(K + 1, seed=9)
+    for k in range(K):
+        b.run(batches[k])
+    a.run(batches[0])
+    a.capture()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for k in range(1, K):
+        a.replay(batches[k], next_batch=batches[k + 1] if k + 1 < K else None)
+    t1.record()
+    torch.cuda.synchronize()
+    assert a._gate.tolist() == [K - 1, K - 1]       # every signal waited for, no wait timed out
+    assert t0.elapsed_time(t1) < (K - 1) * engine.GATE_TIMEOUT_US / 1000
+    assert torch.equal(a.params, b.params) and torch.equal(a.p16, b.p16)
+
+
+def test_gate_position_is_validated(gpu, monkeypatch):
+    st = _make(gpu, 1)
+    st.run(st.make_batches(1, seed=1)[0])
+    monkeypatch.setenv("MFNERF_GATE_AT", "compositing")
+    with pytest.raises(ValueError):
+        st.capture()
+
+
+@pytest.mark.parametrize("log2_T", [20, 21])
+def test_large_tables_train_with_or_without_partitions(gpu, log2_T):
+    """--T 20 / 21 (opt.py:78): layouts beyond the partitioned scatter's limits take the fixed-point
+    atomic scatter instead of failing at construction; eager and replayed steps match bit for bit."""
+    a, b = _make(gpu, 1, log2_T=log2_T), _make(gpu, 1, log2_T=log2_T)
+    batches = a.make_batches(5, seed=11)
+    for k in range(4):
+        b.run(batches[k])
+    a.run(batches[0])
+    a.capture()
+    for k in range(1, 4):
+        a.replay(batches[k], next_batch=batches[k + 1])
+    torch.cuda.synchronize()
+    assert torch.isfinite(a.params).all() and a.skipped_steps() == 0
+    assert torch.equal(a.params, b.params) and torch.equal(a.p16, b.p16)
+    lay = a.layout
+    supported = load().mfnerf_grid_encode_bw_binned_workspace(a.desc, a._bin_slots()) >= 0
+    assert a._binned() == supported

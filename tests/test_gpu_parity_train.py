@@ -1,8 +1,8 @@
 """End-to-end training parity with the reference (north_star: "PSNR within 0.2 dB of reference").
 The Lego images are not in this image, so the comparison runs the protocol of
 tests/parity_protocol.py: BASELINE config 1's shape (64x64 views of the analytic ball scene, 256
-rays per batch, Lego's default field), the same initial weights, ray batches and march
-perturbations on both sides.  tests/golden/parity_train.json holds the REFERENCE side: its own
+rays per batch, Lego's default field), train.py's per-epoch cosine schedule over 10 short epochs,
+16 held-out views, the same initial weights, ray batches and march perturbations on both sides.  tests/golden/parity_train.json holds the REFERENCE side: its own
 render / NeRFLoss / NGP driven in fp32 on the CPU with the oracle kernels
 (tests/golden/make_parity_train.py).  Here this repo's fused MI355X step (fp16 MFMA field, dynamic
 loss scale, fixed-point table gradient, HIP Adam) trains from the same start, and the held-out
@@ -23,6 +23,9 @@ from mfnerf.rendering import render
 pytestmark = pytest.mark.gpu
 
 GOLDEN = os.path.join(ROOT, "tests", "golden", "parity_train.json")
+# seed-averaged relative difference of the two sides' logged batch losses: over the whole run
+# (mean) and at any logged step (max)
+LOSS_TOL_MEAN, LOSS_TOL_MAX = 0.05, 0.15
 
 
 def _ngp(st, cfg):
@@ -55,6 +58,8 @@ def _train(gpu, seed):
     train, test = PP.scene()
     losses = {}
     for step in range(PP.STEPS):
+        if step % PP.STEPS_PER_EPOCH == 0:
+            st.set_lr(PP.lr_at(step))
         o, d, rgb = PP.batch(train, step, seed)
         b = engine.Batch(o.to(gpu), d.to(gpu), rgb.to(gpu))
         st.run(b, noise=PP.noise(step, seed).to(gpu))
@@ -82,34 +87,34 @@ def _reference_runs():
 
 
 def test_training_psnr_matches_reference(gpu):
-    """Paired runs (same seeds on both sides).  At this horizon (400 steps of 256 rays) the held-out
-    PSNR of ONE run swings by ~1.4 dB (std over batch/perturbation seeds, on either side: measured
-    with tools/parity_spread.py), far more than the 0.2-dB north-star bound -- any two
-    implementations that differ in the last bit of the table gradient land anywhere in that band.
-    So the check is statistical: the mean over the K seeds of (ours - reference) must be within
-    0.2 dB plus two standard errors of that mean; every run must be finite, skip no step, and
-    track the reference's loss curve."""
+    """Paired runs (same seeds on both sides).  ONE run's held-out PSNR still varies from seed to
+    seed (0.16 dB sd over 8 seeds on this side at this protocol, tools/parity_spread.py; 0.65 dB
+    without the schedule's decay), so the check is statistical: the mean over the K >= 8 seeds of
+    (ours - reference) must be within 0.2 dB plus two standard errors of that mean, and that bound
+    itself must stay <= 0.5 dB (a systematic 0.5-dB regression fails); every run must be finite,
+    skip no step, and track the reference's loss curve over the whole run."""
     refs = _reference_runs()
-    diffs = []
+    assert len(refs) >= 8, "the protocol's reference side has fewer than 8 seeds"
+    diffs, rels = [], []
     for ref in refs:
         seed = ref["protocol"].get("run_seed", 0)
         assert ref["protocol"]["steps"] == PP.STEPS and ref["protocol"]["n_rays"] == PP.N_RAYS
+        assert ref["protocol"]["steps_per_epoch"] == PP.STEPS_PER_EPOCH and ref["protocol"]["n_test"] == PP.N_TEST
         got, views, losses, skipped = _train(gpu, seed)
-        print(f"\nPARITY seed {seed}: held-out PSNR ours {got:.3f} {[round(v, 2) for v in views]} reference "
-              f"{ref['test_psnr']:.3f} {[round(v, 2) for v in ref['test_psnr_views']]} skipped steps {skipped}\n"
-              "  loss (ours / reference):",
-              [(h["step"], round(losses[h["step"]], 5), round(h["loss"], 5)) for h in ref["history"]])
+        print(f"\nPARITY seed {seed}: held-out PSNR ours {got:.3f} reference {ref['test_psnr']:.3f} "
+              f"(diff {got - ref['test_psnr']:+.3f}) skipped steps {skipped}")
         assert skipped == 0 and got == got
         diffs.append(got - ref["test_psnr"])
-        # the loss curves agree while the trajectories are still together (same batches: the first
-        # 100 steps agree to a few 1e-3; from ~150 steps on single-batch losses drift apart with the
-        # trajectories, both ways, by 10-30 %)
-        rel = [abs(losses[h["step"]] - h["loss"]) / h["loss"] for h in ref["history"]]
-        early = rel[:len(rel) // 4]
-        assert sum(early) / len(early) < 0.02, (seed, rel)
+        rels.append([abs(losses[h["step"]] - h["loss"]) / h["loss"] for h in ref["history"]])
     k = len(diffs)
     mean = sum(diffs) / k
-    sd = (sum((d - mean) ** 2 for d in diffs) / (k - 1)) ** 0.5 if k > 1 else 0.0
+    sd = (sum((d - mean) ** 2 for d in diffs) / (k - 1)) ** 0.5
     tol = 0.2 + 2.0 * sd / k ** 0.5
-    print(f"PARITY {k} seeds: mean(ours - reference) {mean:+.3f} dB, sd {sd:.3f}, bound {tol:.3f}")
+    # the loss curves over the WHOLE log: the per-batch losses of the two trajectories, logged
+    # every LOG_EVERY steps on the same batches, averaged over seeds
+    curve = [sum(r[i] for r in rels) / k for i in range(len(rels[0]))]
+    print(f"PARITY {k} seeds: mean(ours - reference) {mean:+.3f} dB, sd {sd:.3f}, bound {tol:.3f} dB; "
+          f"loss rel. diff mean {sum(curve) / len(curve):.4f} max {max(curve):.4f}")
+    assert tol <= 0.5, (diffs, tol)
     assert abs(mean) < tol, (diffs, tol)
+    assert sum(curve) / len(curve) < LOSS_TOL_MEAN and max(curve) < LOSS_TOL_MAX, curve

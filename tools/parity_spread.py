@@ -20,6 +20,8 @@ def run(seed, dev):
     st.set_occupancy(PP.density_grid())
     train, test = PP.scene()
     for step in range(PP.STEPS):
+        if step % PP.STEPS_PER_EPOCH == 0:
+            st.set_lr(PP.lr_at(step))
         o, d, rgb = PP.batch(train, step, seed)
         st.run(engine.Batch(o.to(dev), d.to(dev), rgb.to(dev)), noise=PP.noise(step, seed).to(dev))
     model = _ngp(st, cfg)
@@ -39,4 +41,5 @@ if __name__ == "__main__":
     ps = [run(s, dev) for s in range(k)]
     m = sum(ps) / k
     sd = (sum((p - m) ** 2 for p in ps) / max(1, k - 1)) ** 0.5
-    print("PSNR per seed", [round(p, 3) for p in ps], "mean", round(m, 3), "std", round(sd, 3), flush=True)
+    print(f"epochs {PP.EPOCHS} x {PP.STEPS_PER_EPOCH} steps, {PP.N_TEST} views: PSNR per seed",
+          [round(p, 3) for p in ps], "mean", round(m, 3), "std", round(sd, 3), flush=True)
