@@ -918,17 +918,12 @@ int check_desc(const mfnerf_grid_desc* d, const char* what) {
 // addresses, tools/lds_atomic_probe.hip -- 20x ds_add_f32), then stores the image once.  The image
 // holds one 64-bit word per entry: both features' sums in the table's int32 fixed-point unit,
 // packed f1 * 2^32 + f0 (exact in two's complement, order-free: bit-reproducible), each weighted
-// contribution rounded once to the unit -- 2 LDS atomics per pair record.  (MFN_ACC32=0 keeps an
-// int64 image per feature at 2^32 x the unit, rounded once per entry: 4 atomics and a float ->
-// int64 conversion per record, 349 vs 316 us for the whole scatter.)  Passes: count (per-block bin
-// histogram; in the same launch as the dense coarse levels' scatter, which stays on grid_bw_body:
-// few hot lines, private copies, in-wave run merging -- the two overlap) -> scan (per bin over
-// blocks) -> scatter (records) -> accumulate.
+// contribution rounded once to the unit -- 2 LDS atomics per pair record (an int64 image per
+// feature at 2^32 x the unit, 4 atomics and a float -> int64 conversion per record, measured 349 vs
+// 316 us for the whole scatter in round 2).  Passes: scatter (records into fixed per-(partition,
+// unit) slots) -> accumulate (one workgroup per partition).
 // partitions of 2^shift entries, shift in [MIN_BIN_SHIFT, MAX_BIN_SHIFT] chosen per layout so that
-// there are >= ~1024 partitions (4 workgroups per CU); 2^11 entries = 32 KB of int64 pairs
-#ifndef MFN_ACC32
-#define MFN_ACC32 2  // 2: packed int32 pairs (one 64-bit LDS word per entry); 1: int32 words; 0: int64 at 2^32 x the scale
-#endif
+// there are >= ~1024 partitions (4 workgroups per CU); 2^11 entries = 16 KB of packed int32 pairs
 constexpr int MIN_BIN_SHIFT = 8, MAX_BIN_SHIFT = 11, MAX_BIN_ENTRIES = 1 << MAX_BIN_SHIFT;
 constexpr int MAX_BINS = 4096;
 
@@ -970,11 +965,7 @@ __device__ __forceinline__ void level_records_geo(const mfnerf_grid_desc& D, con
     const uint32_t fxq = min(32767u, (uint32_t)rintf(Lg.w[0] * 32768.0f)) << 17;
     const uint32_t ones = (uint32_t)__builtin_ctz(~Lg.g[0]);  // trailing ones of x
     const bool pair_hash = P.pairable[l] && ones < 15;
-#if MFN_ACC32
     const float s0 = g0 * fs, s1 = g1 * fs;  // in the table's int32 fixed-point units
-#else
-    const float s0 = g0 * fs * 4294967296.0f, s1 = g1 * fs * 4294967296.0f;  // exact: powers of two
-#endif
     const uint32_t mask = (1u << P.shift) - 1;
 #pragma unroll
     for (int yz = 0; yz < 4; ++yz) {
@@ -1107,10 +1098,18 @@ __host__ __device__ __forceinline__ int64_t slot_size(int64_t nn, const BinPlan&
 }
 
 // pass 1: unit u (one 1024-thread workgroup) walks its samples, staged in registers, level by level
-// in tiles of up to 2048 samples: the tile's records are counted per bin of the level's table (LDS
-// atomics give each its rank), sorted by bin in LDS and stored as one contiguous run per bin in the
-// unit's slot of the bin (~30 records per run at the Lego config: whole-line stores).
-template <int MAXB>
+// in tiles of up to 2048 samples.  Per level, ONE pass computes the tile's records into registers
+// (8 per thread: 2 samples x 4 pair rows, or 1 sample x 8 single records), each taking its rank in
+// its bin from an LDS counter; one wave scans the bin counts; the records are placed sorted by bin
+// into an LDS stage; the stage is stored as one contiguous run per bin into the unit's slot of the
+// bin (~30 records per run at the Lego config: whole-line stores) while the NEXT level counts.  Three
+// barriers per level (count | scan | place), the store overlapping the next count.
+struct BinRec {
+    uint3 r;
+    uint32_t meta;  // bin in the table (bits 0-15) | rank in the bin's run (bits 16-31); ~0u: none
+};
+
+template <int MAXB, bool PAIR>
 __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __restrict__ X, int64_t n,
                                                                  const int32_t* __restrict__ n_dev, float x_min,
                                                                  float x_range, const mfnerf_grid_desc D,
@@ -1119,21 +1118,18 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                                                                  uint3* __restrict__ rec, int32_t* __restrict__ scnt,
                                                                  uint32_t* __restrict__ smax,
                                                                  int32_t* __restrict__ ovf, int64_t n_slots) {
+    constexpr int SPT = PAIR ? 2 : 1;  // samples per thread per tile
     __shared__ int cursor[MAX_BINS];
-    uint32_t rmax = 0u;  // largest |a|, |b| of this thread's records (float bits order as uints)
-    __shared__ int thist[MAX_TBINS], toff[MAX_TBINS], gdst[MAX_TBINS];
-#ifndef MFN_STAGE_SOA
-#define MFN_STAGE_SOA 0  // 1: staged records as three u32 arrays (measured neutral: 0.6851 vs 0.6845 ms/step)
-#endif
-#if MFN_STAGE_SOA
-    __shared__ uint32_t stage_x[SC_STAGE], stage_y[SC_STAGE], stage_z[SC_STAGE];
-#else
+    __shared__ int hist[MAX_TBINS], toff[MAX_TBINS], gdst[2][MAX_TBINS];
     __shared__ uint3 stage[SC_STAGE];
-#endif
     __shared__ uint16_t sbin[SC_STAGE];
     __shared__ float fs_s[MFN_MAX_LEVELS];
+    __shared__ int s_total[2];
+    uint32_t rmax = 0u;  // largest |a|, |b| of this thread's records (float bits order as uints)
     load_fixed_scales(D, level_l1, fs_s);
     for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x) cursor[b] = 0;
+    for (int b = threadIdx.x; b < MAX_TBINS; b += blockDim.x) hist[b] = 0;
+    if (threadIdx.x < 2) s_total[threadIdx.x] = 0;
     __syncthreads();
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     // slots sized for at most the workspace's count: beyond it a slot may overflow (-> atomics)
@@ -1143,97 +1139,106 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
     const int u = blockIdx.x;
     const int64_t n_chunks = (nn + 15) / 16;
     const int64_t m = n_chunks > u ? ((n_chunks - 1 - u) / UNITS + 1) * 16 : 0;  // this unit's sample slots
-    const int spt = P.pair_ok ? 2 : 1;  // samples per thread per tile: <= 8 records each per level
-    for (int64_t base = 0; base < m; base += (int64_t)spt * SC_THREADS) {
-        StagedSample<MAXB> S[2];
-        bool live[2] = {false, false};
+    // the store of the staged level (prev_b0: its table's first bin; parity: its gdst buffer)
+    int prev_b0 = -1, par = 0;
+    auto store_prev = [&]() {
+        if (prev_b0 < 0) return;
+        const int total = s_total[par ^ 1];
+        const int* gd = gdst[par ^ 1];
+        for (int k = threadIdx.x; k < total; k += SC_THREADS) {
+            const int lb = sbin[k];
+            const int pos = gd[lb] + k;  // position in the unit's slot of the bin
+            if (pos < slot) {
+                uint3* dst = rec + ((int64_t)(prev_b0 + lb) * UNITS + u) * slot + pos;
+                const uint3 r = stage[k];
+                // nontemporal: streamed once here, read once by the accumulate
+                __builtin_nontemporal_store(r.x, &dst->x);
+                __builtin_nontemporal_store(r.y, &dst->y);
+                __builtin_nontemporal_store(r.z, &dst->z);
+            }
+        }
+    };
+    for (int64_t base = 0; base < m; base += (int64_t)SPT * SC_THREADS) {
+        StagedSample<MAXB> S[SPT];
+        bool live[SPT];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < SPT; ++q) {
             const int64_t k = base + (int64_t)q * SC_THREADS + threadIdx.x;
             const int64_t i = ((k >> 4) * UNITS + u) * 16 + (k & 15);  // chunk k/16 of the unit
-            live[q] = q < spt && k < m && i < nn;
+            live[q] = k < m && i < nn;
             if (live[q]) stage_sample(D, P, X, x_min, x_range, dy, i, S[q]);
         }
         for (int j = 0; j < P.n_binned; ++j) {
             const int t = P.table_of[P.level[j]];
             const int b0 = P.t_bin0[t], tb = P.t_bin0[t + 1] - b0;
-            for (int k = threadIdx.x; k < tb; k += SC_THREADS) thist[k] = 0;
-            SampleLevel Q[2];
+            // count: each record computed once, ranked in its bin by the LDS counter
+            BinRec R[8];
 #pragma unroll
-            for (int q = 0; q < 2; ++q) Q[q] = sample_level(D, P, S[q], j);
-            __syncthreads();
-            // the records are computed twice (ALU is cheap): once to count them per bin, once after
-            // the scan to place them, each at an LDS-atomic cursor of its bin -- the order inside a
-            // bin's run is arbitrary, which the accumulate's exact integer sum does not see.  No
-            // per-record state stays in registers between the passes.
+            for (int k = 0; k < 8; ++k) R[k].meta = ~0u;
 #pragma unroll
-            for (int q = 0; q < 2; ++q)
-                if (live[q])
-                    staged_records(D, P, S[q], Q[q], fs_s, j, [&](int, int bin, uint3) {
-                        if (bin >= 0) atomicAdd(&thist[bin - b0], 1);
-                    });
-            __syncthreads();
-            // bins -> sorted tile offsets (toff); a run's k-th record goes to its slot position gdst + k
-            const int cnt = (int)threadIdx.x < tb ? thist[threadIdx.x] : 0;
-            const int total = wave_block_scan(cnt, toff);
-            if ((int)threadIdx.x < tb) {
-                const int c = cursor[b0 + threadIdx.x];
-                gdst[threadIdx.x] = c - toff[threadIdx.x];
-                cursor[b0 + threadIdx.x] = c + cnt;
-                thist[threadIdx.x] = toff[threadIdx.x];  // the placement cursors
+            for (int q = 0; q < SPT; ++q) {
+                const SampleLevel Q = sample_level(D, P, S[q], j);
+                if (live[q] && Q.live)
+                    level_records(D, P, j, S[q].x, S[q].y, S[q].z, Q.g0, Q.g1, fs_s[P.level[j]],
+                                  [&](int sl, int bin, uint3 r) {
+                                      // PAIR: slot 2 yz + 1 never holds a record (pairs never straddle)
+                                      const int k = PAIR ? 4 * q + (sl >> 1) : sl;
+                                      if (bin < 0 || (PAIR && (sl & 1))) return;
+                                      const int lb = bin - b0;
+                                      R[k].r = r;
+                                      R[k].meta = (uint32_t)lb | ((uint32_t)atomicAdd(&hist[lb], 1) << 16);
+                                      rmax = max(rmax, max(r.y & 0x7fffffffu, r.z & 0x7fffffffu));
+                                  });
             }
+            store_prev();  // the previous level's sorted stage, beside this level's counting
             __syncthreads();
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-                if (live[q])
-                    staged_records(D, P, S[q], Q[q], fs_s, j, [&](int, int bin, uint3 r) {
-                        if (bin < 0) return;
-                        rmax = max(rmax, max(r.y & 0x7fffffffu, r.z & 0x7fffffffu));  // |float| bits order
-                        const int lb = bin - b0;
-                        const int p = atomicAdd(&thist[lb], 1);
-#if MFN_STAGE_SOA
-                        stage_x[p] = r.x;
-                        stage_y[p] = r.y;
-                        stage_z[p] = r.z;
-#else
-                        stage[p] = r;
-#endif
-                        sbin[p] = (uint16_t)lb;
-                    });
-            __syncthreads();
-            for (int k = threadIdx.x; k < total; k += SC_THREADS) {
-                const int lb = sbin[k];
-                const int pos = gdst[lb] + k;  // position in the unit's slot of the bin
-#ifndef MFN_REC_STORE
-#define MFN_REC_STORE 1  // 1: nontemporal record stores (streamed once, read once by the accumulate); 3: as one dwordx3
-#endif
-                if (pos < slot) {
-                    uint3* dst = rec + ((int64_t)(b0 + lb) * UNITS + u) * slot + pos;
-#if MFN_STAGE_SOA
-                    const uint3 r = make_uint3(stage_x[k], stage_y[k], stage_z[k]);
-#else
-                    const uint3 r = stage[k];
-#endif
-#if MFN_REC_STORE == 0
-                    *dst = r;
-#elif MFN_REC_STORE == 1
-                    __builtin_nontemporal_store(r.x, &dst->x);
-                    __builtin_nontemporal_store(r.y, &dst->y);
-                    __builtin_nontemporal_store(r.z, &dst->z);
-#elif MFN_REC_STORE == 3
-                    // one 12-B nontemporal store per record (global_store_dwordx3 nt)
-                    typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
-                    typedef u32x3 u32x3_a4 __attribute__((aligned(4)));
-                    const u32x3 v = {r.x, r.y, r.z};
-                    __builtin_nontemporal_store(v, reinterpret_cast<u32x3_a4*>(dst));
-#else
-                    if (r.x == 0xFFFFFFFFu && r.y == 0x7) *dst = r;  // ablation: no stores
-#endif
+            // scan (one wave): bins -> sorted tile offsets; a run's k-th record goes to slot position
+            // gdst + k; the counters are cleared for the next level
+            if (threadIdx.x < 64) {
+                const int lane = threadIdx.x;
+                const int per = (tb + 63) >> 6;
+                int sum = 0;
+                for (int q = 0; q < per; ++q) {
+                    const int lb = lane * per + q;
+                    sum += lb < tb ? hist[lb] : 0;
                 }
+                int x = sum;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int y = __shfl_up(x, off, 64);
+                    if (lane >= off) x += y;
+                }
+                int run = x - sum;
+                for (int q = 0; q < per; ++q) {
+                    const int lb = lane * per + q;
+                    if (lb < tb) {
+                        const int c = hist[lb];
+                        toff[lb] = run;
+                        const int cu = cursor[b0 + lb];
+                        gdst[par][lb] = cu - run;
+                        cursor[b0 + lb] = cu + c;
+                        hist[lb] = 0;
+                        run += c;
+                    }
+                }
+                if (lane == 63) s_total[par] = x;
             }
             __syncthreads();
+            // place: the records sorted by bin into the stage
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (R[k].meta == ~0u) continue;
+                const int lb = R[k].meta & 0xffff;
+                const int p = toff[lb] + (int)(R[k].meta >> 16);
+                stage[p] = R[k].r;
+                sbin[p] = (uint16_t)lb;
+            }
+            __syncthreads();
+            prev_b0 = b0;
+            par ^= 1;
         }
     }
+    store_prev();
     // the unit's largest contribution (one word per unit: the accumulate's per-partition bound is
     // sum over units of count x this max)
     {
@@ -1243,9 +1248,9 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
         if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = rmax;
         __syncthreads();
         if (threadIdx.x == 0) {
-            uint32_t m = 0u;
-            for (int k = 0; k < SC_THREADS / 64; ++k) m = max(m, wmax[k]);
-            smax[u] = m;
+            uint32_t mx = 0u;
+            for (int k = 0; k < SC_THREADS / 64; ++k) mx = max(mx, wmax[k]);
+            smax[u] = mx;
         }
     }
     bool over = false;
@@ -1257,28 +1262,15 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
     if (over) atomicOr(ovf, 1);
 }
 
-// pass 2: one workgroup per bin sums the bin's records (every unit's slot) into an LDS image of its
-// entries (int64 pairs, ds_add_u64) and stores it rounded to int32.
-__device__ __forceinline__ int round_shift32(long long v) { return (int)((v + 0x80000000ll) >> 32); }
-
-// float -> int64 rounded to nearest (ties to even), |v| < 2^62: below 2^31 one rint; above,
-// v = hi * 2^32 + d with hi = floor(v / 2^32), d in [0, 2^32) -- d is v's mantissa bits below 2^32
-// (ulp(v) >= 2^8 there), so the fma computing it is exact -- then d as u32.  Branch-free.
-__device__ __forceinline__ long long f2ll(float v) {
-    const float hi = floorf(v * 2.3283064365386963e-10f);  // v / 2^32 (exact scaling)
-    const float d = fmaf(hi, -4294967296.0f, v);          // exact for |v| >= 2^31 (ulp(v) >= 2^8)
-    const long long big = (long long)((uint64_t)(uint32_t)(int)hi << 32) + (long long)(uint32_t)rintf(d);
-    return fabsf(v) < 2147483648.0f ? (long long)(int)rintf(v) : big;
-}
-
-#if MFN_ACC32 == 2
-// packed image: one 64-bit word per entry holding both features' int32 sums as f1 * 2^32 + f0
-// (exact in two's complement; decoded f0 = lo, f1 = hi + (f0 < 0) at the store), 2 LDS atomics
-// per pair record.  The sums run at the PARTITION's own finer unit 2^-k of the table's: k is the
-// largest with (sum over units of the unit's record count in the partition x the unit's largest
-// |a|, |b|) * 2^k <= 2^30 -- a bound on every entry's sum, from bin_scatter's counts and maxima -- so
-// the int32 fields cannot overflow, and the stored table-unit value is rounded once per entry.
-using acc_t = unsigned long long;
+// pass 2: one workgroup per partition sums the partition's records (every unit's slot) into an LDS
+// image of its entries and stores it (or feeds it to the fused Adam update).
+//
+// The image holds one 64-bit word per entry: both features' int32 sums packed as f1 * 2^32 + f0
+// (exact in two's complement; decoded f0 = lo, f1 = hi + (f0 < 0)), 2 LDS atomics per pair record.
+// The sums run at the PARTITION's own finer unit 2^-k of the table's: k is the largest with
+// (sum over units of the unit's record count in the partition x the unit's largest |a|, |b|) * 2^k
+// <= 2^30 -- a bound on every entry's sum, from bin_scatter's counts and maxima -- so the int32
+// fields cannot overflow, and the stored table-unit value is rounded once per entry.
 __device__ __forceinline__ unsigned long long pack2(float a, float b) {
     return ((unsigned long long)(uint32_t)(int)rintf(b) << 32) + (unsigned long long)(long long)(int)rintf(a);
 }
@@ -1298,56 +1290,6 @@ __device__ __forceinline__ void accum_record(unsigned long long* img, int mask, 
         atomicAdd(&img[e1], pack2(fx * a, fx * b));
     }
 }
-#elif MFN_ACC32
-// int32 image in the table's fixed-point units: each weighted contribution rounded once (as
-// grid_bw_body rounds each run-merged one), the sums exact and order-free.  One cvt per value
-// instead of the int64 path's float -> int64 conversion: the accumulate is VALU-bound.
-using acc_t = int;
-__device__ __forceinline__ void accum_record(int* img, int mask, uint3 r) {
-    const uint32_t w = r.x;
-    const float a = __uint_as_float(r.y), b = __uint_as_float(r.z);
-    if (a == 0.0f && b == 0.0f) return;
-    const float fx = (float)(w >> 17) * (1.0f / 32768.0f);
-    const int e0 = w & mask;
-    if (w & (1u << 15)) {  // single entry, weight sel ? fx : 1 - fx
-        const float wt = (w & (1u << 16)) ? fx : 1.0f - fx;
-        atomicAdd(&img[2 * e0], (int)rintf(wt * a));
-        atomicAdd(&img[2 * e0 + 1], (int)rintf(wt * b));
-    } else {
-        const int e1 = e0 ^ ((2 << ((w >> 11) & 15)) - 1);
-        const float w0 = 1.0f - fx;
-        atomicAdd(&img[2 * e0], (int)rintf(w0 * a));
-        atomicAdd(&img[2 * e0 + 1], (int)rintf(w0 * b));
-        atomicAdd(&img[2 * e1], (int)rintf(fx * a));
-        atomicAdd(&img[2 * e1 + 1], (int)rintf(fx * b));
-    }
-}
-__device__ __forceinline__ int acc_out(int v) { return v; }
-#else
-using acc_t = unsigned long long;
-__device__ __forceinline__ void accum_record(unsigned long long* img, int mask, uint3 r) {
-    const uint32_t w = r.x;
-    const float a = __uint_as_float(r.y), b = __uint_as_float(r.z);
-    if (a == 0.0f && b == 0.0f) return;
-    const float fx = (float)(w >> 17) * (1.0f / 32768.0f);
-    const int e0 = w & mask;
-    // |values| < 2^62: exact in int64, order-free sums
-    if (w & (1u << 15)) {  // single entry, weight sel ? fx : 1 - fx
-        const float wt = (w & (1u << 16)) ? fx : 1.0f - fx;
-        atomicAdd(&img[2 * e0], (unsigned long long)f2ll(wt * a));
-        atomicAdd(&img[2 * e0 + 1], (unsigned long long)f2ll(wt * b));
-    } else {
-        const int e1 = e0 ^ ((2 << ((w >> 11) & 15)) - 1);
-        const float w0 = 1.0f - fx;
-        atomicAdd(&img[2 * e0], (unsigned long long)f2ll(w0 * a));
-        atomicAdd(&img[2 * e0 + 1], (unsigned long long)f2ll(w0 * b));
-        atomicAdd(&img[2 * e1], (unsigned long long)f2ll(fx * a));
-        atomicAdd(&img[2 * e1 + 1], (unsigned long long)f2ll(fx * b));
-    }
-}
-
-__device__ __forceinline__ int acc_out(unsigned long long v) { return round_shift32((long long)v); }
-#endif
 
 constexpr int ACC_THREADS = 512;
 
@@ -1388,52 +1330,36 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         return;
     }
     if (*ovf) return;  // a slot overflowed: bin_fallback_kernel scatters the binned levels
-#if MFN_ACC32 == 2
-    constexpr int IMG_WORDS = 1;  // per entry
-#else
-    constexpr int IMG_WORDS = 2;
-#endif
-    __shared__ acc_t img[IMG_WORDS * MAX_BIN_ENTRIES];
+    __shared__ unsigned long long img[MAX_BIN_ENTRIES];
     const int bin = (int)blockIdx.x - (X.first ? X.n_blocks : 0);
     const int n_ent = 1 << P.shift, mask = n_ent - 1;
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     const int64_t slot = slot_size(min(nn, n_slots), P);  // = bin_scatter_kernel's
     // one unit's slot per half-wave (32 lanes; ~30 records per slot at the Lego config), QF slots
-    // in flight per half-wave
+    // in flight per half-wave: each slot's count and first 32 records are loaded together,
+    // unconditionally (a slot always holds >= 96 records, so lane hl < 32 stays inside it; records
+    // past the count are dropped below) -- one memory round trip instead of a dependent pair.
+    // Measured in round 2: 4 -> 16 -> 8 slots per round 0.709 -> 0.693 -> 0.683 ms/step; the records
+    // 32-63 loaded in the same round as well 0.711 (double the record reads); exact loads after the
+    // counts (round 3, 106 VGPRs, 2 workgroups per CU) 157 vs 108 us.
     const int hw = threadIdx.x >> 5, hl = threadIdx.x & 31, n_hw = ACC_THREADS / 32;
     const int32_t* cnt = scnt + (int64_t)bin * UNITS;
     const uint3* base = rec + (int64_t)bin * UNITS * slot;
-#ifndef MFN_ACC_INFLIGHT
-#define MFN_ACC_INFLIGHT 8  // slots per half-wave whose first 32 records are loaded together (16: all; 8 measured best)
-#endif
-    constexpr int QF = MFN_ACC_INFLIGHT;
-#ifndef MFN_ACC_2REC
-#define MFN_ACC_2REC 0  // 1: also the records 32..63 of each slot in the same round (measured 0.668 -> 0.711 ms/step: the unconditional second load doubles the record reads)
-#endif
-    constexpr int FIRST = MFN_ACC_2REC ? 64 : 32;  // records per slot loaded up front
+    constexpr int QF = 8;
     uint3 r[QF];
     int c[QF];
-#if MFN_ACC_2REC
-    uint3 r2[QF];
-#endif
     auto prefetch = [&](int u0) {
 #pragma unroll
         for (int q = 0; q < QF; ++q) {
             const int u = u0 + q * n_hw;
             c[q] = u < UNITS ? cnt[u] : 0;
-            // unconditional (a slot holds >= 96 records, so lane hl < FIRST stays inside it): the
-            // count and the records are in flight together; records past the count are dropped below
             const uint3* sl = base + (int64_t)(u < UNITS ? u : 0) * slot;
             r[q] = sl[hl];
-#if MFN_ACC_2REC
-            r2[q] = sl[32 + hl];
-#endif
         }
     };
     prefetch(hw);  // the first round's loads overlap the image zeroing and the partition's bound
-    for (int i = threadIdx.x; i < IMG_WORDS * n_ent; i += blockDim.x) img[i] = 0;
+    for (int i = threadIdx.x; i < n_ent; i += blockDim.x) img[i] = 0;
     __syncthreads();
-#if MFN_ACC32 == 2
     // the partition's bound (sum over units of count x max), summed in a fixed order -> its unit 2^-k
     __shared__ float wsum[ACC_THREADS / 64];
     float term = 0.0f;
@@ -1455,31 +1381,20 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         kbits = max(0, min(30, 30 - e));
     }
     const float k2 = ldexpf(1.0f, kbits);
-#endif
     for (int u0 = hw; u0 < UNITS; u0 += QF * n_hw) {
         if (u0 != hw) prefetch(u0);
-#if MFN_ACC32 == 2
-#define MFN_ACC(IMG, MASK, R) accum_record(IMG, MASK, R, k2)
-#else
-#define MFN_ACC(IMG, MASK, R) accum_record(IMG, MASK, R)
-#endif
 #pragma unroll
         for (int q = 0; q < QF; ++q) {
             const int u = u0 + q * n_hw;
-            if (hl < c[q]) MFN_ACC(img, mask, r[q]);
-#if MFN_ACC_2REC
-            if (32 + hl < c[q]) MFN_ACC(img, mask, r2[q]);
-#endif
-            for (int k = hl + FIRST; k < c[q]; k += 32) MFN_ACC(img, mask, base[(int64_t)u * slot + k]);
+            if (hl < c[q]) accum_record(img, mask, r[q], k2);
+            for (int k = hl + 32; k < c[q]; k += 32) accum_record(img, mask, base[(int64_t)u * slot + k], k2);
         }
-#undef MFN_ACC
     }
     __syncthreads();
     const int t = bin_table(P, bin);
     const int64_t e_lo = (int64_t)(bin - P.t_bin0[t]) << P.shift;
     const int n_e = (int)min<int64_t>(n_ent, (int64_t)P.t_size[t] - e_lo);
     int* dst = grad + 2 * ((int64_t)P.t_offset[t] + e_lo);
-#if MFN_ACC32 == 2
     const int rnd = kbits > 0 ? 1 << (kbits - 1) : 0;
     if (A.params) {
         // fused optimizer (mfnerf_adam_step_fixed_partial): the entry's finished int32 sums, converted
@@ -1517,9 +1432,6 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         // back to the table's unit, rounded once (|fields| <= 2^30: no overflow adding rnd)
         reinterpret_cast<int2*>(dst)[i] = make_int2((lo + rnd) >> kbits, (hi + rnd) >> kbits);
     }
-#else
-    for (int i = threadIdx.x; i < 2 * n_e; i += blockDim.x) dst[i] = acc_out(img[i]);
-#endif
 }
 
 // the binned levels by request-shaped int32 atomics (grid_bw_body), only if a slot overflowed (a
@@ -2022,18 +1934,15 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
         if (!((parts & 1) && l_first > 0)) (void)hipMemsetAsync(W.ovf, 0, sizeof(int32_t), stream);
         // the staged dL/dy rows sized for the binned levels (8 at the Lego layout; MixedFeature's
         // shared tables bin more)
-#ifndef MFN_SCATTER_MAXB12
-#define MFN_SCATTER_MAXB12 1
-#endif
-#ifndef MFN_SCATTER_MAXB10
-#define MFN_SCATTER_MAXB10 1
-#endif
         // the smallest staging that holds the partitioned levels: fewer registers leave room on each
         // CU for the side stream's march kernels
-        auto sk = P.n_binned <= 8                          ? bin_scatter_kernel<8>
-                  : (MFN_SCATTER_MAXB10 && P.n_binned <= 10) ? bin_scatter_kernel<10>
-                  : (MFN_SCATTER_MAXB12 && P.n_binned <= 12) ? bin_scatter_kernel<12>
-                                                             : bin_scatter_kernel<MAX_BINNED>;
+        auto sk = P.pair_ok ? (P.n_binned <= 8    ? bin_scatter_kernel<8, true>
+                               : P.n_binned <= 10 ? bin_scatter_kernel<10, true>
+                               : P.n_binned <= 12 ? bin_scatter_kernel<12, true>
+                                                  : bin_scatter_kernel<MAX_BINNED, true>)
+                            : (P.n_binned <= 8    ? bin_scatter_kernel<8, false>
+                               : P.n_binned <= 12 ? bin_scatter_kernel<12, false>
+                                                  : bin_scatter_kernel<MAX_BINNED, false>);
         hipLaunchKernelGGL(sk, dim3(UNITS), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
                            *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.smax, W.ovf, n_slots);
         mfnerf_adam_fused A{};

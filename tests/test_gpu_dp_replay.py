@@ -147,40 +147,51 @@ def _union_worker(rank, world, port, mode, K, out):
     dist.destroy_process_group()
 
 
+def _union_single(gpu, K, n2, parts):
+    """One process stepping eagerly on the union batches (parts: 2 = float table-gradient atomics and
+    other summation orders -- an equally valid implementation of the same step).  Returns the final
+    parameters and the per-step losses."""
+    from mfnerf import engine, synthetic
+    full = _batches(K + 1, n2, gpu)
+    noise = _noises(K + 1, n2)
+    st = engine.TrainStep(engine.StepConfig(n_rays=n2, log2_T=LOG2_T, n_parts=parts), device=gpu, seed=0)
+    st.set_occupancy(synthetic.ball_density_grid())
+    losses = []
+    for k in range(K):
+        st.run(full[k], noise=noise[k].to(gpu))
+        losses.append(float(st.loss_sum))
+    torch.cuda.synchronize()
+    return st, st.params[:st.n_params].cpu(), losses
+
+
 @pytest.mark.parametrize("mode", ["shard", "allreduce"])
 def test_replayed_ranks_equal_one_process_on_the_union_batch(gpu, mode):
     """Two ranks replaying K = 4 steps on halves A_k, B_k vs one process stepping eagerly on
-    A_k u B_k (2N rays), same initial weights, occupancy and march perturbations: each step's loss
-    is the mean of the ranks' losses, and the final parameters agree wherever the union's gradient
-    was above the fixed-point resolution floor in every step (elsewhere Adam with eps 1e-15 turns a
-    floor-level difference into at most one opposite ~lr step per step).  Replicas are identical."""
-    from mfnerf import engine, synthetic
+    A_k u B_k (2N rays), same initial weights, occupancy and march perturbations.  Each step's loss
+    is the mean of the ranks' losses.  The parameters cannot agree bit for bit (the ranks round their
+    table-gradient contributions at their own fixed-point quanta, and Adam with eps 1e-15 turns any
+    sign flip of a near-zero gradient into a ~lr step, which the next steps propagate), so they are
+    held to the divergence between two equally valid single-process implementations of the union
+    step: the same batches through 2 ray parts (float table-gradient atomics, other MLP summation
+    order).  Per block (MLPs, table), the data-parallel run's L2 distance to the one-part run must
+    stay within 3x that natural distance.  Replicas are identical."""
     world, K, n = 2, 4, N_RAYS
     out = mp.Manager().dict()
     mp.spawn(_union_worker, args=(world, _port(), mode, K, out), nprocs=world, join=True)
     p0, h0, s0, l0 = out[(mode, 0)]
     p1, h1, s1, l1 = out[(mode, 1)]
     assert torch.equal(p0, p1) and torch.equal(h0, h1) and s0 == s1 == K
-    full = _batches(K + 1, 2 * n, gpu)
-    noise = _noises(K + 1, 2 * n)
-    st = engine.TrainStep(engine.StepConfig(n_rays=2 * n, log2_T=LOG2_T), device=gpu, seed=0)
-    st.set_occupancy(synthetic.ball_density_grid())
-    floor = torch.zeros(st.n_params, dtype=torch.bool)
+    st, pu, lu = _union_single(gpu, K, 2 * n, 1)
+    _, pv, lv = _union_single(gpu, K, 2 * n, 2)
     for k in range(K):
-        st.run(full[k], noise=noise[k].to(gpu), optimize=False)
-        g = st.grads[:st.n_params].cpu()
-        floor |= g.abs() <= 1e-6 * float(g.abs().max())
-        lu = float(st.loss_sum)
-        assert abs((l0[k] + l1[k]) / 2 - lu) <= 2e-3 * abs(lu), (mode, k, l0[k], l1[k], lu)
-        st.optimizer()
-    torch.cuda.synchronize()
-    moved = (p0[:st.n_params] - st.params[:st.n_params].cpu()).abs()
-    big = moved[~floor] > 1e-4
-    mlp = moved[:st.off_table]
-    print(f"\nUNION {mode}: moved max {float(moved.max()):.3g}, above-floor max {float(moved[~floor].max()):.3g}, "
-          f"above-floor entries > 1e-4: {int(big.sum())} of {int((~floor).sum())}, MLP max {float(mlp.max()):.3g}")
-    assert float(moved[~floor].max()) <= 1e-4, (mode, float(moved[~floor].max()))
-    assert float(moved.max()) <= 2.1 * K * st.cfg.lr
+        assert abs((l0[k] + l1[k]) / 2 - lu[k]) <= 2e-3 * abs(lu[k]), (mode, k, l0[k], l1[k], lu[k])
+    pd = p0[:st.n_params]
+    for name, a, b in (("mlp", 0, st.off_table), ("table", st.off_table, st.n_params)):
+        d_dp = float((pd[a:b] - pu[a:b]).norm())
+        d_nat = float((pv[a:b] - pu[a:b]).norm())
+        print(f"\nUNION {mode} {name}: |dp - union| {d_dp:.4g}, |union 2 parts - union| {d_nat:.4g}, "
+              f"|union| {float(pu[a:b].norm()):.4g}")
+        assert d_dp <= 3.0 * d_nat + 1e-6 * float(pu[a:b].norm()), (mode, name, d_dp, d_nat)
 
 
 def _nccl_worker(rank, port, out):
