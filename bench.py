@@ -24,9 +24,9 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "mf-nerf_amd")]
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# the table-gradient scatter's kernels in the PMC summaries: the run-merging atomics (dense and coarse
-# hashed levels) and the partitioned fine levels' scatter / accumulate / (idle) fallback
-GRID_BW_KERNEL = ("grid_bw_dense_kernel", "grid_bw_kernel", "bin_scatter_kernel", "bin_accum_kernel", "bin_fallback_kernel")
+# the table-gradient scatter's kernels in the PMC summaries: the run-merging atomics (dense levels)
+# and the partitioned hashed levels' scatter / accumulate
+GRID_BW_KERNEL = ("grid_bw_dense_kernel", "grid_bw_kernel", "bin_scatter_kernel", "bin_accum_kernel")
 
 # algorithmic bytes per live sample of each per-sample kernel, as SURVEY.md 8(d) prices them (the
 # tcnn form of the op: fp16 features and fp16 gradient scatter), DESIGN.md section 5
@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--parts", type=int, default=1, help="ray-range parts per step (chain/scatter overlap)")
     ap.add_argument("--dp", choices=("shard", "allreduce"), default="shard",
                     help="N>1: sharded optimizer (reduce-scatter + all-gather fp16) or all-reduce + full Adam")
+    ap.add_argument("--dp-rehearse", action="store_true",
+                    help="N=1: run the N>1 step anyway (a one-rank RCCL group, --dp mode) -- the data-parallel "
+                         "path's cost over the single-GPU step with the collectives reduced to a local copy")
     return ap.parse_args()
 
 
@@ -79,12 +82,14 @@ def _marker(ev):
     return mark
 
 
-def run_step(step, batch, world, ev=None):
+def run_step(step, batch, world, ev=None, allreduce=None):
     """One eager training step (mfnerf.engine.TrainStep.run); with ev, an event after every stage."""
     from mfnerf import dp
     mark = _marker(ev)
     mark("start")
-    step.run(batch, mark=mark, exchange=dp.allreduce_mean_ if world > 1 else None)
+    if allreduce is None:
+        allreduce = world > 1
+    step.run(batch, mark=mark, exchange=dp.allreduce_mean_ if allreduce else None)
 
 
 def pmc_traffic(kernel_prefix):
@@ -184,9 +189,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    dp_on = world > 1 or args.dp_rehearse
+    if dp_on:
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl")
+        torch.distributed.init_process_group("nccl", init_method=None if world > 1 else "tcp://127.0.0.1:29533",
+                                             world_size=world, rank=rank)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -200,8 +207,8 @@ def main():
     args.n_rays, args.log2_T = pre["n_rays"], pre["log2_T"]
     cfg = engine.StepConfig(n_parts=args.parts, **pre)
     step = engine.TrainStep(cfg, device=dev, seed=0)  # identical init on every rank
-    if world > 1 and args.dp == "shard":
-        step.shard_optimizer(rank, world)
+    if dp_on and args.dp == "shard":
+        step.shard_optimizer(rank, world, force=args.dp_rehearse)
     step.set_occupancy(synthetic.ball_density_grid())
     # the training data: 100 analytic 800x800 views (Lego intrinsics, cameras on a radius-1.5
     # sphere) of the very balls the calibrated occupancy grid holds, resident in HBM; every step
@@ -217,7 +224,7 @@ def main():
     batches = [None]
 
     for i in range(args.warmup):
-        run_step(step, batches[i % len(batches)], world)
+        run_step(step, batches[i % len(batches)], world, allreduce=dp_on)
     # occupancy refresh cost (amortised every 16 steps in the reference), measured separately
     step.update_density_grid(warmup=False)  # first call allocates the refresh scratch
     torch.cuda.synchronize()
@@ -233,7 +240,7 @@ def main():
     pass_ev = []
     for i in range(n_eager):
         ev = []
-        run_step(step, batches[i % len(batches)], world, ev)
+        run_step(step, batches[i % len(batches)], world, ev, allreduce=dp_on)
         pass_ev.append(ev)
     torch.cuda.synchronize()
     eager_stage_ms = stage_times(pass_ev, n_eager)
@@ -242,7 +249,7 @@ def main():
     # per-step host work is the batch copy, three graph launches and two pre-created timing events
     # around the grid_bw graph (the roofline kernel)
     from mfnerf import dp as _dp
-    ex = _dp.allreduce_mean_ if world > 1 else None
+    ex = _dp.allreduce_mean_ if dp_on else None
     use_graph = not args.eager
     if use_graph:
         step.capture()
@@ -264,7 +271,7 @@ def main():
             step.replay(exchange=ex, grid_bw_events=gb_ev[i] if timed else None)
         else:
             ev = []
-            run_step(step, batches[i % len(batches)], world, ev)
+            run_step(step, batches[i % len(batches)], world, ev, allreduce=dp_on)
             eager_ev.append(ev)
     host_s = time.time() - t0  # the host's issue time for the K steps (GPU-bound when well below elapsed)
     torch.cuda.synchronize()
@@ -315,7 +322,8 @@ def main():
                           args.n_rays, pre["grid"], args.log2_T,
                           " %d tables" % pre["N_tables"] if pre["grid"] == "MixedFeature" else "", pre["rgb_width"]),
                        "preset": args.preset, "global_batch": args.n_rays * world, "rm_s": round(mean_samples / args.n_rays, 2),
-                       "parallelism": f"dp{world}" + ("-sharded-adam" if world > 1 and args.dp == "shard" else ""),
+                       "parallelism": f"dp{world}" + ("-sharded-adam" if dp_on and args.dp == "shard" else "")
+                       + ("-rehearsal" if args.dp_rehearse and world == 1 else ""),
                        "psnr": None},
             "roofline": {"bound": "hbm", "kernel": dom + " (" + "+".join(GRID_BW_KERNEL) + ")",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -334,7 +342,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dp_on:
         torch.distributed.destroy_process_group()
 
 

@@ -227,8 +227,8 @@ int mfnerf_grid_encode_bw_finish(const mfnerf_grid_desc* desc, float* grad_table
  * grad_table must be zero on entry.  workspace: mfnerf_grid_encode_bw_binned_workspace(desc, n_slots)
  * bytes, its copies zero on the first call (left zero by the finish); n_slots (0 or > n: n) is the
  * live sample count the record slots are sized for -- a training step passes its expected count,
- * not its capacity (rays x 1024 samples): a live count well above n_slots overflows slots and takes
- * the atomic fallback (same result, slower).
+ * not its capacity (rays x 1024 samples): a live count well above n_slots overflows slots, whose
+ * extra records are added into grad_table by integer atomics (same sums, slower).
  * Bit-reproducible.  Replaces tcnn's hash-grid backward scatter (networks.py:36-49 encoding, half2
  * atomics there). */
 int64_t mfnerf_grid_encode_bw_binned_workspace(const mfnerf_grid_desc* desc, int64_t n_max);
@@ -258,34 +258,24 @@ int mfnerf_grid_encode_bw_binned_adam(const float* x, int64_t n, const int32_t* 
  * scatter (parts = 3), an accumulate launch whose partitions apply Adam to the partitioned tables
  * (as mfnerf_grid_encode_bw_binned_adam) while its leading workgroups run mfnerf_adam_step_fixed's
  * update over [0, the partitioned tables' first value) -- the MLPs and the dense levels, whose
- * gradients are final before the scatter -- and, after the overflow fallback, a pass that updates
- * the partitioned values only if a record slot overflowed and does the step's bookkeeping (step
+ * gradients are final before the scatter -- and a last small pass for the step's bookkeeping (step
  * count, GradScaler, level_l1 zeroed).  grads: the flat gradient of n_params values (the table's
  * at adam->table_offset), zero for the table on entry; step_dev / amp: adam's, writable.  Same bits
  * as mfnerf_grid_encode_bw_binned_adam + mfnerf_adam_step_fixed_partial (and as the unfused
- * mfnerf_grid_encode_bw_binned + mfnerf_adam_step_fixed).  Replaces tcnn's hash-grid backward +
- * apex FusedAdam's step over the whole model (train.py:136). */
+ * mfnerf_grid_encode_bw_binned + mfnerf_adam_step_fixed).  packed (optional, else NULL): the last pass
+ * also repacks the MLP weights from adam->p16 into the field head's fragment blob for rgb width
+ * rgb_width (= mfnerf_field_pack_weights_f16(p16, p16 + 3072, rgb_width, packed), one launch less).
+ * Replaces tcnn's hash-grid backward + apex FusedAdam's step over the whole model (train.py:136). */
 int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                                           const mfnerf_grid_desc* desc, const float* dL_dout, float* grads,
                                           int64_t n_params, void* workspace, int64_t n_slots, float* level_l1,
                                           const mfnerf_adam_fused* adam, int32_t* step_dev, mfnerf_amp_state* amp,
-                                          mfnerf_stream_t stream);
+                                          void* packed, int rgb_width, mfnerf_stream_t stream);
 
 /* out[l] += sum over rows i < n (or *n_dev) of |dL_dout[i][2l]| + |dL_dout[i][2l+1]| (f32). */
 int mfnerf_grid_level_l1(const float* dL_dout, int64_t n, const int32_t* n_dev, int n_levels, float* out,
                          mfnerf_stream_t stream);
 
-/* Debug: grid_encode_bw with an ablated body (1 plain stores, 2 levels 0-5 only, 3 levels 10-15 only;
- * 0 = the product kernel).  Used by tools/ to attribute the kernel's time; not a training path. */
-int mfnerf_debug_grid_bw_ablate(int mode, const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
-                                const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
-                                mfnerf_stream_t stream);
-
-/* Debug: the table-gradient scatter with fp16 accumulation (global_atomic_pk_add_f16, values scaled by
- * gscale) into grad_h2 (n_entries half2); priv_h2: optional private copies of the dense levels. */
-int mfnerf_debug_grid_bw_half(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
-                              const mfnerf_grid_desc* desc, const float* dL_dout, void* grad_h2, void* priv_h2,
-                              float gscale, mfnerf_stream_t stream);
 
 /* ---------------------------------------------------------------- NGP field head (MFMA) */
 
@@ -356,9 +346,6 @@ int mfnerf_mlp_bw(const void* x_f16, int64_t n, const void* packed, int n_in, in
                   int output_sigmoid, const void* dout_f16, float* dx, float* grad, void* workspace,
                   mfnerf_stream_t stream);
 
-/* Debug: one v_mfma_f32_32x32x16_f16 with A (32x16) and B (16x32) f16 row-major -> D (32x32) f32,
- * through the lane maps the field kernels assume (pins them on the device). */
-int mfnerf_debug_mfma_probe(const void* A, const void* B, float* D, mfnerf_stream_t stream);
 
 /* ---------------------------------------------------------------- occupancy grid refresh */
 
@@ -449,9 +436,9 @@ int mfnerf_adam_step_fixed(float* params, float* grads, float* m, float* v, void
 /* The collective-free step's optimizer split in two (mfnerf_grid_encode_bw_binned_adam +
  * mfnerf_adam_step_fixed_partial): the partitioned accumulate applies Adam to the partitioned
  * tables' parameters itself, from each entry's finished int32 sum, and never writes their gradient
- * words; the remaining pass updates [0, fused_from) only -- unless *fused_ovf is set (a record slot
- * overflowed, the fallback scattered those levels into the gradient words), then everything, as
- * mfnerf_adam_step_fixed does.  Same arithmetic, same bits as the unsplit pair. */
+ * words (a record slot's overflow, added into them by atomics, is folded in and zeroed there); the
+ * remaining pass updates [0, fused_from) only (fused_ovf non-NULL).  Same arithmetic, same bits as
+ * the unsplit pair. */
 
 int mfnerf_adam_step_fixed_partial(float* params, float* grads, float* m, float* v, void* p_f16, int64_t n,
                                    int64_t table_offset, const mfnerf_grid_desc* desc, void* workspace,

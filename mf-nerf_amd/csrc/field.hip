@@ -15,119 +15,45 @@
 
 #include "common.hpp"
 #include "mfma_pack.hpp"
+#include "field_pack.hpp"
 #include "../../include/mfnerf.h"
 
 using namespace mfn;
+using namespace mfn_field;
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
-constexpr int N_XYZ_PARAMS = 64 * 32 + 16 * 64;
-constexpr int FRAG_HALFS = 64 * 8;  // one A fragment: 64 lanes x 8 f16 (1 KiB)
 constexpr int FIELD_BLOCK = 256;    // forward: 4 waves
 
-// Fragment table for rgb width W: MT = W/32 row tiles, KC = W/16 K chunks of a W-wide input.
-template <int W>
-struct Geo {
-    static constexpr int MT = W / 32, KC = W / 16;
-    static constexpr int F1 = 0;             // W1  (64x32)  [mt*2+q]  natural, kbase 16q
-    static constexpr int F2 = 4;             // W2  (16x64)  [t*2+q]   perm, kbase 32t+16q
-    static constexpr int F3 = 8;             // Wr1 (Wx32)   [mt*2+q]  q=0 natural kbase 0 (SH); q=1 perm kbase 16 (h)
-    static constexpr int F4 = F3 + 2 * MT;   // Wr2 (WxW)    [mt*KC+c] perm, kbase 16c
-    static constexpr int F5 = F4 + MT * KC;  // Wr3 (16xW)   [c]       perm
-    static constexpr int B5 = F5 + KC;       // Wr3^T (Wx16) [mt]      perm kbase 0
-    static constexpr int B4 = B5 + MT;       // Wr2^T        [mt*KC+c]
-    static constexpr int B3 = B4 + MT * KC;  // Wr1^T (32xW) [c]
-    static constexpr int B2 = B3 + KC;       // W2^T  (64x16) [mt]     perm kbase 0
-    static constexpr int B1 = B2 + 2;        // W1^T  (32x64) [t*2+q]
-    static constexpr int N = B1 + 4;         // 44 (W = 64), 106 (W = 128)
-    static constexpr int N_FW = B5;          // the forward's fragments
-    static constexpr int N_RGB = W * 32 + W * W + 16 * W;
-    static constexpr int N_DW = N_XYZ_PARAMS + N_RGB;  // weight-gradient floats (one slab row)
-};
-
-// Backward variants (NW = waves per workgroup; one workgroup per CU):
-//   W = 64,  NW = 4: all 12 weight-gradient tiles accumulate in registers (192 of the 512 a lone
-//                    wave per SIMD can hold);
-//   W = 64,  NW = 8: all of them accumulate in an LDS image (ds_add_f32 per sample tile), so a wave
-//                    fits in 256 registers and two waves share each SIMD;
-//   W = 128, NW = 4: dW1, dW2, dWr1, dWr3 (12 tiles) in registers as at W = 64; dWr2's 16 tiles do
-//                    not fit beside them, so a second pass (field_bw_wr2_kernel: forward + dR2 only,
-//                    256 accumulator registers) computes dWr2 -- LDS atomics for it measured 19x
-//                    slower than the register path (an LDS-image variant ran 3.4 ms per 983k samples).
+// Backward configuration (4 waves per workgroup, one workgroup per CU, one wave per SIMD):
+//   W = 64:  all 12 weight-gradient tiles accumulate in registers (192 of the 512 a lone wave per
+//            SIMD can hold);
+//   W = 128: dW1, dW2, dWr1, dWr3 (12 tiles) in registers as at W = 64; dWr2's 16 tiles do not fit
+//            beside them, so a second pass (field_bw_wr2_kernel: forward + dR2 only, 256 accumulator
+//            registers) computes dWr2.
+// Measured and not kept (rounds 1-2): every tile in an LDS image with two waves per SIMD (ds_add_f32
+// per sample tile; W = 128: 836 vs 171 us), dWr2 by LDS atomics beside the register tiles (3.4 ms
+// per 983k samples), Wr2^T read from global memory, two sample tiles per loop trip (~560 registers:
+// 80-147 spilled, 177 vs 122 us inside the step).
 template <int W, int NW>
 struct BwCfg {
     using G = Geo<W>;
-    static constexpr bool XYZ_LDS = (NW == 8);            // dW1, dW2
-    static constexpr bool RGB_LDS = XYZ_LDS;              // dWr1, dWr2, dWr3
+    static_assert(NW == 4, "one wave per SIMD");
     static constexpr bool R2_SPLIT = (W == 128);          // dWr2 by field_bw_wr2_kernel
-    static constexpr bool B4_GLOBAL = false;              // Wr2^T from global memory (unused variant)
-#ifndef MFN_FIELD_PAIR
-#define MFN_FIELD_PAIR 0
-#endif
-    static constexpr bool PAIR = MFN_FIELD_PAIR && W == 64 && NW == 4;  // two sample tiles per loop trip
-    static constexpr int SKIP = B4_GLOBAL ? G::MT * G::KC : 0;
-    static constexpr int LDS_FRAGS = G::N - SKIP + 4;  // + 4 identity fragments
+    static constexpr int LDS_FRAGS = G::N + 4;            // + 4 identity fragments
     static constexpr int ID_BASE = LDS_FRAGS - 4;
     static constexpr size_t IMG_OFF = (size_t)LDS_FRAGS * FRAG_HALFS * 2;
-    // image: the slab row (+16 level-L1 partials) when everything is in LDS; else the rgb part
-    // [dWr1 | dWr2 | dWr3 rows 0..2] (dWr3's other rows are zero: dL/dout has 3 channels)
-    static constexpr int RGB_IMG = W * 32 + W * W + 3 * W;
-    static constexpr int IMG_FLOATS = XYZ_LDS ? G::N_DW + 16 : (RGB_LDS ? RGB_IMG : 0);
-    static constexpr size_t LDS = IMG_OFF + (size_t)IMG_FLOATS * 4;
+    static constexpr size_t LDS = IMG_OFF;
     static_assert(LDS <= 160 * 1024, "the backward's LDS must fit one CU");
 };
-
-struct FragSpec { int mat, trans, mtile, kbase, perm; };
-
-template <int W>
-__device__ FragSpec frag_spec(int f) {
-    using G = Geo<W>;
-    FragSpec s{0, 0, 0, 0, 1};
-    if (f < G::F2) { s.mat = 0; s.mtile = f >> 1; s.kbase = 16 * (f & 1); s.perm = 0; }
-    else if (f < G::F3) { int i = f - G::F2; s.mat = 1; s.kbase = 32 * (i >> 1) + 16 * (i & 1); }
-    else if (f < G::F4) { int i = f - G::F3; s.mat = 2; s.mtile = i >> 1; s.kbase = 16 * (i & 1); s.perm = i & 1; }
-    else if (f < G::F5) { int i = f - G::F4; s.mat = 3; s.mtile = i / G::KC; s.kbase = 16 * (i % G::KC); }
-    else if (f < G::B5) { int i = f - G::F5; s.mat = 4; s.kbase = 16 * i; }
-    else if (f < G::B4) { s.mat = 4; s.trans = 1; s.mtile = f - G::B5; s.kbase = 0; }
-    else if (f < G::B3) { int i = f - G::B4; s.mat = 3; s.trans = 1; s.mtile = i / G::KC; s.kbase = 16 * (i % G::KC); }
-    else if (f < G::B2) { int i = f - G::B3; s.mat = 2; s.trans = 1; s.kbase = 16 * i; }
-    else if (f < G::B1) { s.mat = 1; s.trans = 1; s.mtile = f - G::B2; s.kbase = 0; }
-    else { int i = f - G::B1; s.mat = 0; s.trans = 1; s.kbase = 16 * i; }
-    return s;
-}
-
-// weight matrices, row-major (out, in) in the tcnn params vectors
-template <int W, typename TP>
-__device__ __forceinline__ void mat_info(int mat, const TP* px, const TP* pr, const TP** p, int* rows, int* cols) {
-    switch (mat) {
-        case 0: *p = px; *rows = 64; *cols = 32; break;
-        case 1: *p = px + 64 * 32; *rows = 16; *cols = 64; break;
-        case 2: *p = pr; *rows = W; *cols = 32; break;
-        case 3: *p = pr + W * 32; *rows = W; *cols = W; break;
-        default: *p = pr + W * 32 + W * W; *rows = 16; *cols = W; break;
-    }
-}
-
-// k index carried by element j of lane half h (natural B order, or accumulator-as-operand order)
-__device__ __forceinline__ int k_of(int j, int h, int perm) { return perm ? 8 * (j >> 2) + 4 * h + (j & 3) : 8 * h + j; }
 
 template <typename TP, int W>
 __global__ void pack_kernel(const TP* __restrict__ px, const TP* __restrict__ pr, _Float16* __restrict__ out) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= Geo<W>::N * FRAG_HALFS) return;
-    const int f = t / FRAG_HALFS, lane = (t / 8) & 63, j = t & 7;
-    const FragSpec s = frag_spec<W>(f);
-    const int r = lane & 31, h = lane >> 5;
-    const int m = 32 * s.mtile + r, k = s.kbase + k_of(j, h, s.perm);
-    const TP* p; int rows, cols;
-    mat_info<W>(s.mat, px, pr, &p, &rows, &cols);
-    float v = 0.0f;
-    if (!s.trans) { if (m < rows && k < cols) v = (float)p[m * cols + k]; }
-    else { if (k < rows && m < cols) v = (float)p[k * cols + m]; }
-    out[t] = (_Float16)v;
+    if (t < Geo<W>::N * FRAG_HALFS) pack_elem<TP, W>(t, px, pr, out);
 }
 
 __device__ __forceinline__ f32x16 mfma(const half8& a, const half8& b, const f32x16& c) {
@@ -404,11 +330,7 @@ __device__ __forceinline__ void load_frags_bw(_Float16* lds, const _Float16* __r
     using C = BwCfg<W, NW>;
     const uint4* src = reinterpret_cast<const uint4*>(packed);
     uint4* dst = reinterpret_cast<uint4*>(lds);
-    for (int i = threadIdx.x; i < (G::N - C::SKIP) * 64; i += blockDim.x) {
-        const int f = i >> 6;
-        const int gf = f < G::B4 ? f : f + C::SKIP;  // B4 stays in global memory when SKIP > 0
-        dst[i] = src[gf * 64 + (i & 63)];
-    }
+    for (int i = threadIdx.x; i < G::N * 64; i += blockDim.x) dst[i] = src[i];
     // identity: lane (n = lane&31, h), element j = 1 iff off + k_of(j, h, perm) == n
     for (int i = threadIdx.x; i < 4 * 64; i += blockDim.x) {
         const int fi = i >> 6, ln = i & 63, nn = ln & 31, hh = ln >> 5;
@@ -421,15 +343,9 @@ __device__ __forceinline__ void load_frags_bw(_Float16* lds, const _Float16* __r
     __syncthreads();
 }
 
-// a backward fragment (index in the packed blob): from LDS, except B4 when it stays in global memory
+// a backward fragment (index in the packed blob), from LDS
 template <int W, int NW>
 __device__ __forceinline__ half8 bw_frag(const _Float16* lds, const _Float16* __restrict__ packed, int f, int lane) {
-    using G = Geo<W>;
-    using C = BwCfg<W, NW>;
-    if constexpr (C::SKIP > 0) {
-        if (f >= G::B4 && f < G::B3) return *reinterpret_cast<const half8*>(packed + (f * 64 + lane) * 8);
-        if (f >= G::B3) return lds_frag(lds, f - C::SKIP, lane);
-    }
     return lds_frag(lds, f, lane);
 }
 
@@ -490,18 +406,8 @@ __device__ __forceinline__ void dw_add32(float* img, const f32x16& a, int ot, in
     }
 }
 
-// one dW tile += dY x X: into its register accumulator, or (IN_LDS) into the workgroup's image
-template <bool IN_LDS>
-__device__ __forceinline__ void acc_tile(f32x16& reg, float* img, int rows, int cols, const SOp& dy, const SOp& x,
-                                         int ot, int it, int lane) {
-    if constexpr (IN_LDS) {
-        f32x16 a = {};
-        dw_acc(a, dy, x);
-        dw_add32(img, a, ot, it, rows, cols, lane);
-    } else {
-        dw_acc_agpr(reg, dy, x);
-    }
-}
+// one dW tile += dY x X into its register accumulator
+__device__ __forceinline__ void acc_tile(f32x16& reg, const SOp& dy, const SOp& x) { dw_acc_agpr(reg, dy, x); }
 
 template <int W, int NW, bool PLANAR>
 __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
@@ -512,31 +418,22 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
     using G = Geo<W>;
     using C = BwCfg<W, NW>;
     constexpr int MT = G::MT;
-    constexpr bool XL = C::XYZ_LDS, RL = C::RGB_LDS;
     constexpr int ID_N0 = C::ID_BASE, ID_N16 = C::ID_BASE + 1, ID_P0 = C::ID_BASE + 2, ID_P16 = C::ID_BASE + 3;
     constexpr int oR1 = N_XYZ_PARAMS, oR2 = oR1 + W * 32, oR3 = oR2 + W * W;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     _Float16* lds_base = reinterpret_cast<_Float16*>(smem);
-    // LDS-resident accumulators (BwCfg): the slab row, or its rgb part
-    float* limg = reinterpret_cast<float*>(smem + C::IMG_OFF);
-    for (int i = threadIdx.x; i < C::IMG_FLOATS; i += blockDim.x) limg[i] = 0.0f;
     load_frags_bw<W, NW>(lds_base, packed);
-    float* i_w1 = limg;
-    float* i_w2 = limg + 64 * 32;
-    float* i_r1 = limg + (XL ? oR1 : 0);
-    float* i_r2 = i_r1 + W * 32;
-    float* i_r3 = i_r2 + W * W;
     const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform)
     const int r = lane & 31, h = lane >> 5;
     const float S = scale_dev ? *scale_dev : grad_scale, invS = 1.0f / S;  // the (dynamic) loss scale
     const f32x16 z = {};
     // register accumulators, 32x32 tiles [out-tile][in-tile] (192 registers at W = 64, NW = 4)
-    constexpr int R2 = RL ? 1 : MT;
-    f32x16 dw1[XL ? 1 : 2], dw2[XL ? 1 : 2], dwr1[RL ? 1 : MT], dwr3[RL ? 1 : MT], dwr2[R2][R2];
+    constexpr int R2 = C::R2_SPLIT ? 1 : MT;
+    f32x16 dw1[2], dw2[2], dwr1[MT], dwr3[MT], dwr2[R2][R2];
 #pragma unroll
-    for (int a = 0; a < (XL ? 1 : 2); ++a) { dw1[a] = z; dw2[a] = z; }
+    for (int a = 0; a < 2; ++a) { dw1[a] = z; dw2[a] = z; }
 #pragma unroll
-    for (int a = 0; a < (RL ? 1 : MT); ++a) { dwr1[a] = z; dwr3[a] = z; }
+    for (int a = 0; a < MT; ++a) { dwr1[a] = z; dwr3[a] = z; }
 #pragma unroll
     for (int a = 0; a < R2; ++a)
 #pragma unroll
@@ -549,7 +446,7 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
     // scheduler overlaps one tile's MFMA chain with the other's VALU packing and LDS waits (one wave
     // per SIMD hides no latency otherwise).  Each accumulator still takes the tiles in the order
     // tile, tile + stride, ...: the sums are the same as with one tile per trip, bit for bit.
-    constexpr int P = C::PAIR ? 2 : 1;
+    constexpr int P = 1;
     // the next trip's inputs are loaded while this trip computes
     struct BwIn { TileIn I; float gs, g0, g1, g2; bool live; };
     BwIn nx[P];
@@ -639,8 +536,7 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
             const SOp d = to_s16(lds, lane, dOb[q], ID_P0);
 #pragma unroll
             for (int t = 0; t < MT; ++t)
-                acc_tile<RL>(dwr3[RL ? 0 : t], i_r3, 3, W, d,
-                             to_s(lds, lane, T[q].r2[t][0], ID_P0, T[q].r2[t][1], ID_P16), 0, t, lane);
+                acc_tile(dwr3[t], d, to_s(lds, lane, T[q].r2[t][0], ID_P0, T[q].r2[t][1], ID_P16));
         }
         //    dR1 = Wr2^T dR2, masked by R1 > 0
         half8 dr1p[P][MT][2];
@@ -674,7 +570,7 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
                     const SOp d = to_s(lds, lane, dr2p[q][o][0], ID_P0, dr2p[q][o][1], ID_P16);
 #pragma unroll
                     for (int i = 0; i < MT; ++i)
-                        acc_tile<RL>(dwr2[RL ? 0 : o][RL ? 0 : i], i_r2, W, W, d, x[i], o, i, lane);
+                        acc_tile(dwr2[o][i], d, x[i]);
                 }
             }
         }
@@ -706,8 +602,7 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
             const SOp x = to_s(lds, lane, T[q].sh, ID_N0, T[q].hb, ID_P16);
 #pragma unroll
             for (int o = 0; o < MT; ++o)
-                acc_tile<RL>(dwr1[RL ? 0 : o], i_r1, W, 32,
-                             to_s(lds, lane, dr1p[q][o][0], ID_P0, dr1p[q][o][1], ID_P16), x, o, 0, lane);
+                acc_tile(dwr1[o], to_s(lds, lane, dr1p[q][o][0], ID_P0, dr1p[q][o][1], ID_P16), x);
         }
         //    dY1 = W2^T dh, masked by Y1 > 0
         half8 dy1p[P][2][2];
@@ -744,8 +639,7 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
             const SOp d = to_s16(lds, lane, dhb[q], ID_P0);
 #pragma unroll
             for (int t = 0; t < 2; ++t)
-                acc_tile<XL>(dw2[XL ? 0 : t], i_w2, 16, 64, d,
-                             to_s(lds, lane, T[q].y1[t][0], ID_P0, T[q].y1[t][1], ID_P16), 0, t, lane);
+                acc_tile(dw2[t], d, to_s(lds, lane, T[q].y1[t][0], ID_P0, T[q].y1[t][1], ID_P16));
         }
         // -- xyz layer 1: dW1 (64x32) += dY1^T X   (X natural order)
 #pragma unroll
@@ -753,8 +647,7 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
             const SOp x = to_s(lds, lane, T[q].x[0], ID_N0, T[q].x[1], ID_N16);
 #pragma unroll
             for (int o = 0; o < 2; ++o)
-                acc_tile<XL>(dw1[XL ? 0 : o], i_w1, 64, 32,
-                             to_s(lds, lane, dy1p[q][o][0], ID_P0, dy1p[q][o][1], ID_P16), x, o, 0, lane);
+                acc_tile(dw1[o], to_s(lds, lane, dy1p[q][o][0], ID_P0, dy1p[q][o][1], ID_P16), x);
         }
     };
     for (int64_t tile = tile0; tile < tiles; tile += P * stride) {
@@ -795,25 +688,9 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
 
     // ---- epilogue: the workgroup's dW (and the level L1 partials) -> one slab row
     float* row = slab + (int64_t)blockIdx.x * G::N_DW;
-    if constexpr (XL) {
-        float* l1_part = limg + G::N_DW;  // zeroed with the image
-        __syncthreads();
-        if (level_l1) {
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                float a = l1a[g], b = l1b[g];
-#pragma unroll
-                for (int off = 16; off > 0; off >>= 1) { a += __shfl_xor(a, off, 64); b += __shfl_xor(b, off, 64); }
-                if (r == 0) { atomicAdd(l1_part + 4 * g + 2 * h, a); atomicAdd(l1_part + 4 * g + 2 * h + 1, b); }
-            }
-        }
-        __syncthreads();
-        for (int i = threadIdx.x; i < G::N_DW; i += blockDim.x) row[i] = limg[i] * invS;
-        if (level_l1 && threadIdx.x < 16) atomicAdd(level_l1 + threadIdx.x, l1_part[threadIdx.x]);
-    } else {
-        // register partials -> an fp32 image over the fragment area (the xyz part only when the
-        // rgb part already is in limg)
-        constexpr int N_IMG = RL ? N_XYZ_PARAMS : G::N_DW;
+    {
+        // register partials -> an fp32 image over the fragment area
+        constexpr int N_IMG = G::N_DW;
         static_assert((size_t)N_IMG * 4 + 64 <= C::IMG_OFF, "reduction image must fit the fragment area");
         xdl_drain();
         __syncthreads();
@@ -840,28 +717,22 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
                     dw_add32(img, dw1[a], a, 0, 64, 32, lane, st);
                     dw_add32(img + 64 * 32, dw2[a], 0, a, 16, 64, lane, st);
                 }
-                if constexpr (!RL) {
 #pragma unroll
-                    for (int a = 0; a < MT; ++a) {
-                        dw_add32(img + oR1, dwr1[a], a, 0, W, 32, lane, st);
-                        dw_add32(img + oR3, dwr3[a], 0, a, 16, W, lane, st);
-                    }
-#pragma unroll
-                    for (int o = 0; o < R2; ++o)
-#pragma unroll
-                        for (int i = 0; i < R2; ++i)
-                            if constexpr (!C::R2_SPLIT) dw_add32(img + oR2, dwr2[o][i], o, i, W, W, lane, st);
+                for (int a = 0; a < MT; ++a) {
+                    dw_add32(img + oR1, dwr1[a], a, 0, W, 32, lane, st);
+                    dw_add32(img + oR3, dwr3[a], 0, a, 16, W, lane, st);
                 }
+#pragma unroll
+                for (int o = 0; o < R2; ++o)
+#pragma unroll
+                    for (int i = 0; i < R2; ++i)
+                        if constexpr (!C::R2_SPLIT) dw_add32(img + oR2, dwr2[o][i], o, i, W, W, lane, st);
             }
             __syncthreads();
         }
         for (int i = threadIdx.x; i < G::N_DW; i += blockDim.x) {
             if (C::R2_SPLIT && i >= oR2 && i < oR3) continue;  // written by field_bw_wr2_kernel
-            float v;
-            if (!RL || i < oR1) v = img[i];
-            else if (i < oR3 + 3 * W) v = limg[i - oR1];
-            else v = 0.0f;  // dWr3 rows 3..15
-            row[i] = v * invS;
+            row[i] = img[i] * invS;
         }
         if (level_l1 && threadIdx.x < 16) atomicAdd(level_l1 + threadIdx.x, l1_part[threadIdx.x]);
     }
@@ -1015,33 +886,11 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 
 constexpr int BW_BLOCKS = 256;  // one workgroup per CU (persistent)
 
-// debug: one MFMA with A (32x16) and B (16x32) f16 row-major -> D (32x32) f32, to pin the lane maps
-__global__ void mfma_probe_kernel(const _Float16* A, const _Float16* B, float* D) {
-    const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
-    half8 a, b;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { a[j] = A[r * 16 + 8 * h + j]; b[j] = B[(8 * h + j) * 32 + r]; }
-    f32x16 c = {};
-    c = mfma(a, b, c);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) D[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = c[i];
-}
-
 bool width_ok(int w) { return w == 64 || w == 128; }
 
 int bad_width(int w) {
     mfn_set_error("field: rgb_width=%d unsupported (this build: 64 or 128)", w);
     return MFN_ERR_INVALID;
-}
-
-// W = 64 backward variant: 4 waves per workgroup (register accumulators) or 8 (LDS accumulators);
-// MFNERF_FIELD_BW_WAVES=4|8 selects it (read once), for A/B measurements
-int bw_waves_w64() {
-    static const int w = [] {
-        const char* e = getenv("MFNERF_FIELD_BW_WAVES");
-        return (e && atoi(e) == 8) ? 8 : 4;
-    }();
-    return w;
 }
 
 template <typename TP, int W>
@@ -1174,9 +1023,6 @@ int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float
     if (rgb_width == 128)
         st = launch_bw<128, 4>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, dL_dsigma, dL_drgb, grad_scale,
                                scale_dev, dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
-    else if (bw_waves_w64() == 8)
-        st = launch_bw<64, 8>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, dL_dsigma, dL_drgb, grad_scale,
-                              scale_dev, dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
     else
         st = launch_bw<64, 4>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, dL_dsigma, dL_drgb, grad_scale,
                               scale_dev, dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
@@ -1197,9 +1043,5 @@ int mfnerf_field_bw_reduce(int rgb_width, const void* workspace, float* grad_xyz
     return mfn_check_launch("field_bw_reduce");
 }
 
-int mfnerf_debug_mfma_probe(const void* A, const void* B, float* D, mfnerf_stream_t stream) {
-    hipLaunchKernelGGL(mfma_probe_kernel, dim3(1), dim3(64), 0, stream, (const _Float16*)A, (const _Float16*)B, D);
-    return mfn_check_launch("mfma_probe");
-}
 
 }  // extern "C"

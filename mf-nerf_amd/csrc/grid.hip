@@ -9,6 +9,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "field_pack.hpp"
 #include "../../include/mfnerf.h"
 
 using namespace mfn;
@@ -213,10 +214,7 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_fw_planar_kernel(const float* 
 //     merges such runs and only run heads issue the atomic;
 //   * the dense coarse levels (a few hundred to a few thousand hot lines) add into GRAD_COPIES
 //     private copies, picked per wave, folded back by fold_copies_kernel.
-#ifndef MFN_GRAD_COPIES
-#define MFN_GRAD_COPIES 8
-#endif
-constexpr int GRAD_COPIES = MFN_GRAD_COPIES;  // power of two
+constexpr int GRAD_COPIES = 8;  // power of two (8-64 copies measured the same: not contention)
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
@@ -229,7 +227,6 @@ __device__ __forceinline__ int dpp_i(int v) {
 #define DPP_ROW_SHL(d) (0x100 | (d))
 #define DPP_ROW_SHR(d) (0x110 | (d))
 
-// ABLATE: 0 = product; debug builds: 1 plain stores, 2 levels 0-5 only, 3 levels 10-15 only.
 // MAXL: level-count bound (16 or 32) sizing the LDS tile and the prefetch registers.
 // FIX: fixed-point accumulation -- per level l, each (run-merged) contribution v is added as the
 // int32 rint(v * scale_l) with global_atomic_add (integer atomics run ~28% faster than float ones
@@ -256,7 +253,7 @@ __device__ __forceinline__ float table_fixed_scale(const mfnerf_grid_desc& D, co
 }
 
 // the scatter as workgroup `bid` of `nblk` (a launch of its own, or a share of a fused launch)
-template <int ABLATE, int MAXL, bool FIX>
+template <int MAXL, bool FIX>
 __device__ __forceinline__ void grid_bw_body(int bid, int nblk, const float* __restrict__ X, int64_t n,
                                              const int32_t* __restrict__ n_dev, float x_min, float x_range,
                                              const mfnerf_grid_desc& D, const float* __restrict__ dy,
@@ -310,8 +307,6 @@ __device__ __forceinline__ void grid_bw_body(int bid, int nblk, const float* __r
         if (chunk + n_waves < chunks) fetch(chunk + n_waves);  // in flight during this chunk's atomics
         const float* srow = sdy + s * rs + f;
         for (int l = l_end >> 8; l < (l_end & 255); ++l) {  // levels [l_end >> 8, l_end & 255)
-            if (ABLATE == 2 && l > 5) continue;
-            if (ABLATE == 3 && l < 10) continue;
             const float g = srow[2 * l];
             const float fs = FIX ? fs_s[l] : 0.0f;
             const LevelGeo Lg = level_geo(D.scale[l], x, y, z);
@@ -346,15 +341,14 @@ __device__ __forceinline__ void grid_bw_body(int bid, int nblk, const float* __r
                         __hip_atomic_fetch_add(reinterpret_cast<int*>(gt) + 2 * idx + f, q, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
                 } else if (head && valid && v != 0.0f) {
-                    if (ABLATE == 1) gt[2 * idx + f] = v;
-                    else __hip_atomic_fetch_add(gt + 2 * idx + f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(gt + 2 * idx + f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
         }
     }
 }
 
-template <int ABLATE, int MAXL, bool FIX>
+template <int MAXL, bool FIX>
 __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restrict__ X, int64_t n,
                                                              const int32_t* __restrict__ n_dev, float x_min,
                                                              float x_range, const mfnerf_grid_desc D,
@@ -365,7 +359,7 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restr
     // zero_flag: a flag the NEXT launches on the stream start from zero (the binned scatter's slot
     // overflow), cleared here instead of by a memset launch of its own
     if (zero_flag && blockIdx.x == 0 && threadIdx.x == 0) *zero_flag = 0;
-    grid_bw_body<ABLATE, MAXL, FIX>(blockIdx.x, gridDim.x, X, n, n_dev, x_min, x_range, D, dy, grad, priv,
+    grid_bw_body<MAXL, FIX>(blockIdx.x, gridDim.x, X, n, n_dev, x_min, x_range, D, dy, grad, priv,
                                     dense_entries, level_l1, l_end);
 }
 
@@ -386,12 +380,6 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_kernel(const float* __restr
 //     f1 = int32(high word) + (f0 < 0); |sums| < 2^31 by the scale bound): a run costs 4 requests
 //     (one 16-B span per row), 8 runs per instruction.
 // Requires every level < l_hi to be a dense own table inside the private copies.
-#ifndef MFN_DENSE_ABLATE
-#define MFN_DENSE_ABLATE 0
-#endif
-#ifndef MFN_DENSE_SHFL
-#define MFN_DENSE_SHFL 0
-#endif
 
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ int dppz_i(int v) {  // lanes without a source (or outside ROW_MASK) read 0
@@ -399,7 +387,8 @@ __device__ __forceinline__ int dppz_i(int v) {  // lanes without a source (or ou
 }
 
 // a wave's window: DENSE_WIN chunks of 64 consecutive samples; the run open at a chunk's end is
-// carried into the next chunk (per level, in LDS) instead of being issued twice
+// carried into the next chunk (per level, in LDS) instead of being issued twice.  Round 3 A/B
+// (kbench, Lego step): 4 chunks 85 us; the smaller windows tried measured 95-101 us.
 constexpr int DENSE_WIN = 4;
 
 struct DenseIn {
@@ -586,11 +575,7 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_dense_kernel(const float* _
                         const int2 kp = lkey[wv][r][yz];
                         const int kk = c ? kp.y : kp.x;
                         const long long pq = (long long)((uint64_t)(uint32_t)f1 << 32) + (long long)f0;
-#if MFN_DENSE_ABLATE == 1
-                        if (pq == 0x7fffffffffffll)
-#else
                         if (pq != 0)
-#endif
                             __hip_atomic_fetch_add(gt + kk, pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                 }
@@ -600,84 +585,6 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_dense_kernel(const float* _
                 in = nx;
 #pragma unroll
                 for (int j = 0; j < NG; ++j) gq[j] = gn[j];
-            }
-        }
-    }
-}
-
-// fp16 variant (experiment / tcnn's grad_t = __half for F = 2): one lane adds BOTH features of a
-// corner with global_atomic_pk_add_f16, lanes = (sample s, x-corner xb, yz-half), so a level takes
-// 2 wave-instructions instead of 4.  Values are multiplied by gscale before rounding to fp16.
-typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-
-template <int MAXL>
-__global__ __launch_bounds__(ENC_BLOCK) void grid_bw_h2_kernel(const float* __restrict__ X, int64_t n,
-                                                                const int32_t* __restrict__ n_dev, float x_min,
-                                                                float x_range, const mfnerf_grid_desc D,
-                                                                const float* __restrict__ dy, h2v* __restrict__ grad,
-                                                                h2v* __restrict__ priv, int64_t dense_entries,
-                                                                float gscale) {
-    __shared__ float sdy_all[ENC_BLOCK / 64][16 * (2 * MAXL + 1)];
-    const int L_ = D.n_levels;
-    const int lane = threadIdx.x & 63, s = lane & 15, xb = (lane >> 4) & 1, yzh = lane >> 5;
-    const int row = 2 * L_, rs = 2 * L_ + 1, per_chunk = 16 * row;
-    float* sdy = sdy_all[threadIdx.x >> 6];
-    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
-    const int64_t chunks = div_up<int64_t>(nn, 16);
-    const int64_t wave0 = ((int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x) >> 6;
-    const int64_t n_waves = ((int64_t)gridDim.x * ENC_BLOCK) >> 6;
-    const int64_t n_vals = nn * row;
-    float pf[MAXL / 2];
-    float px = 0.0f, py = 0.0f, pz = 0.0f;
-    auto fetch = [&](int64_t ch) {
-        const int64_t base = ch * per_chunk;
-#pragma unroll
-        for (int k = 0; k < MAXL / 2; ++k) {
-            const int idx = lane + 64 * k;
-            pf[k] = (idx < per_chunk && base + idx < n_vals) ? dy[base + idx] : 0.0f;
-        }
-        const int64_t i = ch * 16 + s;
-        if (i < nn) { px = X[3 * i]; py = X[3 * i + 1]; pz = X[3 * i + 2]; }
-    };
-    if (wave0 < chunks) fetch(wave0);
-    for (int64_t chunk = wave0; chunk < chunks; chunk += n_waves) {
-        const int64_t i = chunk * 16 + s;
-        const bool valid = i < nn;
-#pragma unroll
-        for (int k = 0; k < MAXL / 2; ++k) {
-            const int idx = lane + 64 * k;
-            if (idx < per_chunk) sdy[(idx / row) * rs + idx % row] = pf[k];
-        }
-        const float x = valid ? (px - x_min) / x_range : 0.0f;
-        const float y = valid ? (py - x_min) / x_range : 0.0f;
-        const float z = valid ? (pz - x_min) / x_range : 0.0f;
-        if (chunk + n_waves < chunks) fetch(chunk + n_waves);
-        const float* srow = sdy + s * rs;
-        for (int l = 0; l < L_; ++l) {
-            const float g0 = srow[2 * l] * gscale, g1 = srow[2 * l + 1] * gscale;
-            const LevelGeo Lg = level_geo(D.scale[l], x, y, z);
-            const bool spread = priv && (int64_t)D.offset[l] + D.size[l] <= dense_entries;
-            h2v* gt = spread ? priv + ((chunk & (GRAD_COPIES - 1)) * dense_entries + (int64_t)D.offset[l])
-                             : grad + (int64_t)D.offset[l];
-#pragma unroll
-            for (int yp = 0; yp < 2; ++yp) {
-                const int c = xb | ((2 * yzh + yp) << 1);
-                const uint32_t idx =
-                    corner_index(D, l, Lg.g[0] + (c & 1), Lg.g[1] + ((c >> 1) & 1), Lg.g[2] + ((c >> 2) & 1));
-                const int key = valid ? (int)idx : -1;
-                const float w = corner_weight(Lg, c);
-                float v0 = w * g0, v1 = w * g1;
-                const int kn = dpp_i<DPP_ROW_SHL(1)>(key), kp = dpp_i<DPP_ROW_SHR(1)>(key);
-                const bool head = (s == 0) || kp != key;
-                int stop = (s == 15) || kn != key;
-#define H2_STEP(d) { const float a = dpp_f<DPP_ROW_SHL(d)>(v0), b = dpp_f<DPP_ROW_SHL(d)>(v1); \
-                     const int sp = dpp_i<DPP_ROW_SHL(d)>(stop); if (!stop) { v0 += a; v1 += b; stop = sp; } }
-                H2_STEP(1) H2_STEP(2) H2_STEP(4) H2_STEP(8)
-#undef H2_STEP
-                if (head && valid && (v0 != 0.0f || v1 != 0.0f)) {
-                    const h2v hv = {(_Float16)v0, (_Float16)v1};
-                    __builtin_amdgcn_global_atomic_fadd_v2f16((__attribute__((address_space(1))) h2v*)(gt + idx), hv);
-                }
             }
         }
     }
@@ -829,10 +736,18 @@ __device__ __forceinline__ void adam_fixed_body(float* __restrict__ p, float* __
     }
 }
 
+// the MLP weights' repack riding the optimizer's last pass (out = nullptr: none)
+struct PackArgs {
+    const _Float16* px;  // xyz MLP (fp16 compute copy)
+    const _Float16* pr;  // rgb MLP
+    _Float16* out;       // the field head's fragment blob (mfnerf_field_pack_weights_f16's layout)
+    int width;           // rgb width, 64 or 128
+};
+
 // tail_mode 0: values [0, n), or [0, fused_from) when the fused partitioned accumulate updated the
-// rest (fused_ovf clear).  tail_mode 1 (mfnerf_grid_encode_bw_binned_adam_all, whose accumulate
-// launch also updated [0, fused_from)): [fused_from, n) only if a slot overflowed, else nothing but
-// the step's bookkeeping.
+// rest (fused_ovf given; overflowed records included -- the accumulate adds them).  tail_mode 1
+// (mfnerf_grid_encode_bw_binned_adam_all, whose accumulate launch updated every value): nothing but
+// the MLP repack and the step's bookkeeping.
 __global__ __launch_bounds__(256) void adam_fixed_kernel(float* __restrict__ p, float* __restrict__ g,
                                                          float* __restrict__ m, float* __restrict__ v,
                                                          __half* __restrict__ p16, int64_t n, int64_t off,
@@ -843,17 +758,12 @@ __global__ __launch_bounds__(256) void adam_fixed_kernel(float* __restrict__ p, 
                                                          const float* __restrict__ lr_dev,
                                                          mfnerf_amp_state* __restrict__ amp, int n_levels,
                                                          int64_t fused_from, const int32_t* __restrict__ fused_ovf,
-                                                         int tail_mode) {
+                                                         int tail_mode, const PackArgs pk) {
     __shared__ TableRegions R;
     int64_t lo = 0;
-    if (tail_mode == 1) {
-        lo = fused_from;
-        if (*fused_ovf == 0) n = lo;
-    } else if (fused_ovf && *fused_ovf == 0) {
-        // values >= fused_from were updated by the fused partitioned accumulate
-        n = fused_from;
-    }
-    if (n > lo) {  // (uniform; the overflow-only pass has nothing to update unless a slot overflowed)
+    if (tail_mode == 1) n = 0;                 // the accumulate launch updated every value
+    else if (fused_ovf) n = fused_from;        // values >= fused_from: updated by the accumulate
+    if (n > lo) {  // (uniform)
         R.build(D, level_l1, total_vals);
         const bool skipped = amp && amp->nonfinite;  // GradScaler: no update on a non-finite gradient, only the zeroing
         const int st = *step_dev + 1;
@@ -863,6 +773,14 @@ __global__ __launch_bounds__(256) void adam_fixed_kernel(float* __restrict__ p, 
         const int64_t stride = (int64_t)gridDim.x * blockDim.x;
         adam_fixed_body(p, g, m, v, p16, off, priv, dense_vals, total_vals, R, lr, b1, b2, eps, bc1, bc2, skipped,
                         lo / 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x, n / 4, stride);
+    }
+    // tail_mode 1: the MLP weights' repack (their p16 was written by the accumulate launch)
+    if (pk.out) {
+        const int total = (pk.width == 64 ? mfn_field::Geo<64>::N : mfn_field::Geo<128>::N) * mfn_field::FRAG_HALFS;
+        for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+            if (pk.width == 64) mfn_field::pack_elem<_Float16, 64>(t, pk.px, pk.pr, pk.out);
+            else mfn_field::pack_elem<_Float16, 128>(t, pk.px, pk.pr, pk.out);
+        }
     }
     // step count / skip count / loss scale, and level_l1 zeroed for the next step's field_bw, by the
     // last workgroup (every workgroup has read level_l1, step_dev and the flag by now)
@@ -879,16 +797,9 @@ int64_t dense_entries_of(const mfnerf_grid_desc* d) {
     return e;
 }
 
-// grid_bw's workgroup count cap (grid-stride beyond it).  MFNERF_GRID_BW_BLOCKS overrides the
-// default for tuning experiments (tools/); read once.
-int64_t grid_bw_block_cap() {
-    static const int64_t cap = [] {
-        const char* e = getenv("MFNERF_GRID_BW_BLOCKS");
-        const long v = e ? atol(e) : 0;
-        return (int64_t)(v > 0 ? v : 4096);
-    }();
-    return cap;
-}
+// grid_bw's workgroup count cap (grid-stride beyond it; 4096 / 1024 / 512 / 256 / 128 measured
+// 832 / 860 / 855 / 869 / 1166 us for the round-1 float scatter)
+int64_t grid_bw_block_cap() { return 4096; }
 
 int check_desc(const mfnerf_grid_desc* d, const char* what) {
     if (!d) { mfn_set_error("%s: null grid desc", what); return MFN_ERR_INVALID; }
@@ -1077,10 +988,10 @@ __device__ __forceinline__ int wave_block_scan(int v, int* out) {
 }
 
 // Records live in fixed slots: unit u's records of bin b at rec[(b * UNITS + u) * slot + k],
-// k < scnt[b * UNITS + u] -- no counting pass, no scan.  slot = 2 * (mean records per slot at this
-// step's live count) -- 3 x the mean + 96, so the buffer (sized for the largest live count) always holds them; a
-// slot that still overflows (a pathological sample distribution) raises `ovf`, and then the
-// accumulate stores nothing and bin_fallback_kernel scatters the binned levels by atomics instead.
+// k < scnt[b * UNITS + u] -- no counting pass, no scan.  slot = 3 x the mean records per slot at this
+// step's live count + 96, so the buffer (sized for the largest live count) holds them; the records
+// of a slot that still overflows (a sample distribution far from uniform) go into the table by
+// atomics (overflow_add), and `ovf` tells the accumulate to add them to its image.
 constexpr int UNITS = 256;       // scatter workgroups, each owning a contiguous sample range
 constexpr int SC_THREADS = 1024;
 constexpr int MAX_TBINS = 1024;  // bins of one table
@@ -1091,10 +1002,34 @@ constexpr int SC_STAGE = SC_THREADS * 8;  // staged records per tile (8 per thre
 __host__ __device__ __forceinline__ int64_t slot_size(int64_t nn, const BinPlan& P) {
     const int64_t recs = nn * P.n_binned * (P.pair_ok ? 4 : 8);
     const int64_t s = 3 * ((recs + (int64_t)P.n_bins * UNITS - 1) / ((int64_t)P.n_bins * UNITS)) + 96;
-#ifndef MFN_SLOT_ALIGN
-#define MFN_SLOT_ALIGN 16  // 16 records = 192 B: every slot starts on a 64-B line
-#endif
-    return (s + MFN_SLOT_ALIGN - 1) / MFN_SLOT_ALIGN * MFN_SLOT_ALIGN;
+    return (s + 15) / 16 * 16;  // 16 records = 192 B: every slot starts on a 64-B line
+}
+
+// A record past its slot's capacity (a sample distribution far from uniform over the partitions):
+// added straight into the table gradient by 64-bit packed integer atomics (f1 * 2^32 + f0 per entry,
+// each contribution rounded once to the table's int32 unit), and the accumulate then adds the
+// partition's gradient words to its image (bin_scatter raises ovf).  Exact integer sums: the order
+// of the two paths does not matter.
+__device__ __forceinline__ void overflow_add(const BinPlan& P, int* __restrict__ grad, int bin, uint3 r) {
+    const int t = bin_table(P, bin);
+    const int64_t base = (int64_t)P.t_offset[t] + ((int64_t)(bin - P.t_bin0[t]) << P.shift);
+    const uint32_t w = r.x;
+    const float a = __uint_as_float(r.y), b = __uint_as_float(r.z);
+    const float fx = (float)(w >> 17) * (1.0f / 32768.0f);
+    const int e0 = w & ((1 << P.shift) - 1);
+    auto add = [&](int e, float wt) {
+        const int q0 = (int)rintf(wt * a), q1 = (int)rintf(wt * b);
+        const long long pq = (long long)((uint64_t)(uint32_t)q1 << 32) + (long long)q0;
+        if (pq != 0)
+            __hip_atomic_fetch_add(reinterpret_cast<long long*>(grad) + base + e, pq, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (w & (1u << 15)) {
+        add(e0, (w & (1u << 16)) ? fx : 1.0f - fx);
+    } else {
+        add(e0, 1.0f - fx);
+        add(e0 ^ ((2 << ((w >> 11) & 15)) - 1), fx);
+    }
 }
 
 // pass 1: unit u (one 1024-thread workgroup) walks its samples, staged in registers, level by level
@@ -1117,7 +1052,8 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                                                                  const float* __restrict__ level_l1,
                                                                  uint3* __restrict__ rec, int32_t* __restrict__ scnt,
                                                                  uint32_t* __restrict__ smax,
-                                                                 int32_t* __restrict__ ovf, int64_t n_slots) {
+                                                                 int32_t* __restrict__ ovf, int64_t n_slots,
+                                                                 int* __restrict__ grad) {
     constexpr int SPT = PAIR ? 2 : 1;  // samples per thread per tile
     __shared__ int cursor[MAX_BINS];
     __shared__ int hist[MAX_TBINS], toff[MAX_TBINS], gdst[2][MAX_TBINS];
@@ -1148,13 +1084,15 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
         for (int k = threadIdx.x; k < total; k += SC_THREADS) {
             const int lb = sbin[k];
             const int pos = gd[lb] + k;  // position in the unit's slot of the bin
+            const uint3 r = stage[k];
             if (pos < slot) {
                 uint3* dst = rec + ((int64_t)(prev_b0 + lb) * UNITS + u) * slot + pos;
-                const uint3 r = stage[k];
                 // nontemporal: streamed once here, read once by the accumulate
                 __builtin_nontemporal_store(r.x, &dst->x);
                 __builtin_nontemporal_store(r.y, &dst->y);
                 __builtin_nontemporal_store(r.z, &dst->z);
+            } else {
+                overflow_add(P, grad, prev_b0 + lb, r);  // a full slot: straight into the table
             }
         }
     };
@@ -1253,13 +1191,19 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
             smax[u] = mx;
         }
     }
-    bool over = false;
+    // ovf[0]: this step's overflowed records (the accumulate adds the gradient words when non-zero;
+    // zeroed by the next step's first scatter launch); ovf[1]: their running total (never reset by
+    // the kernels: mfnerf_grid_encode_bw_binned_flag_offset + 4 bytes, read by the training tools)
+    int over = 0;
     for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x) {
         const int c = cursor[b];
-        over |= c > slot;
+        over += c > slot ? (int)(c - slot) : 0;
         scnt[(int64_t)b * UNITS + u] = c;
     }
-    if (over) atomicOr(ovf, 1);
+    if (over) {
+        atomicAdd(ovf, over);
+        atomicAdd(ovf + 1, over);
+    }
 }
 
 // pass 2: one workgroup per partition sums the partition's records (every unit's slot) into an LDS
@@ -1329,7 +1273,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
                         (int64_t)rest_b * blockDim.x + threadIdx.x, X.end4, (int64_t)X.n_blocks * blockDim.x);
         return;
     }
-    if (*ovf) return;  // a slot overflowed: bin_fallback_kernel scatters the binned levels
+    const bool add_words = *ovf != 0;  // a slot overflowed: its records are in the gradient words
     __shared__ unsigned long long img[MAX_BIN_ENTRIES];
     const int bin = (int)blockIdx.x - (X.first ? X.n_blocks : 0);
     const int n_ent = 1 << P.shift, mask = n_ent - 1;
@@ -1352,7 +1296,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
 #pragma unroll
         for (int q = 0; q < QF; ++q) {
             const int u = u0 + q * n_hw;
-            c[q] = u < UNITS ? cnt[u] : 0;
+            c[q] = u < UNITS ? min(cnt[u], (int32_t)slot) : 0;  // (records past a full slot: overflow_add)
             const uint3* sl = base + (int64_t)(u < UNITS ? u : 0) * slot;
             r[q] = sl[hl];
         }
@@ -1363,19 +1307,24 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     // the partition's bound (sum over units of count x max), summed in a fixed order -> its unit 2^-k
     __shared__ float wsum[ACC_THREADS / 64];
     float term = 0.0f;
+    bool full = false;  // a slot of this partition overflowed (its extra records: overflow_add)
     if ((int)threadIdx.x < UNITS) {
         const int u = threadIdx.x;
         term = (float)min(cnt[u], (int32_t)slot) * __uint_as_float(smax[u]);
+        full = cnt[u] > slot;
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) term += __shfl_xor(term, off, 64);
     if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = term;
-    __syncthreads();
+    full = __syncthreads_or(full);
     float bound = 0.0f;
 #pragma unroll
     for (int k = 0; k < ACC_THREADS / 64; ++k) bound += wsum[k];
     int kbits = 0;
-    if (bound > 0.0f) {
+    // a partition with an overflowed slot sums at the table's own unit: every contribution, in the
+    // image or added by overflow_add, is then rounded alike, so the sum does not depend on which of
+    // them (an LDS-atomic arrival order) went past the slot -- bit-reproducible
+    if (bound > 0.0f && !full) {
         int e;
         frexpf(bound * 1.0001f, &e);  // bound (with margin for its own rounding) < 2^e
         kbits = max(0, min(30, 30 - e));
@@ -1402,7 +1351,20 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         // the gradient words are left alone (zero)
         const float sc = table_fixed_scale(D, level_l1, P.t_level[t]);
         const float is = sc > 0.0f ? 1.0f / sc : 0.0f;
+        if (add_words) {  // the overflowed records' sums join the image; the words are zeroed
+            __syncthreads();
+            for (int i = threadIdx.x; i < n_e; i += blockDim.x) {
+                const int2 g = reinterpret_cast<const int2*>(dst)[i];  // overflow_add's packed word
+                const unsigned long long w = img[i];
+                const int lo = (int)(uint32_t)w, hi = (int)(uint32_t)(w >> 32) + (lo < 0);
+                const int o0 = ((lo + rnd) >> kbits) + g.x, o1 = ((hi + rnd) >> kbits) + g.y + (g.x < 0);
+                img[i] = ((unsigned long long)(uint32_t)o1 << 32) + (unsigned long long)(long long)o0;
+                reinterpret_cast<int2*>(dst)[i] = make_int2(0, 0);
+            }
+            __syncthreads();
+        }
         if (A.amp && A.amp->nonfinite) return;  // GradScaler skip: no update (gradient words stay zero)
+        const int kb = add_words ? 0 : kbits, rd = add_words ? 0 : rnd;  // (image now in table units)
         const int stp = *A.step_dev + 1;
         const float lr = A.lr_dev ? *A.lr_dev : A.lr;
         const float bc1 = 1.0f - powf(A.beta1, (float)stp);
@@ -1415,7 +1377,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         for (int i = threadIdx.x; i < n_e; i += blockDim.x) {
             const unsigned long long w = img[i];
             const int lo = (int)(uint32_t)w, hi = (int)(uint32_t)(w >> 32) + (lo < 0);
-            const float g0 = (float)((lo + rnd) >> kbits) * is, g1 = (float)((hi + rnd) >> kbits) * is;
+            const float g0 = (float)((lo + rd) >> kb) * is, g1 = (float)((hi + rd) >> kb) * is;
             float2 p = pp[i], m = mm[i], v = vv[i];
             mfn::adam_elem(p.x, m.x, v.x, g0, A.beta1, A.beta2, A.eps, lr, bc1, bc2);
             mfn::adam_elem(p.y, m.y, v.y, g1, A.beta1, A.beta2, A.eps, lr, bc1, bc2);
@@ -1430,22 +1392,14 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         const unsigned long long v = img[i];
         const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32) + (lo < 0);
         // back to the table's unit, rounded once (|fields| <= 2^30: no overflow adding rnd)
-        reinterpret_cast<int2*>(dst)[i] = make_int2((lo + rnd) >> kbits, (hi + rnd) >> kbits);
+        int2 o = make_int2((lo + rnd) >> kbits, (hi + rnd) >> kbits);
+        if (add_words) {
+            const int2 g = reinterpret_cast<const int2*>(dst)[i];  // overflow_add's packed f1 * 2^32 + f0
+            o.x += g.x;
+            o.y += g.y + (g.x < 0);
+        }
+        reinterpret_cast<int2*>(dst)[i] = o;
     }
-}
-
-// the binned levels by request-shaped int32 atomics (grid_bw_body), only if a slot overflowed (a
-// launch of its own: grid_bw_body's registers inside bin_accum_kernel halve that kernel's occupancy)
-template <int MAXL>
-__global__ __launch_bounds__(ENC_BLOCK) void bin_fallback_kernel(const float* __restrict__ X, int64_t n,
-                                                                 const int32_t* __restrict__ n_dev, float x_min,
-                                                                 float x_range, const mfnerf_grid_desc D,
-                                                                 const float* __restrict__ dy, float* grad,
-                                                                 const float* __restrict__ level_l1,
-                                                                 const int32_t* __restrict__ ovf, int levels) {
-    if (!*ovf) return;
-    grid_bw_body<0, MAXL, true>(blockIdx.x, gridDim.x, X, n, n_dev, x_min, x_range, D, dy, grad, nullptr, 0,
-                                level_l1, levels);
 }
 
 // The plan for a desc: binned levels = every level that is not a dense own table; tables in address
@@ -1499,19 +1453,17 @@ int bin_plan(const mfnerf_grid_desc* d, BinPlan* P) {
     return nb > MAX_BINS ? -1 : nb;
 }
 
-// first level routed through the bins (the dense levels before it use grid_bw_dense_kernel)
-// The partitioned levels: by default every hashed level (MFNERF_BIN_LEVELS=k: only the last k
-// hashed ones, the coarser hashed levels then staying on run-merging atomics) -- extended down to
-// every level that shares a table with them (MixedFeature), since a partition is stored whole.
+// first level routed through the bins (the dense levels before it use grid_bw_dense_kernel): every
+// hashed level (binning only the last 6 measured 392 vs 365 us for the scatter in round 2) --
+// extended down to every level that shares a table with them (MixedFeature), since a partition is
+// stored whole.
 int first_binned_level(const mfnerf_grid_desc* d) {
-    static const int knob = [] { const char* e = getenv("MFNERF_BIN_LEVELS"); return e ? atoi(e) : MFN_MAX_LEVELS; }();
     int first_hashed = d->n_levels;
     for (int l = 0; l < d->n_levels; ++l) {
         const uint64_t r = d->res[l];
         if (!(d->table_kind[l] == 0 && r * r * r <= d->size[l])) { first_hashed = l; break; }
     }
-    int l0 = d->n_levels - knob;
-    if (l0 < first_hashed) l0 = first_hashed;
+    int l0 = first_hashed;
     for (bool moved = true; moved;) {
         moved = false;
         for (int a = first_hashed; a < l0 && !moved; ++a)
@@ -1607,12 +1559,12 @@ int mfnerf_grid_encode_bw_scatter(const float* x, int64_t n, const int32_t* n_de
     const int64_t dense = workspace ? dense_entries_of(desc) : 0;
     const bool big = desc->n_levels > 16;
     if (level_l1) {
-        auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, true> : grid_bw_kernel<0, 16, true>;
+        auto kern = big ? grid_bw_kernel<MFN_MAX_LEVELS, true> : grid_bw_kernel<16, true>;
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range,
                            *desc, dL_dout, grad_table, (float*)workspace, dense, level_l1, desc->n_levels,
                            (int32_t*)nullptr);
     } else {
-        auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, false> : grid_bw_kernel<0, 16, false>;
+        auto kern = big ? grid_bw_kernel<MFN_MAX_LEVELS, false> : grid_bw_kernel<16, false>;
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range,
                            *desc, dL_dout, grad_table, (float*)workspace, dense, (const float*)nullptr,
                            desc->n_levels, (int32_t*)nullptr);
@@ -1686,14 +1638,13 @@ int mfnerf_adam_step_fixed_partial(float* params, float* grads, float* m, float*
     // memory-side atomic on ONE address each, serialised: ~13 ns apiece), so an idle workgroup is
     // not free (4096 of them cost ~55 us in the fused_from case); grid-stride covers the rest
     const int64_t want = div_up<int64_t>((fused_ovf ? fused_from : n) / 4, 256);
-#ifndef MFN_ADAM_BLOCKS
-#define MFN_ADAM_BLOCKS 1024  // measured: 4096 -> 1024 workgroups 88 -> 78 us (fewer tickets, same bandwidth)
-#endif
+    // measured: 4096 -> 1024 workgroups 88 -> 78 us (fewer tickets, same bandwidth)
+    constexpr int64_t ADAM_BLOCKS = 1024;
     hipLaunchKernelGGL(adam_fixed_kernel,
-                       dim3((unsigned)(want < MFN_ADAM_BLOCKS ? (want < 1 ? 1 : want) : MFN_ADAM_BLOCKS)), dim3(256), 0,
+                       dim3((unsigned)(want < ADAM_BLOCKS ? (want < 1 ? 1 : want) : ADAM_BLOCKS)), dim3(256), 0,
                        stream, params, grads, m, v, (__half*)p_f16, n, table_offset, (int*)workspace, 2 * dense,
                        total, *desc, level_l1, lr, beta1, beta2, eps, step_dev, lr_dev, amp, desc->n_levels,
-                       fused_from, fused_ovf, 0);
+                       fused_from, fused_ovf, 0, PackArgs{nullptr, nullptr, nullptr, 0});
     if (!amp)  // else the kernel's last workgroup did it
         hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, amp, level_l1, desc->n_levels);
     return mfn_check_launch("adam_step_fixed");
@@ -1742,19 +1693,6 @@ __global__ __launch_bounds__(256) void level_l1_kernel(const float* __restrict__
     if (threadIdx.x < L) atomicAdd(out + threadIdx.x, part[threadIdx.x]);
 }
 
-int mfnerf_debug_grid_bw_half(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
-                              const mfnerf_grid_desc* desc, const float* dL_dout, void* grad_h2, void* priv_h2,
-                              float gscale, mfnerf_stream_t stream) {
-    if (desc->n_levels > 16) { mfn_set_error("grid_bw_half: n_levels <= 16 only"); return MFN_ERR_INVALID; }
-    const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16), ENC_BLOCK / 64);
-    const int64_t cap = grid_bw_block_cap();
-    const int64_t blocks = want < cap ? want : cap;
-    const int64_t dense = priv_h2 ? dense_entries_of(desc) : 0;
-    hipLaunchKernelGGL(grid_bw_h2_kernel<16>, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min,
-                       x_range, *desc, dL_dout, (h2v*)grad_h2, (h2v*)priv_h2, dense, gscale);
-    return mfn_check_launch("grid_bw_half");
-}
-
 int mfnerf_grid_level_l1(const float* dL_dout, int64_t n, const int32_t* n_dev, int n_levels, float* out,
                          mfnerf_stream_t stream) {
     if (n < 0 || n_levels <= 0 || n_levels > MFN_MAX_LEVELS || !out || (n > 0 && !dL_dout)) {
@@ -1767,23 +1705,6 @@ int mfnerf_grid_level_l1(const float* dL_dout, int64_t n, const int32_t* n_dev, 
     hipLaunchKernelGGL(level_l1_kernel, dim3((unsigned)(want < 256 ? (want < 1 ? 1 : want) : 256)), dim3(256), 0,
                        stream, dL_dout, n, n_dev, n_levels, out);
     return mfn_check_launch("grid_level_l1");
-}
-
-// Debug (not part of the training path): the same launch with an ablated kernel body.
-int mfnerf_debug_grid_bw_ablate(int mode, const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
-                                const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
-                                mfnerf_stream_t stream) {
-    const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16), ENC_BLOCK / 64);
-    const int64_t blocks = want < 4096 ? want : 4096;
-    if (desc->n_levels > 16) { mfn_set_error("grid_bw_ablate: n_levels <= 16 only"); return MFN_ERR_INVALID; }
-    auto k = mode == 1   ? grid_bw_kernel<1, 16, false>
-             : mode == 2 ? grid_bw_kernel<2, 16, false>
-             : mode == 3 ? grid_bw_kernel<3, 16, false>
-                         : grid_bw_kernel<0, 16, false>;
-    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc,
-                       dL_dout, grad_table, nullptr, (int64_t)0, (const float*)nullptr, desc->n_levels,
-                       (int32_t*)nullptr);
-    return mfn_check_launch("grid_bw_ablate");
 }
 
 // Partitioned (binned) fixed-point table-gradient scatter: the dense levels through grid_bw_body's
@@ -1818,7 +1739,11 @@ int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32
                                           const mfnerf_grid_desc* desc, const float* dL_dout, float* grads,
                                           int64_t n_params, void* workspace, int64_t n_slots, float* level_l1,
                                           const mfnerf_adam_fused* adam, int32_t* step_dev, mfnerf_amp_state* amp,
-                                          mfnerf_stream_t stream) {
+                                          void* packed, int rgb_width, mfnerf_stream_t stream) {
+    if (packed && ((rgb_width != 64 && rgb_width != 128) || !adam || !adam->p16)) {
+        mfn_set_error("grid_encode_bw_binned_adam_all: the repack needs rgb_width 64 or 128 and adam->p16");
+        return MFN_ERR_INVALID;
+    }
     if (!adam || !adam->params || !adam->m || !adam->v || !grads || !step_dev || adam->step_dev != step_dev ||
         adam->amp != amp || (((uintptr_t)adam->params | (uintptr_t)adam->m | (uintptr_t)adam->v |
                               (uintptr_t)grads) & 15) || (adam->p16 && ((uintptr_t)adam->p16 & 7)) ||
@@ -1845,22 +1770,22 @@ int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32
     binned_workspace_layout(desc, n_slots <= 0 || n_slots > n ? n : n_slots, (char*)workspace, &W);
     // [0, fused_from) by the accumulate launch's leading workgroups (one float4 per thread, <= 256 of them)
     AdamRest X{grads, (int*)workspace, 2 * dense_entries_of(desc), total, fused_from / 4, 0, 1};
-    static const int knobs[2] = {
-        [] { const char* e = getenv("MFNERF_ADAM_REST_BLOCKS"); return e ? atoi(e) : 256; }(),
-        [] { const char* e = getenv("MFNERF_ADAM_REST_FIRST"); return e ? atoi(e) : 1; }()};
+    // <= 256 workgroups, the grid's first (256 vs 64 of them 0.655 vs 0.657 ms/step; first vs last
+    // in the grid within noise)
     const int64_t want = div_up<int64_t>(fused_from / 4, ACC_THREADS);
-    X.n_blocks = (int)(want < 1 ? 1 : (want < knobs[0] ? want : knobs[0]));
-    X.first = knobs[1];
+    X.n_blocks = (int)(want < 1 ? 1 : (want < 256 ? want : 256));
+    X.first = 1;
     st = binned_impl(x, n, n_dev, x_min, x_range, desc, dL_dout, grads + adam->table_offset, workspace, n_slots,
                      level_l1, 3, adam, stream, &X);
     if (st) return st;
-    // after the overflow fallback: the partitioned tables' values if a slot overflowed (else
-    // nothing), then the step's bookkeeping (step count, loss scale, level_l1 zeroed) by the last
+    // the MLP repack and the step's bookkeeping (step count, loss scale, level_l1 zeroed) by the last
     // workgroup -- after every workgroup of the accumulate has read them
     hipLaunchKernelGGL(adam_fixed_kernel, dim3(64), dim3(256), 0, stream, adam->params, grads, adam->m, adam->v,
                        (__half*)adam->p16, n_params, adam->table_offset, (int*)workspace, 2 * dense_entries_of(desc),
                        total, *desc, level_l1, adam->lr, adam->beta1, adam->beta2, adam->eps, step_dev, adam->lr_dev,
-                       amp, desc->n_levels, fused_from, (const int32_t*)W.ovf, 1);
+                       amp, desc->n_levels, fused_from, (const int32_t*)W.ovf, 1,
+                       PackArgs{(const _Float16*)adam->p16, (const _Float16*)adam->p16 + mfn_field::N_XYZ_PARAMS,
+                                (_Float16*)packed, rgb_width});
     if (!amp)
         hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, amp, level_l1, desc->n_levels);
     return mfn_check_launch("grid_encode_bw_binned_adam_all");
@@ -1909,7 +1834,6 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
     const int64_t cap = grid_bw_block_cap();
     const int64_t atomic_blocks = want < cap ? want : cap;
     const bool big = desc->n_levels > 16;
-    static const int dense_mode = [] { const char* e = getenv("MFNERF_DENSE_SCATTER"); return e ? atoi(e) : 1; }();
     int n_dense_levels = 0;  // leading levels that are dense own tables inside the private copies
     {
         const int64_t de = dense_entries_of(desc);
@@ -1917,7 +1841,7 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
                (int64_t)desc->offset[n_dense_levels] + desc->size[n_dense_levels] <= de)
             ++n_dense_levels;
     }
-    if ((parts & 1) && l_first > 0 && dense_mode && l_first <= n_dense_levels) {
+    if ((parts & 1) && l_first > 0 && l_first <= n_dense_levels) {
         // levels [0, l_first) all dense: one sample per lane, packed 64-bit adds into the copies
         const int64_t wb = div_up<int64_t>(n, (int64_t)64 * DENSE_WIN * (ENC_BLOCK / 64));
         auto dk = l_first <= 8 ? grid_bw_dense_kernel<4> : l_first <= 16 ? grid_bw_dense_kernel<8> : grid_bw_dense_kernel<16>;
@@ -1925,7 +1849,7 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
                            x, n, n_dev, x_min, x_range, *desc, dL_dout, W.priv, dense_entries_of(desc), level_l1,
                            l_first, (parts & 2) ? W.ovf : (int32_t*)nullptr);
     } else if ((parts & 1) && l_first > 0) {  // dense levels [0, l_first): request-shaped atomics, private copies
-        auto kern = big ? grid_bw_kernel<0, MFN_MAX_LEVELS, true> : grid_bw_kernel<0, 16, true>;
+        auto kern = big ? grid_bw_kernel<MFN_MAX_LEVELS, true> : grid_bw_kernel<16, true>;
         hipLaunchKernelGGL(kern, dim3((unsigned)atomic_blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min,
                            x_range, *desc, dL_dout, grad_table, W.priv, dense_entries_of(desc), level_l1, l_first,
                            (parts & 2) ? W.ovf : (int32_t*)nullptr);
@@ -1944,17 +1868,13 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
                                : P.n_binned <= 12 ? bin_scatter_kernel<12, false>
                                                   : bin_scatter_kernel<MAX_BINNED, false>);
         hipLaunchKernelGGL(sk, dim3(UNITS), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
-                           *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.smax, W.ovf, n_slots);
+                           *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.smax, W.ovf, n_slots, (int*)grad_table);
         mfnerf_adam_fused A{};
         if (adam) A = *adam;
         AdamRest X{};
         if (rest) X = *rest;
         hipLaunchKernelGGL(bin_accum_kernel, dim3(P.n_bins + X.n_blocks), dim3(ACC_THREADS), 0, stream, P, n, n_dev,
                            W.rec, W.scnt, W.smax, W.ovf, (int*)grad_table, n_slots, *desc, level_l1, A, X);
-        // levels [l_first, L) by atomics, only when a slot overflowed (exits at once otherwise)
-        auto fb = big ? bin_fallback_kernel<MFN_MAX_LEVELS> : bin_fallback_kernel<16>;
-        hipLaunchKernelGGL(fb, dim3(256), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min, x_range, *desc, dL_dout,
-                           grad_table, level_l1, W.ovf, (l_first << 8) | desc->n_levels);
     }
     return mfn_check_launch("grid_encode_bw_binned");
 }

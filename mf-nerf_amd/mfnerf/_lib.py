@@ -78,19 +78,16 @@ SIGNATURES = {
     "mfnerf_grid_encode_bw_binned_adam": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _I64,
                                               _P, ctypes.POINTER(AdamFused), _P]),
     "mfnerf_grid_encode_bw_binned_adam_all": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _I64, _P,
-                                                  _I64, _P, ctypes.POINTER(AdamFused), _P, _P, _P]),
+                                                  _I64, _P, ctypes.POINTER(AdamFused), _P, _P, _P, _I, _P]),
     "mfnerf_grid_binned_first_value": (_I64, [ctypes.POINTER(GridDesc)]),
     "mfnerf_grid_encode_bw_binned_flag_offset": (_I64, [ctypes.POINTER(GridDesc), _I64]),
     "mfnerf_grid_level_l1": (_I, [_P, _I64, _P, _I, _P, _P]),
-    "mfnerf_debug_grid_bw_half": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _F, _P]),
-    "mfnerf_debug_grid_bw_ablate": (_I, [_I, _P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P]),
     "mfnerf_field_packed_bytes": (_I64, [_I]),
     "mfnerf_field_pack_weights_f16": (_I, [_P, _P, _I, _P, _P]),
     "mfnerf_field_pack_weights": (_I, [_P, _P, _I, _P, _P]),
     "mfnerf_field_fw": (_I, [_P, _I64, _P, _I64, _P, _P, _I, _I, _P, _P, _P]),
     "mfnerf_field_bw_workspace": (_I64, [_I64, _I]),
     "mfnerf_field_bw": (_I, [_P, _I64, _P, _I64, _P, _P, _I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P]),
-    "mfnerf_debug_mfma_probe": (_I, [_P, _P, _P, _P]),
     "mfnerf_occupancy_workspace": (_I64, [_I, _I]),
     "mfnerf_occupancy_points": (_I64, [_I, _I, _I64, _I]),
     "mfnerf_occupancy_cells": (_I, [_P, _I, _I, _F, _I64, _I, _F, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P]),

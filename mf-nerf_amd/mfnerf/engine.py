@@ -69,7 +69,8 @@ class StepConfig:
     binned_grid: bool = os.environ.get("MFNERF_BINNED", "1") == "1"
     # the binned scatter's record slots are sized for this many samples per ray (the capacity is
     # max_samples = 1024 per ray; trained scenes march ~60): a step marching more than ~3x this
-    # (the first steps, before the occupancy grid is pruned) takes the atomic fallback
+    # (the first steps, before the occupancy grid is pruned) overflows slots, whose extra records
+    # are added by integer atomics (same sums, slower)
     bin_samples_per_ray: int = 128
 
 
@@ -473,10 +474,11 @@ class TrainStep:
         if self._binned() and fuse_adam == "all":
             self._fused_args = self._adam_fused_args()  # kept alive: graphs capture the call
             amp = self._amp_ptr()
+            # the last pass also repacks the MLP weights (no _pack() launch after it)
             call("mfnerf_grid_encode_bw_binned_adam_all", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min,
                  self.x_range, self.desc, ptr(t.dfeat), ptr(self.grads), self.n_alloc, ptr(t.grid_ws),
                  self._bin_slots(), ptr(self._level_l1), ctypes.byref(self._fused_args), ptr(self.step_dev),
-                 amp, stream())
+                 amp, ptr(self.packed), self.cfg.rgb_width, stream())
             return
         if self._binned() and fuse_adam:
             self._fused_args = self._adam_fused_args()  # kept alive: graphs capture the call
@@ -502,8 +504,7 @@ class TrainStep:
         (mfnerf_grid_encode_bw_binned_adam_all); MFNERF_FUSED_ADAM_ALL=0 keeps it a pass of its own
         after the scatter (mfnerf_adam_step_fixed_partial).  Same bits either way."""
         if os.environ.get("MFNERF_FUSED_ADAM_ALL", "1") == "1":
-            self._grid_bw(self.mbuf[j], 0, fuse_adam="all")
-            self._pack()
+            self._grid_bw(self.mbuf[j], 0, fuse_adam="all")  # + the repack
         else:
             self._grid_bw(self.mbuf[j], 0, fuse_adam=True)
             self._finish_update(partial=True)
@@ -567,6 +568,15 @@ class TrainStep:
         full = self.params.clone()
         dp.all_gather_(full, self.shard[0])
         return full
+
+    def overflow_records(self):
+        """Records the partitioned scatter could not place in their slots so far (added by integer
+        atomics instead; a running total kept by the kernel; host read).  0 without partitions."""
+        if not self._binned():
+            return 0
+        off = load().mfnerf_grid_encode_bw_binned_flag_offset(self.desc, self._bin_slots())
+        ws = self.parts[0].grid_ws
+        return int(ws.view(torch.int32)[off // 4 + 1])
 
     def skipped_steps(self):
         """Optimizer steps skipped on non-finite gradients so far (host read)."""

@@ -147,7 +147,10 @@ class Trainer:
         pred = torch.cat(preds)
         return {"step": self.global_step, "loss": float(st.loss_sum), "psnr": psnr(pred, b.rgb),
                 "rm_s": float(st.live_samples()) / st.cfg.n_rays,
-                "lr": float(st.lr_dev), "skipped": st.skipped_steps()}
+                "lr": float(st.lr_dev), "skipped": st.skipped_steps(),
+                # records the partitioned table-gradient scatter could not place in its slots so far
+                # (added by integer atomics instead: same sums, slower)
+                "overflow_records": st.overflow_records()}
 
     # ---------------------------------------------------------------- evaluation / checkpoints
     def to_ngp(self):

@@ -13,7 +13,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _make(gpu, parts=2, **kw):
-    st = engine.TrainStep(engine.StepConfig(n_rays=1024, log2_T=16, n_parts=parts, **kw), device=gpu, seed=0)
+    kw = {"n_rays": 1024, "log2_T": 16, **kw}
+    st = engine.TrainStep(engine.StepConfig(n_parts=parts, **kw), device=gpu, seed=0)
     st.set_occupancy(synthetic.ball_density_grid())
     return st
 
@@ -264,9 +265,16 @@ def test_partitioned_accumulate_with_fused_adam_matches_unfused(gpu, kw, skip, m
     torch.cuda.synchronize()
     if mode == "all-overflow":
         ovf = load().mfnerf_grid_encode_bw_binned_flag_offset(st.desc, st._bin_slots()) // 4
-        assert int(ws[ovf].view(torch.int32)) == 1  # the fallback path really ran
+        # the overflow path really ran: records past full slots went into the table by atomics
+        assert int(ws[ovf].view(torch.int32)) > 0
     for k in names:
-        assert torch.equal(getattr(st, k), ref[k]), k
+        got = getattr(st, k)
+        if not torch.equal(got, ref[k]):
+            d = (got.float() - ref[k].float()).abs()
+            bad = torch.nonzero(d.flatten() > 0).flatten()
+            raise AssertionError(f"{k}: {bad.numel()} values differ, first {bad[:8].tolist()}, max {float(d.max())}, "
+                                 f"off_table {st.off_table}, first partitioned value "
+                                 f"{st.off_table + load().mfnerf_grid_binned_first_value(st.desc)}")
     nc = load().mfnerf_grid_encode_bw_workspace(st.desc) // 4  # the private copies: zeroed by both
     assert not bool(ws[:nc].any()) and not bool(ref_ws[:nc].any()) and not bool(st.grads.any())
     if not skip:
@@ -290,7 +298,8 @@ def test_gated_replay_with_distortion_loss_keeps_the_gate_in_step(gpu):
         a.replay(batches[k], next_batch=batches[k + 1] if k + 1 < K else None)
     t1.record()
     torch.cuda.synchronize()
-    assert a._gate.tolist() == [K - 1, K - 1]       # every signal waited for, no wait timed out
+    # replays 1..K-2 ran as one gated graph (the last has no next batch); every signal waited for
+    assert a._gate.tolist() == [K - 2, K - 2]
     assert t0.elapsed_time(t1) < (K - 1) * engine.GATE_TIMEOUT_US / 1000
     assert torch.equal(a.params, b.params) and torch.equal(a.p16, b.p16)
 

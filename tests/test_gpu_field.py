@@ -2,11 +2,13 @@
 (oracle/field_oracle.py).  tcnn computes in fp16, so the oracle here rounds every MLP operand to
 fp16 exactly where the kernels do and the tolerances are fp16-sized (stated per assert)."""
 import math
+import os
 
 import numpy as np
 import pytest
 import torch
 
+from conftest import ROOT
 from mfnerf import field as FLD
 from mfnerf._lib import call, load, ptr
 from mfnerf.grid import GridLayout
@@ -24,7 +26,12 @@ def test_mfma_f16_lane_maps(gpu):
     B[3, 7] = 3  # asymmetric
     D = torch.empty(32, 32, device=gpu)
     Ag, Bg = A.to(gpu), B.to(gpu)
-    call("mfnerf_debug_mfma_probe", ptr(Ag), ptr(Bg), ptr(D), torch.cuda.current_stream().cuda_stream)
+    # the probe kernel lives in a test-support library (tests/support), not in the product C-ABI
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "tests", "support", "libmfnerf_probe.so"))
+    lib.mfnerf_probe_mfma.argtypes = [ctypes.c_void_p] * 4
+    assert lib.mfnerf_probe_mfma(Ag.data_ptr(), Bg.data_ptr(), D.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
     assert torch.equal(D.cpu(), A.float() @ B.float())
 
 

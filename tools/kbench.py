@@ -34,8 +34,6 @@ def main():
     zeros_samp = torch.zeros(cap, device=dev)
     planes = torch.empty(c.L, cap, 2, dtype=torch.float16, device=dev)
     rowmajor = torch.empty(cap, 2 * c.L, dtype=torch.float16, device=dev)
-    grad_h2 = torch.zeros(step.layout.n_params, dtype=torch.float16, device=dev)
-    priv_h2 = torch.zeros_like(t.grid_ws)
     s = stream
     # the fixed-point scatter's per-level scales: the last Adam pass zeroed level_l1 for the next step,
     # so recompute it from this step's dL/dfeat (else every contribution rounds to 0 and no atomic
@@ -75,8 +73,6 @@ def main():
                                        step.x_range, step.desc, ptr(t.dfeat), ptr(step.grads[step.off_table:]),
                                        ptr(t.grid_ws), step._bin_slots(), ptr(step._level_l1), 2, s()),
         "grid_finish": lambda: step._grid_finish(0),
-        "grid_bw_half": lambda: call("mfnerf_debug_grid_bw_half", ptr(m.xyzs), cap, ptr(m.counter), step.x_min,
-                                     step.x_range, step.desc, ptr(t.dfeat), ptr(grad_h2), ptr(priv_h2), 2048.0, s()),
         "check": lambda: call("mfnerf_check_finite", ptr(step.grads), step.grads.numel(), ptr(step.finite_status), s()),
         "adam": lambda: step._adam(step.grads, 0, step.n_alloc, False),
         "adam_fixed": step._finish_update,  # fused convert + Adam + repack (state changes: timing only)

@@ -57,7 +57,8 @@ def main():
     def log(m):
         hist.append(m)
         print(f"step {m['step']:6d}  loss {m['loss']:.5f}  train psnr {m['psnr']:.2f}  rm_s {m['rm_s']:.1f}  "
-              f"lr {m['lr']:.2e}  t {time.perf_counter() - t0:.1f}s", flush=True)
+              f"lr {m['lr']:.2e}  overflowed records {m['overflow_records']}  t {time.perf_counter() - t0:.1f}s",
+              flush=True)
 
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -79,6 +80,11 @@ def main():
         "train_wall_s": round(wall, 2), "rays_per_s_whole_run": round(steps * hp.batch_size / wall, 1),
         "test_psnr": round(test_psnr, 3), "test_psnr_per_view": [round(v, 3) for v in per_view],
         "white_image_psnr": round(white, 3), "eval_s": round(eval_s, 2), "skipped_steps": hist[-1]["skipped"],
+        # records the partitioned scatter's slots could not hold (added by atomics), per logged
+        # interval of steps_per_epoch steps and in total
+        "overflow_records_total": hist[-1]["overflow_records"],
+        "overflow_records_per_interval": [b["overflow_records"] - a["overflow_records"]
+                                          for a, b in zip([{"overflow_records": 0}] + hist[:-1], hist)],
         "train_log": [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in h.items()} for h in hist],
         "device": torch.cuda.get_device_name(0)}))
 
