@@ -92,7 +92,7 @@ def run_step(step, batch, world, ev=None, allreduce=None):
     step.run(batch, mark=mark, exchange=dp.allreduce_mean_ if allreduce else None)
 
 
-def pmc_traffic(kernel_prefix):
+def pmc_traffic(kernel_prefix, preset="lego"):
     """(HBM-side bytes, memory-side atomic requests, source) per launch, summed over the kernels whose
     names start with one of `kernel_prefix` (one step's launches of them), from the newest
     committed PMC summary (profiles/rNN_*pmc_traffic.json, made by tools/pmc_traffic.py from separate
@@ -104,7 +104,8 @@ def pmc_traffic(kernel_prefix):
     def order(f):  # profiles/rNN_vMM_pmc_traffic.json: newest round, then newest version
         m = re.match(r"r(\d+)(?:_v(\d+))?_", os.path.basename(f))
         return (int(m.group(1)), int(m.group(2) or 0)) if m else (-1, -1)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*pmc_traffic.json")), key=order)
+    suffix = "" if preset == "lego" else "_" + preset  # tools/gpu_pmc.sh PRESET=...
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*pmc_traffic{suffix}.json")), key=order)
     if not files:
         return None, None, None
     d = json.load(open(files[-1]))
@@ -293,8 +294,8 @@ def main():
 
     # roofline: grid_bw (the dominant kernel), timed by events around it inside the timed region
     dom = "grid_bw"
-    # the committed PMC summary is of the lego workload
-    traffic, atomic_req, traffic_src = pmc_traffic(GRID_BW_KERNEL) if args.preset == "lego" else (None, None, None)
+    # the newest committed PMC summary of this preset's workload
+    traffic, atomic_req, traffic_src = pmc_traffic(GRID_BW_KERNEL, args.preset)
     dom_bytes = BYTES_PER_SAMPLE[dom] * mean_samples
     achieved = dom_bytes / (grid_bw_ms * 1e-3) / 1e9
     # the bound the scatter actually meets: memory-side atomic requests per second

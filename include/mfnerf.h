@@ -73,8 +73,9 @@ int mfnerf_morton3d_invert(const int32_t* idx, int64_t n, int32_t* coords, mfner
 int mfnerf_packbits(const float* grid, int64_t n_bytes, float thr, const float* thr_dev, uint8_t* bitfield,
                     mfnerf_stream_t stream);
 
-/* Workspace bytes mfnerf_raymarching_train needs for n_rays rays. */
-int64_t mfnerf_raymarching_train_workspace(int64_t n_rays);
+/* Workspace bytes mfnerf_raymarching_train needs for n_rays rays of at most max_samples samples
+ * (the per-ray counts, and the march's per-ray sample positions t: n_rays x max_samples f32). */
+int64_t mfnerf_raymarching_train_workspace(int64_t n_rays, int max_samples);
 
 /* vren.raymarching_train (binding.cpp:60-85, raymarching.cu:166-332).
  * hits_t: (n_rays,2) f32 rows (t1,t2) with row stride hits_stride floats.

@@ -823,8 +823,9 @@ int check_desc(const mfnerf_grid_desc* d, const char* what) {
 // ~30 adds per step from unrelated rays, so no ordering of the samples lets memory-side atomics
 // merge them (tools/sim_scatter_requests.py: >= 3 requests per sample per fine level in any window
 // of a Morton-sorted batch, 0.13 distinct lines per sample over the whole batch).  Instead each
-// table is cut into 2^shift-entry partitions, every (sample, level, (y,z) corner row) becomes a
-// 12-B record routed to its partition by a counting sort, and one workgroup per partition sums its
+// table is cut into 2^shift-entry partitions, every (sample, level, (y,z) corner row) becomes an
+// 8-B record (entry, x weight, both features' values in fp16: the algorithmic fp16 scatter's own
+// payload; 12 B with f32 values until round 3) routed to its partition by a counting sort, and one workgroup per partition sums its
 // records into an LDS image with integer LDS atomics (ds_add_u32: ~4 T adds/s chip-wide at random
 // addresses, tools/lds_atomic_probe.hip -- 20x ds_add_f32), then stores the image once.  The image
 // holds one 64-bit word per entry: both features' sums in the table's int32 fixed-point unit,
@@ -859,14 +860,28 @@ __device__ __forceinline__ int bin_table(const BinPlan& P, int b) {
 }
 
 // The records of one (sample, binned level j): up to 4 (y,z) rows x (1 or 2 records).  EMIT(bin,
-// rec) is called per record; rec = {w0, a, b} (12 B), a/b = wy*wz*dL/dy_f * scale * 2^32 (scale:
-// the table's int32 fixed-point scale) and
+// rec) is called per record; rec = {w0, a | b << 16} (8 B): a/b = wy*wz*dL/dy_f * scale * 2^-15 as
+// fp16 (scale: the table's int32 fixed-point scale, so |wy*wz*dL/dy_f * scale| < 2^30 and the fp16
+// value < 2^15 never overflows; rounded once to 11 significant bits -- the precision of the fp16
+// operands field_bw computed dL/dy from, and of tcnn's own half-precision gradient, whose SUM is
+// rounded to fp16 at every add) and
 //   w0 = e0 (bits 0-10, entry in the bin) | t << 11 (4 bits) | single << 15 | sel << 16 | fx << 17,
 // fx = the x weight as 15-bit unorm (exact for the fine levels, whose positions carry <= 13
 // fraction bits).  A pair record adds (1-fx)(a,b) to e0 and fx(a,b) to e1 = e0 ^ (2^(t+1) - 1): an
 // own power-of-two hash table has idx(x+1) = idx(x) ^ (x ^ (x+1)), t = trailing ones of x, and the
 // two share a bin unless the carry reaches bit `shift` (1 x in 2^shift).  Otherwise (shared
 // MixedFeature tables, straddles) each entry gets a single record with weight sel ? fx : 1-fx.
+// a record's two values: fp16 of v * 2^-15, round to nearest even (v in the table's int32 units)
+constexpr float REC_DOWN = 1.0f / 32768.0f, REC_UP = 32768.0f;
+__device__ __forceinline__ uint32_t rec_values(float a, float b) {
+    const _Float16 ha = (_Float16)(a * REC_DOWN), hb = (_Float16)(b * REC_DOWN);  // (exact scaling)
+    return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
+}
+// value k of a record (0: a, 1: b) times 2^-15 (scale it by 2^15 x the unit to use)
+__device__ __forceinline__ float rec_value(uint32_t ab, int k) {
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)(ab >> (16 * k)));
+}
+
 template <typename EMIT>
 __device__ __forceinline__ void level_records_geo(const mfnerf_grid_desc& D, const BinPlan& P, int j,
                                                   const LevelGeo& Lg, float g0, float g1, float fs, EMIT&& emit) {
@@ -887,12 +902,12 @@ __device__ __forceinline__ void level_records_geo(const mfnerf_grid_desc& D, con
         const uint32_t i0 = corner_index(D, l, Lg.g[0], gy, gz);
         const uint32_t i1 = corner_index(D, l, Lg.g[0] + 1, gy, gz);
         const int b0 = bin0 + (int)(i0 >> P.shift), b1 = bin0 + (int)(i1 >> P.shift);
-        const uint32_t a = __float_as_uint(wyz * s0), b = __float_as_uint(wyz * s1);
+        const uint32_t ab = rec_values(wyz * s0, wyz * s1);
         // static record slots 2 yz, 2 yz + 1, both always emitted (bin -1: no record), so the
         // caller's per-slot register arrays see constant indices on every path and stay registers
         const bool pair = pair_hash && b0 == b1;
-        emit(2 * yz, b0, make_uint3((i0 & mask) | (pair ? (ones << 11) : (1u << 15)) | fxq, a, b));
-        emit(2 * yz + 1, pair ? -1 : b1, make_uint3((i1 & mask) | (1u << 15) | (1u << 16) | fxq, a, b));
+        emit(2 * yz, b0, make_uint2((i0 & mask) | (pair ? (ones << 11) : (1u << 15)) | fxq, ab));
+        emit(2 * yz + 1, pair ? -1 : b1, make_uint2((i1 & mask) | (1u << 15) | (1u << 16) | fxq, ab));
     }
 }
 
@@ -1002,7 +1017,7 @@ constexpr int SC_STAGE = SC_THREADS * 8;  // staged records per tile (8 per thre
 __host__ __device__ __forceinline__ int64_t slot_size(int64_t nn, const BinPlan& P) {
     const int64_t recs = nn * P.n_binned * (P.pair_ok ? 4 : 8);
     const int64_t s = 3 * ((recs + (int64_t)P.n_bins * UNITS - 1) / ((int64_t)P.n_bins * UNITS)) + 96;
-    return (s + 15) / 16 * 16;  // 16 records = 192 B: every slot starts on a 64-B line
+    return (s + 15) / 16 * 16;  // 16 records = 128 B: every slot starts on a 128-B line
 }
 
 // A record past its slot's capacity (a sample distribution far from uniform over the partitions):
@@ -1010,11 +1025,11 @@ __host__ __device__ __forceinline__ int64_t slot_size(int64_t nn, const BinPlan&
 // each contribution rounded once to the table's int32 unit), and the accumulate then adds the
 // partition's gradient words to its image (bin_scatter raises ovf).  Exact integer sums: the order
 // of the two paths does not matter.
-__device__ __forceinline__ void overflow_add(const BinPlan& P, int* __restrict__ grad, int bin, uint3 r) {
+__device__ __forceinline__ void overflow_add(const BinPlan& P, int* __restrict__ grad, int bin, uint2 r) {
     const int t = bin_table(P, bin);
     const int64_t base = (int64_t)P.t_offset[t] + ((int64_t)(bin - P.t_bin0[t]) << P.shift);
     const uint32_t w = r.x;
-    const float a = __uint_as_float(r.y), b = __uint_as_float(r.z);
+    const float a = rec_value(r.y, 0) * REC_UP, b = rec_value(r.y, 1) * REC_UP;
     const float fx = (float)(w >> 17) * (1.0f / 32768.0f);
     const int e0 = w & ((1 << P.shift) - 1);
     auto add = [&](int e, float wt) {
@@ -1040,7 +1055,7 @@ __device__ __forceinline__ void overflow_add(const BinPlan& P, int* __restrict__
 // bin (~30 records per run at the Lego config: whole-line stores) while the NEXT level counts.  Three
 // barriers per level (count | scan | place), the store overlapping the next count.
 struct BinRec {
-    uint3 r;
+    uint2 r;
     uint32_t meta;  // bin in the table (bits 0-15) | rank in the bin's run (bits 16-31); ~0u: none
 };
 
@@ -1050,18 +1065,18 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                                                                  float x_range, const mfnerf_grid_desc D,
                                                                  const BinPlan P, const float* __restrict__ dy,
                                                                  const float* __restrict__ level_l1,
-                                                                 uint3* __restrict__ rec, int32_t* __restrict__ scnt,
+                                                                 uint2* __restrict__ rec, int32_t* __restrict__ scnt,
                                                                  uint32_t* __restrict__ smax,
                                                                  int32_t* __restrict__ ovf, int64_t n_slots,
                                                                  int* __restrict__ grad) {
     constexpr int SPT = PAIR ? 2 : 1;  // samples per thread per tile
     __shared__ int cursor[MAX_BINS];
     __shared__ int hist[MAX_TBINS], toff[MAX_TBINS], gdst[2][MAX_TBINS];
-    __shared__ uint3 stage[SC_STAGE];
+    __shared__ uint2 stage[SC_STAGE];
     __shared__ uint16_t sbin[SC_STAGE];
     __shared__ float fs_s[MFN_MAX_LEVELS];
     __shared__ int s_total[2];
-    uint32_t rmax = 0u;  // largest |a|, |b| of this thread's records (float bits order as uints)
+    uint32_t rmax = 0u;  // largest |a|, |b| of this thread's records (fp16 bits order as uints)
     load_fixed_scales(D, level_l1, fs_s);
     for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x) cursor[b] = 0;
     for (int b = threadIdx.x; b < MAX_TBINS; b += blockDim.x) hist[b] = 0;
@@ -1084,13 +1099,12 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
         for (int k = threadIdx.x; k < total; k += SC_THREADS) {
             const int lb = sbin[k];
             const int pos = gd[lb] + k;  // position in the unit's slot of the bin
-            const uint3 r = stage[k];
+            const uint2 r = stage[k];
             if (pos < slot) {
-                uint3* dst = rec + ((int64_t)(prev_b0 + lb) * UNITS + u) * slot + pos;
+                uint2* dst = rec + ((int64_t)(prev_b0 + lb) * UNITS + u) * slot + pos;
                 // nontemporal: streamed once here, read once by the accumulate
-                __builtin_nontemporal_store(r.x, &dst->x);
-                __builtin_nontemporal_store(r.y, &dst->y);
-                __builtin_nontemporal_store(r.z, &dst->z);
+                __builtin_nontemporal_store((unsigned long long)r.x | ((unsigned long long)r.y << 32),
+                                            reinterpret_cast<unsigned long long*>(dst));
             } else {
                 overflow_add(P, grad, prev_b0 + lb, r);  // a full slot: straight into the table
             }
@@ -1118,14 +1132,14 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                 const SampleLevel Q = sample_level(D, P, S[q], j);
                 if (live[q] && Q.live)
                     level_records(D, P, j, S[q].x, S[q].y, S[q].z, Q.g0, Q.g1, fs_s[P.level[j]],
-                                  [&](int sl, int bin, uint3 r) {
+                                  [&](int sl, int bin, uint2 r) {
                                       // PAIR: slot 2 yz + 1 never holds a record (pairs never straddle)
                                       const int k = PAIR ? 4 * q + (sl >> 1) : sl;
                                       if (bin < 0 || (PAIR && (sl & 1))) return;
                                       const int lb = bin - b0;
                                       R[k].r = r;
                                       R[k].meta = (uint32_t)lb | ((uint32_t)atomicAdd(&hist[lb], 1) << 16);
-                                      rmax = max(rmax, max(r.y & 0x7fffffffu, r.z & 0x7fffffffu));
+                                      rmax = max(rmax, max(r.y & 0x7fffu, (r.y >> 16) & 0x7fffu));
                                   });
             }
             store_prev();  // the previous level's sorted stage, beside this level's counting
@@ -1188,7 +1202,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
         if (threadIdx.x == 0) {
             uint32_t mx = 0u;
             for (int k = 0; k < SC_THREADS / 64; ++k) mx = max(mx, wmax[k]);
-            smax[u] = mx;
+            smax[u] = __float_as_uint(rec_value(mx, 0) * REC_UP);  // as a float in table units
         }
     }
     // ovf[0]: this step's overflowed records (the accumulate adds the gradient words when non-zero;
@@ -1218,9 +1232,9 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
 __device__ __forceinline__ unsigned long long pack2(float a, float b) {
     return ((unsigned long long)(uint32_t)(int)rintf(b) << 32) + (unsigned long long)(long long)(int)rintf(a);
 }
-__device__ __forceinline__ void accum_record(unsigned long long* img, int mask, uint3 r, float k2) {
+__device__ __forceinline__ void accum_record(unsigned long long* img, int mask, uint2 r, float k2) {
     const uint32_t w = r.x;
-    const float a = __uint_as_float(r.y) * k2, b = __uint_as_float(r.z) * k2;  // exact: a power of two
+    const float a = rec_value(r.y, 0) * k2, b = rec_value(r.y, 1) * k2;  // exact: k2 a power of two
     if (a == 0.0f && b == 0.0f) return;
     const float fx = (float)(w >> 17) * (1.0f / 32768.0f);
     const int e0 = w & mask;
@@ -1250,7 +1264,7 @@ struct AdamRest {
 
 __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, int64_t n,
                                                                 const int32_t* __restrict__ n_dev,
-                                                                const uint3* __restrict__ rec,
+                                                                const uint2* __restrict__ rec,
                                                                 const int32_t* __restrict__ scnt,
                                                                 const uint32_t* __restrict__ smax,
                                                                 const int32_t* __restrict__ ovf,
@@ -1288,16 +1302,16 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     // counts (round 3, 106 VGPRs, 2 workgroups per CU) 157 vs 108 us.
     const int hw = threadIdx.x >> 5, hl = threadIdx.x & 31, n_hw = ACC_THREADS / 32;
     const int32_t* cnt = scnt + (int64_t)bin * UNITS;
-    const uint3* base = rec + (int64_t)bin * UNITS * slot;
+    const uint2* base = rec + (int64_t)bin * UNITS * slot;
     constexpr int QF = 8;
-    uint3 r[QF];
+    uint2 r[QF];
     int c[QF];
     auto prefetch = [&](int u0) {
 #pragma unroll
         for (int q = 0; q < QF; ++q) {
             const int u = u0 + q * n_hw;
             c[q] = u < UNITS ? min(cnt[u], (int32_t)slot) : 0;  // (records past a full slot: overflow_add)
-            const uint3* sl = base + (int64_t)(u < UNITS ? u : 0) * slot;
+            const uint2* sl = base + (int64_t)(u < UNITS ? u : 0) * slot;
             r[q] = sl[hl];
         }
     };
@@ -1329,7 +1343,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         frexpf(bound * 1.0001f, &e);  // bound (with margin for its own rounding) < 2^e
         kbits = max(0, min(30, 30 - e));
     }
-    const float k2 = ldexpf(1.0f, kbits);
+    const float k2 = ldexpf(1.0f, kbits + 15);  // the records' values are 2^-15 x table units
     for (int u0 = hw; u0 < UNITS; u0 += QF * n_hw) {
         if (u0 != hw) prefetch(u0);
 #pragma unroll
@@ -1482,7 +1496,7 @@ struct BinWorkspace {
     float* priv;
     int32_t *scnt, *ovf;
     uint32_t* smax;
-    uint3* rec;
+    uint2* rec;
 };
 
 int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
@@ -1500,9 +1514,9 @@ int64_t binned_workspace_layout(const mfnerf_grid_desc* d, int64_t n_max, char* 
     off += align256(UNITS * 4);
     if (W) W->ovf = reinterpret_cast<int32_t*>(base + off);
     off += 256;
-    if (W) W->rec = reinterpret_cast<uint3*>(base + off);
+    if (W) W->rec = reinterpret_cast<uint2*>(base + off);
     // every slot at the largest live count (the same function the kernels size them with)
-    off += align256(nb * UNITS * slot_size(n_max, P) * (int64_t)sizeof(uint3));
+    off += align256(nb * UNITS * slot_size(n_max, P) * (int64_t)sizeof(uint2));
     return off;
 }
 

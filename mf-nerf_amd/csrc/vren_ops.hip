@@ -224,26 +224,22 @@ __global__ void march_write_kernel(MarchParams p, int64_t n_rays, const int64_t*
 // the lanes then replays the reference's control flow exactly (occupied: emit and step; empty:
 // jump to the first chain point >= the DDA target), and the emitted lanes are compacted with a
 // ballot prefix count.  Bit-identical to march_ray<> (and the oracle), ~64x more parallel.
+// The march runs ONCE: it counts the ray's samples and keeps their t values at tbuf[r * max_samples
+// + j]; after the scan, march_expand_kernel writes the compacted samples from them (x = fmaf(t, d, o)
+// as here, the ray's direction, t, the constant dt).  Until round 3 a second march re-walked every
+// ray to write (count + re-march ~250 us on the side stream, beside the table-gradient scatter).
 __device__ __forceinline__ float readlane_f(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 __device__ __forceinline__ int ffs64(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
 
-template <bool WRITE>
 __global__ __launch_bounds__(256) void march_wave_kernel(MarchParams p, int64_t n_rays, int32_t* __restrict__ counts,
-                                                         const int64_t* __restrict__ rays_a, float* __restrict__ xyzs,
-                                                         float* __restrict__ dirs, float* __restrict__ deltas,
-                                                         float* __restrict__ ts) {
+                                                         float* __restrict__ tbuf) {
     const int lane = threadIdx.x & 63;
     const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (r >= n_rays) return;  // wave-uniform
-    int limit = p.max_samples;
-    int64_t base = 0;
-    if (WRITE) {
-        limit = (int)rays_a[3 * r + 2];
-        base = rays_a[3 * r + 1];
-        if (limit == 0) return;
-    }
+    const int limit = p.max_samples;
+    float* tr = tbuf + r * (int64_t)p.max_samples;
     const float gsi = 1.0f / (float)p.grid_size;
     const float ox = p.o[3 * r], oy = p.o[3 * r + 1], oz = p.o[3 * r + 2];
     const float dx = p.d[3 * r], dy = p.d[3 * r + 1], dz = p.d[3 * r + 2];
@@ -298,16 +294,37 @@ __global__ __launch_bounds__(256) void march_wave_kernel(MarchParams p, int64_t 
                     else { skip = true; pending = target; c = chain_end; }
                 }
             }
-            if (WRITE && ((emit_m >> lane) & 1)) {
-                const int64_t s = base + n0 + __popcll(emit_m & ((1ull << lane) - 1));
-                xyzs[3 * s] = x; xyzs[3 * s + 1] = y; xyzs[3 * s + 2] = z;
-                dirs[3 * s] = dx; dirs[3 * s + 1] = dy; dirs[3 * s + 2] = dz;
-                ts[s] = tl; deltas[s] = dt;
-            }
+            if ((emit_m >> lane) & 1) tr[n0 + __popcll(emit_m & ((1ull << lane) - 1))] = tl;
             t_base = next_base;
         }
     }
-    if (!WRITE && lane == 0) counts[r] = n;
+    if (lane == 0) counts[r] = n;
+}
+
+// The compacted samples of ray r (one wave): its first rays_a[r].count t values from march_wave.
+__global__ __launch_bounds__(256) void march_expand_kernel(MarchParams p, int64_t n_rays,
+                                                           const int64_t* __restrict__ rays_a,
+                                                           const float* __restrict__ tbuf, float* __restrict__ xyzs,
+                                                           float* __restrict__ dirs, float* __restrict__ deltas,
+                                                           float* __restrict__ ts) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (r >= n_rays) return;  // wave-uniform
+    const int cnt = (int)rays_a[3 * r + 2];
+    if (cnt == 0) return;
+    const int64_t base = rays_a[3 * r + 1];
+    const float ox = p.o[3 * r], oy = p.o[3 * r + 1], oz = p.o[3 * r + 2];
+    const float dx = p.d[3 * r], dy = p.d[3 * r + 1], dz = p.d[3 * r + 2];
+    // march_wave's constant step, from the same un-perturbed entry point
+    const float dt = calc_dt(p.hits_t[r * p.hits_stride], p.exp_step, p.max_samples, p.grid_size, p.scale);
+    const float* tr = tbuf + r * (int64_t)p.max_samples;
+    for (int j = lane; j < cnt; j += 64) {
+        const float t = tr[j];
+        const int64_t s = base + j;
+        xyzs[3 * s] = fmaf(t, dx, ox); xyzs[3 * s + 1] = fmaf(t, dy, oy); xyzs[3 * s + 2] = fmaf(t, dz, oz);
+        dirs[3 * s] = dx; dirs[3 * s + 1] = dy; dirs[3 * s + 2] = dz;
+        ts[s] = t; deltas[s] = dt;
+    }
 }
 
 // raymarching_test_kernel (raymarching.cu:335-404) with the calc_dt(..., cascades) quirk.
@@ -775,7 +792,11 @@ int mfnerf_packbits(const float* grid, int64_t n_bytes, float thr, const float* 
     return mfn_check_launch("packbits");
 }
 
-int64_t mfnerf_raymarching_train_workspace(int64_t n_rays) { return ((n_rays * 4 + 255) / 256) * 256; }
+// the per-ray counts, then (constant-dt scenes) the per-ray sample t values of march_wave
+int64_t mfnerf_raymarching_train_workspace(int64_t n_rays, int max_samples) {
+    const int64_t counts = ((n_rays * 4 + 255) / 256) * 256;
+    return counts + (max_samples > 0 ? n_rays * (int64_t)max_samples * 4 : 0);
+}
 
 int mfnerf_raymarching_train(const float* rays_o, const float* rays_d, const float* hits_t, int64_t hits_stride,
                              const uint8_t* bitfield, int cascades, float scale, float exp_step_factor,
@@ -795,18 +816,18 @@ int mfnerf_raymarching_train(const float* rays_o, const float* rays_d, const flo
     MarchParams p{rays_o, rays_d, hits_t, hits_stride, bitfield, cascades, scale, exp_step_factor, noise,
                   grid_size, max_samples};
     int32_t* counts = (int32_t*)workspace;
+    float* tbuf = reinterpret_cast<float*>((char*)workspace + ((n_rays * 4 + 255) / 256) * 256);
     const unsigned nb = blocks_for(n_rays, RAY_BLOCK);
     const bool wave = exp_step_factor == 0.0f;  // constant dt: the wave-per-ray marcher applies
     const unsigned nbw = (unsigned)div_up<int64_t>(n_rays, 4);
     if (wave)
-        hipLaunchKernelGGL(march_wave_kernel<false>, dim3(nbw), dim3(256), 0, stream, p, n_rays, counts, nullptr,
-                           nullptr, nullptr, nullptr, nullptr);
+        hipLaunchKernelGGL(march_wave_kernel, dim3(nbw), dim3(256), 0, stream, p, n_rays, counts, tbuf);
     else
         hipLaunchKernelGGL(march_count_kernel, dim3(nb), dim3(RAY_BLOCK), 0, stream, p, n_rays, counts);
     hipLaunchKernelGGL(march_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, counts, n_rays, capacity, rays_a,
                        counter);
     if (wave)
-        hipLaunchKernelGGL(march_wave_kernel<true>, dim3(nbw), dim3(256), 0, stream, p, n_rays, nullptr, rays_a, xyzs,
+        hipLaunchKernelGGL(march_expand_kernel, dim3(nbw), dim3(256), 0, stream, p, n_rays, rays_a, tbuf, xyzs,
                            dirs, deltas, ts);
     else
         hipLaunchKernelGGL(march_write_kernel, dim3(nb), dim3(RAY_BLOCK), 0, stream, p, n_rays, rays_a, xyzs, dirs,

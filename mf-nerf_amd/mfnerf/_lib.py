@@ -53,7 +53,7 @@ SIGNATURES = {
     "mfnerf_morton3d": (_I, [_P, _I64, _P, _P]),
     "mfnerf_morton3d_invert": (_I, [_P, _I64, _P, _P]),
     "mfnerf_packbits": (_I, [_P, _I64, _F, _P, _P, _P]),
-    "mfnerf_raymarching_train_workspace": (_I64, [_I64]),
+    "mfnerf_raymarching_train_workspace": (_I64, [_I64, _I]),
     "mfnerf_raymarching_train": (_I, [_P, _P, _P, _I64, _P, _I, _F, _F, _P, _I, _I, _I64, _I64,
                                       _P, _P, _P, _P, _P, _P, _P, _P]),
     "mfnerf_raymarching_test": (_I, [_P, _P, _P, _I64, _P, _I64, _P, _I, _F, _F, _I, _I, _I,

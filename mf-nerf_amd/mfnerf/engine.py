@@ -269,8 +269,8 @@ class TrainStep:
             t.deltas = torch.empty(self.cap_p, **f32)
             t.ts = torch.empty(self.cap_p, **f32)
             t.counter = m.counters[q]
-            t.march_ws = torch.empty(max(16, load().mfnerf_raymarching_train_workspace(self.Np)), dtype=torch.uint8,
-                                     device=dev)
+            ws_bytes = load().mfnerf_raymarching_train_workspace(self.Np, c.max_samples)
+            t.march_ws = torch.empty(max(16, ws_bytes), dtype=torch.uint8, device=dev)
             m.part.append(t)
         return m
 

@@ -84,16 +84,16 @@ def raymarching_train(rays_o, rays_d, hits_t, density_bitfield, cascades, scale,
     deltas = torch.empty(cap, dtype=_f32, device=dev)
     ts = torch.empty(cap, dtype=_f32, device=dev)
     counter = torch.empty(2, dtype=_i32, device=dev)
-    ws = _workspace(_lib_ws(N), dev)
+    ws = _workspace(_lib_ws(N, int(max_samples)), dev)
     call("mfnerf_raymarching_train", ptr(rays_o), ptr(rays_d), ptr(hits_t), hits_t.stride(0), ptr(density_bitfield),
          int(cascades), float(scale), float(exp_step_factor), ptr(noise), int(grid_size), int(max_samples), N, cap,
          ptr(rays_a), ptr(xyzs), ptr(dirs), ptr(deltas), ptr(ts), ptr(counter), ptr(ws), stream())
     return [rays_a, xyzs, dirs, deltas, ts, counter]
 
 
-def _lib_ws(n):
+def _lib_ws(n, max_samples):
     from ._lib import load
-    return load().mfnerf_raymarching_train_workspace(n)
+    return load().mfnerf_raymarching_train_workspace(n, max_samples)
 
 
 def raymarching_test(rays_o, rays_d, hits_t, alive_indices, density_bitfield, cascades, scale, exp_step_factor,

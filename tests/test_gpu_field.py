@@ -18,6 +18,27 @@ pytestmark = pytest.mark.gpu
 
 LEGO_B = math.exp(math.log(2048 * 0.5 / 16) / 15)
 
+# The partitioned (binned) scatter carries each weighted contribution of the hashed levels as an
+# fp16 value (8-B records: the algorithmic fp16 scatter's own payload; tcnn's gradient is an fp16
+# SUM, rounded at every add): each contribution is rounded once to 11 significant bits, so an
+# entry's error is within 2^-11 of the sum of its contributions' magnitudes -- the oracle's
+# gradient of the same encoding taken with |dL/dy| (the interpolation weights are >= 0).
+REC_REL = 2.0 ** -11
+
+
+def _abs_grad(x, dy, olay):
+    """Per table entry: the sum over samples of |contribution| (fp64)."""
+    ta = torch.zeros(olay.n_params).requires_grad_(True)
+    (FO.grid_encode(x, ta, olay).double() * dy.abs().double()).sum().backward()
+    return ta.grad.double()
+
+
+def _assert_binned(got, gref, gabs, atol, rtol=0.0, what=None):
+    """|got - ref| <= 2^-11 x (sum of |contributions|) + the fixed-point path's own tolerance."""
+    got, gref = got.double(), gref.double()
+    excess = (got - gref).abs() - (REC_REL * 1.0001 * gabs + atol + rtol * gref.abs())
+    assert float(excess.max()) <= 0, (what, float(excess.max()), int(excess.argmax()))
+
 
 def test_mfma_f16_lane_maps(gpu):
     g = torch.Generator().manual_seed(0)
@@ -86,11 +107,12 @@ def test_grid_encode_fw_bw(gpu, name, args):
     # partitioned LDS scatter (the training path): same fixed point, bit-reproducible, workspace
     # copies left zero
     bn = []
+    gabs = _abs_grad(x, dy, olay)
     for _ in range(2):
         ws = FLD.grid_bw_binned_workspace(desc, N, gpu)
         gt = torch.zeros(lay.n_params, device=gpu)
         FLD.grid_encode_bw(xg, N, dyg, gt, lay, desc, workspace=ws, binned=True)
-        assert torch.allclose(gt.cpu(), gref, rtol=1e-4, atol=1e-4 * float(gref.abs().max()))
+        _assert_binned(gt.cpu(), gref, gabs, 1e-4 * float(gref.abs().max()), rtol=1e-4)
         nc = load().mfnerf_grid_encode_bw_workspace(desc) // 4
         assert int((ws[:nc] != 0).sum()) == 0
         bn.append(gt)
@@ -107,7 +129,7 @@ def test_grid_encode_fw_bw(gpu, name, args):
     gt = torch.zeros(lay.n_params, device=gpu)
     FLD.grid_encode_bw(xg, N, dyg, gt, lay, desc, n_dev=n_dev, workspace=FLD.grid_bw_binned_workspace(desc, N, gpu),
                        binned=True)
-    assert torch.allclose(gt.cpu(), tp.grad, rtol=1e-4, atol=1e-4 * float(tp.grad.abs().max()))
+    _assert_binned(gt.cpu(), tp.grad, _abs_grad(x[:m], dy[:m], olay), 1e-4 * float(tp.grad.abs().max()), rtol=1e-4)
 
 
 def test_grid_encode_bw_along_rays(gpu):
@@ -127,6 +149,7 @@ def test_grid_encode_bw_along_rays(gpu):
     (FO.grid_encode(x, table, olay) * dy).sum().backward()
     gref = table.grad
     desc = lay.desc()
+    gabs = _abs_grad(x, dy, olay)
     for fixed, binned in ((False, False), (True, False), (True, True)):
         gt = torch.zeros(lay.n_params, device=gpu)
         ws = FLD.grid_bw_binned_workspace(desc, N, gpu) if binned else FLD.grid_bw_workspace(desc, gpu)
@@ -134,14 +157,17 @@ def test_grid_encode_bw_along_rays(gpu):
         # the fixed-point quantum is 2^-30 of the level's L1 (~1e-3 of one contribution here); the
         # binned path's dense levels round every sample's contribution once (run sums are integer),
         # ~sqrt(contributions) quanta per entry: 2e-4 of the level's largest entry
-        tol = 2e-4 if binned else 1e-4
-        assert torch.allclose(gt.cpu(), gref, rtol=1e-4, atol=tol * float(gref.abs().max()))
+        if binned:
+            _assert_binned(gt.cpu(), gref, gabs, 2e-4 * float(gref.abs().max()), rtol=1e-4)
+        else:
+            assert torch.allclose(gt.cpu(), gref, rtol=1e-4, atol=1e-4 * float(gref.abs().max()))
     # the training regime: per-sample gradients ~1e-7 of very different size per level; the
     # fixed-point resolution (2^-30 of each level's L1) stays far below fp32's relative error
     dys = dy * torch.logspace(-9, -5, 32).view(1, 32)
     tp = torch.zeros(lay.n_params).requires_grad_(True)
     (FO.grid_encode(x, tp, olay).double() * dys.double()).sum().backward()
     gref = tp.grad.double()
+    gabs = _abs_grad(x, dys, olay)
     for binned in (False, True):
         gt = torch.zeros(lay.n_params, device=gpu)
         ws = FLD.grid_bw_binned_workspace(desc, N, gpu) if binned else FLD.grid_bw_workspace(desc, gpu)
@@ -151,8 +177,11 @@ def test_grid_encode_bw_along_rays(gpu):
             a, b = lay.offsets[l] * 2, lay.offsets[l + 1] * 2 if l + 1 < 16 else lay.n_params
             scale = float(gref[a:b].abs().max())
             if scale > 0:
-                err = float((got[a:b] - gref[a:b]).abs().max()) / scale
-                assert err < (2e-4 if binned else 1e-4), (binned, l, err)
+                if binned:
+                    _assert_binned(got[a:b], gref[a:b], gabs[a:b], 2e-4 * scale, what=l)
+                else:
+                    err = float((got[a:b] - gref[a:b]).abs().max()) / scale
+                    assert err < 1e-4, (l, err)
 
 
 @pytest.mark.parametrize("name,args", [_layouts()[0], _layouts()[2]])
@@ -177,6 +206,7 @@ def test_grid_encode_bw_ragged_rays(gpu, name, args):
     tp = torch.zeros(lay.n_params).requires_grad_(True)
     (FO.grid_encode(x, tp, olay).double() * dy.double()).sum().backward()
     gref = tp.grad.double()
+    gabs = _abs_grad(x, dy, olay)
     desc = lay.desc()
     outs = []
     for fixed, binned in ((True, False), (True, True), (True, True)):
@@ -188,8 +218,10 @@ def test_grid_encode_bw_ragged_rays(gpu, name, args):
         for a, b in zip(cuts[:-1], cuts[1:]):
             scale = float(gref[a:b].abs().max())
             if scale > 0:  # fixed point: quanta of 2^-30 of the table's L1 (see test_grid_encode_bw_along_rays)
-                assert float((got[a:b] - gref[a:b]).abs().max()) <= (2e-4 if binned else 1e-4) * scale, \
-                    (name, binned, a)
+                if binned:
+                    _assert_binned(got[a:b], gref[a:b], gabs[a:b], 2e-4 * scale, what=(name, a))
+                else:
+                    assert float((got[a:b] - gref[a:b]).abs().max()) <= 1e-4 * scale, (name, a)
         outs.append(gt)
     assert torch.equal(outs[1], outs[2])
 
@@ -208,13 +240,17 @@ def test_grid_encode_bw_fixed_point_extreme_range(gpu):
         tp = torch.zeros(lay.n_params).requires_grad_(True)
         (FO.grid_encode(x, tp, olay).double() * dy.double()).sum().backward()
         gref = tp.grad.double()
+        gabs = _abs_grad(x, dy, olay)
         for binned in (False, True):
             gt = torch.zeros(lay.n_params, device=gpu)
             ws = FLD.grid_bw_binned_workspace(desc, N, gpu) if binned else FLD.grid_bw_workspace(desc, gpu)
             FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=ws, fixed_point=True, binned=binned)
             got = gt.cpu().double()
             assert torch.isfinite(got).all()
-            assert float((got - gref).abs().max()) <= 1e-4 * float(gref.abs().max()), (mag, binned)
+            if binned:
+                _assert_binned(got, gref, gabs, 1e-4 * float(gref.abs().max()), what=mag)
+            else:
+                assert float((got - gref).abs().max()) <= 1e-4 * float(gref.abs().max()), mag
     gt = torch.ones(lay.n_params, device=gpu) * 0
     FLD.grid_encode_bw(x.to(gpu), N, torch.zeros(N, 32, device=gpu), gt, lay, desc, fixed_point=True)
     assert int((gt != 0).sum()) == 0
@@ -237,8 +273,7 @@ def test_grid_encode_bw_binned_slot_overflow_falls_back(gpu):
     gt = torch.zeros(lay.n_params, device=gpu)
     FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=FLD.grid_bw_binned_workspace(desc, N, gpu),
                        binned=True)
-    got = gt.cpu().double()
-    assert float((got - gref).abs().max()) <= 1e-4 * float(gref.abs().max())
+    _assert_binned(gt.cpu(), gref, _abs_grad(x, dy, olay), 1e-4 * float(gref.abs().max()))
 
 
 @pytest.mark.parametrize("div", [1, 2, 16])
@@ -261,8 +296,7 @@ def test_grid_encode_bw_binned_slots_sized_below_the_count(gpu, div):
     assert ws.numel() * 4 == max(16, load().mfnerf_grid_encode_bw_binned_workspace(desc, ns))
     gt = torch.zeros(lay.n_params, device=gpu)
     FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=ws, binned=True, n_slots=ns)
-    got = gt.cpu().double()
-    assert float((got - gref).abs().max()) <= 1e-4 * float(gref.abs().max())
+    _assert_binned(gt.cpu(), gref, _abs_grad(x, dy, olay), 1e-4 * float(gref.abs().max()))
 
 
 def test_grid_encode_world_coords_normalisation(gpu):
@@ -448,6 +482,7 @@ def test_grid_encode_bw_fixed_point_shared_tables(gpu):
     tp = torch.zeros(lay.n_params).requires_grad_(True)
     (FO.grid_encode(x, tp, olay).double() * dy.double()).sum().backward()
     gref = tp.grad.double()
+    gabs = _abs_grad(x, dy, olay)
     desc = lay.desc()
     for binned in (False, True):
         gt = torch.zeros(lay.n_params, device=gpu)
@@ -459,6 +494,8 @@ def test_grid_encode_bw_fixed_point_shared_tables(gpu):
         for off, size in regions:
             a, b = 2 * off, 2 * (off + size)
             scale = float(gref[a:b].abs().max())
-            if scale > 0:
+            if scale > 0 and binned:
+                _assert_binned(got[a:b], gref[a:b], gabs[a:b], 1e-4 * scale, what=off)
+            elif scale > 0:
                 err = float((got[a:b] - gref[a:b]).abs().max()) / scale
-                assert err < 1e-4, (binned, off, err)
+                assert err < 1e-4, (off, err)
