@@ -79,7 +79,10 @@ def all_gather_(full, rank):
         return full
     w = _world()
     k = full.numel() // w
-    _host_staged(lambda x: dist.all_gather_into_tensor(x, x[rank * k:(rank + 1) * k].clone()), full)
+    if dist.get_backend() == "nccl":  # in place: RCCL reads this rank's slice where it lies
+        dist.all_gather_into_tensor(full, full[rank * k:(rank + 1) * k])
+    else:
+        _host_staged(lambda x: dist.all_gather_into_tensor(x, x[rank * k:(rank + 1) * k].clone()), full)
     return full
 
 

@@ -761,10 +761,11 @@ class TrainStep:
             # GATE_TIMEOUT_US before starting
             raise RuntimeError(f"gated graphs signalled {signal_at.count} times")
         torch.cuda.synchronize()
-        # the next step's march runs beside this step's grid_bw scatter, whose 4096 workgroups would
-        # otherwise take every dispatch slot first (the march's small kernels then finish after the
-        # scatter, on the critical path): the side stream gets the higher queue priority
-        hi = os.environ.get("MFNERF_SIDE_HIGH_PRIORITY", "1") == "1"
+        # the side stream at normal queue priority: a high-priority one measured the same alone
+        # (0.601 vs 0.601 ms/step) but, once an RCCL communicator exists in the process, it ran every
+        # step at 1.10 ms (kernels on the main queue 2-7x slower; GPU_MAX_HW_QUEUES=8 also cured it:
+        # the extra streams share hardware queues) -- the data-parallel step would pay it on every rank
+        hi = os.environ.get("MFNERF_SIDE_HIGH_PRIORITY", "0") == "1"
         self._side = torch.cuda.Stream(device=self.dev, priority=torch.cuda.Stream.priority_range()[1] if hi else 0)
         self._part_streams = [None] + [torch.cuda.Stream(device=self.dev) for _ in range(P - 1)]
         self._ev_march = [torch.cuda.Event(), torch.cuda.Event()]
