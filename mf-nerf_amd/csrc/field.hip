@@ -38,16 +38,54 @@ constexpr int FIELD_BLOCK = 256;    // forward: 4 waves
 // per sample tile; W = 128: 836 vs 171 us), dWr2 by LDS atomics beside the register tiles (3.4 ms
 // per 983k samples), Wr2^T read from global memory, two sample tiles per loop trip (~560 registers:
 // 80-147 spilled, 177 vs 122 us inside the step).
+// The weight gradients' operands need the samples in the MFMA K dimension: the TRANSPOSE of the
+// chain's T operands (channel on the row, sample on the lane).  Each T chunk goes to a per-wave LDS
+// image of the tile, [sample][channel] in 64-B rows of eight 8-B chunks (4 channels), the chunk index
+// XOR-swizzled with (row >> 1) & 7 (2-way bank conflicts on the writes, none on the reads), and comes
+// back with ds_read_b64_tr_b16, which hands each 16-lane group a 4-sample x 16-channel block column by
+// column (cdna_hip_programming.md T10).  The S operand's k order is the one the accumulator-as-operand
+// packing has (element j of lane half h = sample 8(j>>2) + 4h + (j&3) of the k-step), so both operands
+// of every dW product agree.  Exact.  (Rounds 1-2 transposed on the matrix core instead: D = T x I,
+// 2 MFMAs + 8 packing instructions per tile, ~30 of the 98 MFMAs of a sample tile.)
+constexpr int TILE_HALFS = 32 * 32;
+constexpr size_t TILE_BYTES = TILE_HALFS * 2;
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int tix(int row, int chunk) { return row * 32 + 4 * (chunk ^ ((row >> 1) & 7)); }
+
+// this lane's 8 channels of a T chunk (sample = lane & 31) into the tile image; cbase = first channel / 4;
+// perm: element j is channel 4 cbase + 8(j>>2) + 4h + (j&3) (a packed accumulator), else 4 cbase + 8h + j
+__device__ __forceinline__ void t_put(_Float16* slot, int lane, const half8& v, int cbase, bool perm) {
+    const int r = lane & 31, h = lane >> 5;
+    const int c0 = cbase + (perm ? h : 2 * h), c1 = cbase + (perm ? 2 + h : 2 * h + 1);
+    H8 u;
+    u.h = v;
+    *reinterpret_cast<u32x2*>(slot + tix(r, c0)) = u32x2{u.w[0], u.w[1]};
+    *reinterpret_cast<u32x2*>(slot + tix(r, c1)) = u32x2{u.w[2], u.w[3]};
+}
+
+__device__ __forceinline__ u32x2 tr_read(const _Float16* p) {
+    typedef __attribute__((address_space(3))) short4v* lds_s4;
+    return __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(p)));
+}
+
+struct SOp;
+__device__ __forceinline__ SOp s_get(const _Float16* slot, int lane);
+
 template <int W, int NW>
 struct BwCfg {
     using G = Geo<W>;
     static_assert(NW == 4, "one wave per SIMD");
     static constexpr bool R2_SPLIT = (W == 128);          // dWr2 by field_bw_wr2_kernel
-    static constexpr int LDS_FRAGS = G::N + 4;            // + 4 identity fragments
-    static constexpr int ID_BASE = LDS_FRAGS - 4;
+    static constexpr int LDS_FRAGS = G::N;
     static constexpr size_t IMG_OFF = (size_t)LDS_FRAGS * FRAG_HALFS * 2;
-    static constexpr size_t LDS = IMG_OFF;
-    static_assert(LDS <= 160 * 1024, "the backward's LDS must fit one CU");
+    // per wave: SLOTS transpose images of one 32x32 f16 tile (t_put / s_get), after the fragments
+    static constexpr int SLOTS_FIT = (int)((160 * 1024 - IMG_OFF) / ((size_t)NW * TILE_BYTES));
+    static constexpr int SLOTS = SLOTS_FIT < 12 ? SLOTS_FIT : 12;
+    static constexpr size_t SLOT_OFF = IMG_OFF;
+    static constexpr size_t LDS = SLOT_OFF + (size_t)NW * SLOTS * TILE_BYTES;
+    static_assert(SLOTS >= 2 && LDS <= 160 * 1024, "the backward's LDS must fit one CU");
 };
 
 template <typename TP, int W>
@@ -315,10 +353,9 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_fw_kernel(const _Float16* _
 // Data gradients chain through accumulators exactly like the forward ("T" orientation: channel on
 // the MFMA row, sample on the lane).  Weight gradients dW = dY^T X reduce over SAMPLES, which must
 // therefore sit in the MFMA K dimension, i.e. inside each lane's registers -- the transpose of the
-// T operands.  That transpose runs on the matrix core: D = Top x I (A = a T operand, B = an
-// identity fragment) is the "S" orientation (sample on the row, channel on the lane), and an S
-// accumulator packed to f16 IS an operand with K = samples.  Exact (products with 1.0, one
-// non-zero term per output), no LDS round trip, no wave-level synchronisation.
+// T operands, the "S" orientation (channel on the lane, samples in the registers): each T chunk is
+// written to a per-wave LDS tile image and read back with the transposing ds_read_b64_tr_b16
+// (t_put / s_get above; exact, no wave-level synchronisation).
 //   dW[out][in] (32x32 tile) += S(dY)[out-tile] x S(X)[in-tile], K = the tile's 32 samples (2 MFMAs)
 // The dW tiles accumulate across all sample tiles a wave processes (persistent grid) in registers
 // or in the workgroup's LDS image (BwCfg), then one slab row per workgroup, summed in a fixed order
@@ -327,19 +364,9 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_fw_kernel(const _Float16* _
 template <int W, int NW>
 __device__ __forceinline__ void load_frags_bw(_Float16* lds, const _Float16* __restrict__ packed) {
     using G = Geo<W>;
-    using C = BwCfg<W, NW>;
     const uint4* src = reinterpret_cast<const uint4*>(packed);
     uint4* dst = reinterpret_cast<uint4*>(lds);
     for (int i = threadIdx.x; i < G::N * 64; i += blockDim.x) dst[i] = src[i];
-    // identity: lane (n = lane&31, h), element j = 1 iff off + k_of(j, h, perm) == n
-    for (int i = threadIdx.x; i < 4 * 64; i += blockDim.x) {
-        const int fi = i >> 6, ln = i & 63, nn = ln & 31, hh = ln >> 5;
-        const int perm = fi >> 1, off = 16 * (fi & 1);
-        half8 v;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (_Float16)((off + k_of(j, hh, perm) == nn) ? 1.0f : 0.0f);
-        *reinterpret_cast<half8*>(lds + ((C::ID_BASE + fi) * 64 + ln) * 8) = v;
-    }
     __syncthreads();
 }
 
@@ -352,25 +379,22 @@ __device__ __forceinline__ half8 bw_frag(const _Float16* lds, const _Float16* __
 // S operands (K = samples 0..15 / 16..31 of the tile) of one 32-channel tile given as two T chunks
 struct SOp { half8 k[2]; };
 
-__device__ __forceinline__ SOp to_s(const _Float16* lds, int lane, const half8& lo, int lo_id, const half8& hi,
-                                    int hi_id) {
-    const f32x16 z = {};
-    f32x16 a = mfma(lo, lds_frag(lds, lo_id, lane), z);
-    a = mfma(hi, lds_frag(lds, hi_id, lane), a);
+// the S operand of a tile image (t_put): lane 4q+p of 16-lane group g supplies row (sample)
+// 16s + 4h + q (+8) at channels 16(g&1) + 4p; lane i of the group gets channel 16(g&1) + i
+__device__ __forceinline__ SOp s_get(const _Float16* slot, int lane) {
+    const int h = lane >> 5, q = (lane >> 2) & 3, c = 4 * ((lane >> 4) & 1) + (lane & 3);
     SOp o;
-    o.k[0] = pack8<0, false>(a);
-    o.k[1] = pack8<8, false>(a);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int r0 = 16 * s + 4 * h + q;
+        const u32x2 a = tr_read(slot + tix(r0, c)), b = tr_read(slot + tix(r0 + 8, c));
+        H8 u;
+        u.w[0] = a[0]; u.w[1] = a[1]; u.w[2] = b[0]; u.w[3] = b[1];
+        o.k[s] = u.h;
+    }
     return o;
 }
-// a tile with only its low 16 channels present (the 16-wide layer outputs)
-__device__ __forceinline__ SOp to_s16(const _Float16* lds, int lane, const half8& lo, int lo_id) {
-    const f32x16 z = {};
-    const f32x16 a = mfma(lo, lds_frag(lds, lo_id, lane), z);
-    SOp o;
-    o.k[0] = pack8<0, false>(a);
-    o.k[1] = pack8<8, false>(a);
-    return o;
-}
+
 __device__ __forceinline__ void dw_acc(f32x16& acc, const SOp& dy, const SOp& x) {
     acc = mfma(dy.k[0], x.k[0], acc);
     acc = mfma(dy.k[1], x.k[1], acc);
@@ -409,6 +433,35 @@ __device__ __forceinline__ void dw_add32(float* img, const f32x16& a, int ot, in
 // one dW tile += dY x X into its register accumulator
 __device__ __forceinline__ void acc_tile(f32x16& reg, const SOp& dy, const SOp& x) { dw_acc_agpr(reg, dy, x); }
 
+// Transpose-slot plans of field_bw (slot ids < N_SLOTS; every slot is read before it is written
+// again in program order).  W = 64, 12 slots: the forward's operands are written right after the
+// forward, so their LDS traffic overlaps the backward chain.  W = 128, 6 slots (the fragments take
+// 106 KB): every operand is written just before its products.
+template <int W>
+struct TPlan;
+template <>
+struct TPlan<64> {
+    static constexpr bool EARLY = true;
+    static constexpr int N_SLOTS = 12, SHH = 4, X = 7, DO = 8, DH = 1;
+    static constexpr int r2(int t) { return t; }
+    static constexpr int r1(int t) { return 2 + t; }
+    static constexpr int y1(int t) { return 5 + t; }
+    static constexpr int dr2(int t) { return 9 + t; }
+    static constexpr int dr1(int t) { return t ? 0 : 11; }
+    static constexpr int dy1(int t) { return 2 + t; }
+};
+template <>
+struct TPlan<128> {
+    static constexpr bool EARLY = false;
+    static constexpr int N_SLOTS = 6, SHH = 5, X = 5, DO = 0, DH = 4;
+    static constexpr int r2(int t) { return 1 + t; }
+    static constexpr int r1(int) { return 0; }   // (dWr2: field_bw_wr2_kernel)
+    static constexpr int dr2(int) { return 0; }
+    static constexpr int y1(int t) { return 2 + t; }
+    static constexpr int dr1(int t) { return t; }
+    static constexpr int dy1(int t) { return t; }
+};
+
 template <int W, int NW, bool PLANAR>
 __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
     const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n,
@@ -418,7 +471,6 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
     using G = Geo<W>;
     using C = BwCfg<W, NW>;
     constexpr int MT = G::MT;
-    constexpr int ID_N0 = C::ID_BASE, ID_N16 = C::ID_BASE + 1, ID_P0 = C::ID_BASE + 2, ID_P16 = C::ID_BASE + 3;
     constexpr int oR1 = N_XYZ_PARAMS, oR2 = oR1 + W * 32, oR3 = oR2 + W * W;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     _Float16* lds_base = reinterpret_cast<_Float16*>(smem);
@@ -497,6 +549,7 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
     float l1a[4] = {0.f, 0.f, 0.f, 0.f}, l1b[4] = {0.f, 0.f, 0.f, 0.f};
     // one trip: the P tiles' forward + backward stage by stage (see forward_tiles); dW into the
     // accumulators (tile 0's contribution before tile 1's), dX^T (scaled by S) into dx[]
+    _Float16* tsl = nullptr;  // this wave's transpose slots (set per trip from the opaque base)
     auto trip_bw = [&](const _Float16* lds, const _Float16* pk, const BwIn* in, const bool* valid, f32x16* dx) {
         FwdTile<W> T[P];
         {
@@ -516,6 +569,33 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
             dO[2] = in[q].g2 * S * T[q].rgb[2] * (1.0f - T[q].rgb[2]);
             dOb[q] = pack8<0, false>(dO);
         }
+        // this wave's transpose images (TPlan: compile-time slots, each read before it is rewritten;
+        // one wave's LDS accesses complete in program order)
+        using TP = TPlan<W>;
+        static_assert(P == 1 && TP::N_SLOTS <= C::SLOTS, "one transpose set per trip");
+        auto slot = [&](int k) { return tsl + k * TILE_HALFS; };
+        auto put2 = [&](int k, const half8* v) {  // a 32-channel tile given as two perm chunks
+            t_put(slot(k), lane, v[0], 0, true);
+            t_put(slot(k), lane, v[1], 4, true);
+        };
+        auto put_fw = [&](bool early) {  // the forward's operands
+            if (early != TP::EARLY) return;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) put2(TP::r2(t), T[0].r2[t]);
+            if constexpr (!C::R2_SPLIT) {
+#pragma unroll
+                for (int t = 0; t < MT; ++t) put2(TP::r1(t), T[0].r1[t]);
+            }
+        };
+        put_fw(true);
+        if constexpr (TP::EARLY) {
+            t_put(slot(TP::SHH), lane, T[0].sh, 0, false);
+            t_put(slot(TP::SHH), lane, T[0].hb, 4, true);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) put2(TP::y1(t), T[0].y1[t]);
+            t_put(slot(TP::X), lane, T[0].x[0], 0, false);
+            t_put(slot(TP::X), lane, T[0].x[1], 4, false);
+        }
         //    dR2 = Wr3^T dO, masked by R2 > 0 (the data-gradient chain first, the dW products after)
         half8 dr2p[P][MT][2];
 #pragma unroll
@@ -530,13 +610,18 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
                 dr2p[q][mt][1] = relu_mask8(pack8<8, false>(a[q]), T[q].r2[mt][1]);
             }
         }
-        // dWr3 (16 x W, rows 0..2 non-zero) += dO^T R2
+        if constexpr (!C::R2_SPLIT) {
 #pragma unroll
-        for (int q = 0; q < P; ++q) {
-            const SOp d = to_s16(lds, lane, dOb[q], ID_P0);
+            for (int mt = 0; mt < MT; ++mt) put2(TP::dr2(mt), dr2p[0][mt]);
+        }
+        // dWr3 (16 x W, rows 0..2 non-zero) += dO^T R2 (channels 16..31 of the dO image are stale:
+        // they only reach rows 16..31 of the dWr3 tiles, which the epilogue drops)
+        t_put(slot(TP::DO), lane, dOb[0], 0, true);
+        put_fw(false);
+        {
+            const SOp d = s_get(slot(TP::DO), lane);
 #pragma unroll
-            for (int t = 0; t < MT; ++t)
-                acc_tile(dwr3[t], d, to_s(lds, lane, T[q].r2[t][0], ID_P0, T[q].r2[t][1], ID_P16));
+            for (int t = 0; t < MT; ++t) acc_tile(dwr3[t], d, s_get(slot(TP::r2(t)), lane));
         }
         //    dR1 = Wr2^T dR2, masked by R1 > 0
         half8 dr1p[P][MT][2];
@@ -559,19 +644,17 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
                 dr1p[q][mt][1] = relu_mask8(pack8<8, false>(a[q]), T[q].r1[mt][1]);
             }
         }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) put2(TP::dr1(mt), dr1p[0][mt]);
         if constexpr (!C::R2_SPLIT) {   // -- rgb layer 2: dWr2 (WxW) += dR2^T R1
+            SOp x[MT];
 #pragma unroll
-            for (int q = 0; q < P; ++q) {
-                SOp x[MT];
+            for (int i = 0; i < MT; ++i) x[i] = s_get(slot(TP::r1(i)), lane);
 #pragma unroll
-                for (int i = 0; i < MT; ++i) x[i] = to_s(lds, lane, T[q].r1[i][0], ID_P0, T[q].r1[i][1], ID_P16);
+            for (int o = 0; o < MT; ++o) {
+                const SOp d = s_get(slot(TP::dr2(o)), lane);
 #pragma unroll
-                for (int o = 0; o < MT; ++o) {
-                    const SOp d = to_s(lds, lane, dr2p[q][o][0], ID_P0, dr2p[q][o][1], ID_P16);
-#pragma unroll
-                    for (int i = 0; i < MT; ++i)
-                        acc_tile(dwr2[o][i], d, x[i]);
-                }
+                for (int i = 0; i < MT; ++i) acc_tile(dwr2[o][i], d, x[i]);
             }
         }
         //    d[SH;h] = Wr1^T dR1 (rows 16..31 = dh) + TruncExp backward into h[0]
@@ -596,13 +679,16 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
                 dhb[q] = pack8<8, false>(dsh[q]);
             }
         }
+        t_put(slot(TP::DH), lane, dhb[0], 0, true);
         // -- rgb layer 1: dWr1 (Wx32) += dR1^T [SH;h]   (SH natural order, h perm order)
+        if constexpr (!TP::EARLY) {
+            t_put(slot(TP::SHH), lane, T[0].sh, 0, false);
+            t_put(slot(TP::SHH), lane, T[0].hb, 4, true);
+        }
+        {
+            const SOp x = s_get(slot(TP::SHH), lane);
 #pragma unroll
-        for (int q = 0; q < P; ++q) {
-            const SOp x = to_s(lds, lane, T[q].sh, ID_N0, T[q].hb, ID_P16);
-#pragma unroll
-            for (int o = 0; o < MT; ++o)
-                acc_tile(dwr1[o], to_s(lds, lane, dr1p[q][o][0], ID_P0, dr1p[q][o][1], ID_P16), x);
+            for (int o = 0; o < MT; ++o) acc_tile(dwr1[o], s_get(slot(TP::dr1(o)), lane), x);
         }
         //    dY1 = W2^T dh, masked by Y1 > 0
         half8 dy1p[P][2][2];
@@ -618,6 +704,8 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
                 dy1p[q][1][0] = relu_mask8(pack8<0, false>(a1[q]), T[q].y1[1][0]);
                 dy1p[q][1][1] = relu_mask8(pack8<8, false>(a1[q]), T[q].y1[1][1]);
             }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) put2(TP::dy1(t), dy1p[0][t]);
         }
         //    dX = W1^T dY1
         {
@@ -633,21 +721,25 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
                     for (int k = 0; k < 2; ++k) dx[q] = mfma(f[t * 2 + k], dy1p[q][t][k], dx[q]);
             }
         }
-        // -- xyz layer 2: dW2 (16x64) += dh^T Y1
+        // -- xyz layer 2: dW2 (16x64) += dh^T Y1 (dh: channels 16..31 of its image stale, rows dropped)
+        if constexpr (!TP::EARLY) {
 #pragma unroll
-        for (int q = 0; q < P; ++q) {
-            const SOp d = to_s16(lds, lane, dhb[q], ID_P0);
+            for (int t = 0; t < 2; ++t) put2(TP::y1(t), T[0].y1[t]);
+        }
+        {
+            const SOp d = s_get(slot(TP::DH), lane);
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
-                acc_tile(dw2[t], d, to_s(lds, lane, T[q].y1[t][0], ID_P0, T[q].y1[t][1], ID_P16));
+            for (int t = 0; t < 2; ++t) acc_tile(dw2[t], d, s_get(slot(TP::y1(t)), lane));
         }
         // -- xyz layer 1: dW1 (64x32) += dY1^T X   (X natural order)
+        if constexpr (!TP::EARLY) {
+            t_put(slot(TP::X), lane, T[0].x[0], 0, false);
+            t_put(slot(TP::X), lane, T[0].x[1], 4, false);
+        }
+        {
+            const SOp x = s_get(slot(TP::X), lane);
 #pragma unroll
-        for (int q = 0; q < P; ++q) {
-            const SOp x = to_s(lds, lane, T[q].x[0], ID_N0, T[q].x[1], ID_N16);
-#pragma unroll
-            for (int o = 0; o < 2; ++o)
-                acc_tile(dw1[o], to_s(lds, lane, dy1p[q][o][0], ID_P0, dy1p[q][o][1], ID_P16), x);
+            for (int o = 0; o < 2; ++o) acc_tile(dw1[o], s_get(slot(TP::dy1(o)), lane), x);
         }
     };
     for (int64_t tile = tile0; tile < tiles; tile += P * stride) {
@@ -657,6 +749,7 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
         asm volatile("" : "+s"(opaque));
         const _Float16* lds = lds_base + opaque;
         const _Float16* pk = packed + opaque;  // B4 from global memory (W = 128): not hoisted either
+        tsl = lds_base + opaque + C::SLOT_OFF / 2 + wid * (C::SLOTS * TILE_HALFS);
         BwIn in[P];
 #pragma unroll
         for (int q = 0; q < P; ++q) { in[q] = nx[q]; zero_grads(in[q]); }
@@ -741,6 +834,10 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
 // Second backward pass at W = 128: dWr2 (W x W) = sum over samples of dR2^T R1, with all 16 tiles in
 // registers.  Recomputes the forward and dR2 = relu'(R2) * Wr3^T dO (what field_bw_kernel does before
 // it), and writes the dWr2 segment of the same slab rows.
+constexpr int WR2_SLOTS = 8;  // (W = 128: R1's 4 tiles + dR2's 4)
+template <int W>
+constexpr size_t WR2_LDS() { return (size_t)Geo<W>::B4 * FRAG_HALFS * 2 + 4 * WR2_SLOTS * TILE_BYTES; }
+
 template <int W>
 __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_wr2_kernel(
     const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n,
@@ -749,23 +846,14 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_wr2_kernel(
     using G = Geo<W>;
     constexpr int MT = G::MT;
     constexpr int NF = G::B4;  // forward fragments + Wr3^T (B5)
-    constexpr int ID_P0 = NF + 2, ID_P16 = NF + 3;
     constexpr int oR2 = N_XYZ_PARAMS + W * 32;
-    static_assert((size_t)W * W * 4 <= (size_t)(NF + 4) * FRAG_HALFS * 2, "dWr2 image must fit the fragment area");
+    static_assert((size_t)W * W * 4 <= WR2_LDS<W>(), "dWr2 image must fit the kernel's LDS");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     _Float16* lds_base = reinterpret_cast<_Float16*>(smem);
     {
         const uint4* src = reinterpret_cast<const uint4*>(packed);
         uint4* dst = reinterpret_cast<uint4*>(lds_base);
         for (int i = threadIdx.x; i < NF * 64; i += blockDim.x) dst[i] = src[i];
-        for (int i = threadIdx.x; i < 4 * 64; i += blockDim.x) {
-            const int fi = i >> 6, ln = i & 63, nn = ln & 31, hh = ln >> 5;
-            const int perm = fi >> 1, off = 16 * (fi & 1);
-            half8 v;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = (_Float16)((off + k_of(j, hh, perm) == nn) ? 1.0f : 0.0f);
-            *reinterpret_cast<half8*>(lds_base + ((NF + fi) * 64 + ln) * 8) = v;
-        }
         __syncthreads();
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -795,6 +883,8 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_wr2_kernel(
         int opaque = 0;
         asm volatile("" : "+s"(opaque));
         const _Float16* lds = lds_base + opaque;
+        // this wave's transpose slots: R1's MT tiles, then one per dR2 tile
+        _Float16* tsl = lds_base + opaque + NF * FRAG_HALFS + wid * (WR2_SLOTS * TILE_HALFS);
         const bool valid = tile * 32 + r < nn;
         const TileIn I = nI;
         const float g0 = ng0, g1 = ng1, g2 = ng2;
@@ -808,14 +898,26 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_wr2_kernel(
             dO[2] = g2 * S * T.rgb[2] * (1.0f - T.rgb[2]);
         }
         const half8 dOb = pack8<0, false>(dO);
-        SOp x[MT];
 #pragma unroll
-        for (int i = 0; i < MT; ++i) x[i] = to_s(lds, lane, T.r1[i][0], ID_P0, T.r1[i][1], ID_P16);
+        for (int i = 0; i < MT; ++i) {
+            t_put(tsl + i * TILE_HALFS, lane, T.r1[i][0], 0, true);
+            t_put(tsl + i * TILE_HALFS, lane, T.r1[i][1], 4, true);
+        }
+        half8 dr2[MT][2];
 #pragma unroll
         for (int o = 0; o < MT; ++o) {
             f32x16 a = mfma(lds_frag(lds, G::B5 + o, lane), dOb, z);
-            const SOp d = to_s(lds, lane, relu_mask8(pack8<0, false>(a), T.r2[o][0]), ID_P0,
-                               relu_mask8(pack8<8, false>(a), T.r2[o][1]), ID_P16);
+            dr2[o][0] = relu_mask8(pack8<0, false>(a), T.r2[o][0]);
+            dr2[o][1] = relu_mask8(pack8<8, false>(a), T.r2[o][1]);
+            t_put(tsl + (MT + o) * TILE_HALFS, lane, dr2[o][0], 0, true);
+            t_put(tsl + (MT + o) * TILE_HALFS, lane, dr2[o][1], 4, true);
+        }
+        SOp x[MT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) x[i] = s_get(tsl + i * TILE_HALFS, lane);
+#pragma unroll
+        for (int o = 0; o < MT; ++o) {
+            const SOp d = s_get(tsl + (MT + o) * TILE_HALFS, lane);
 #pragma unroll
             for (int i = 0; i < MT; ++i) dw_acc_agpr(acc[o][i], d, x[i]);
         }
@@ -927,7 +1029,11 @@ int launch_bw(const void* feat, int64_t ps, const float* dirs, int64_t n, const 
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
             const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_kernel<W, NW, true>),
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
-            return a0 != hipSuccess ? a0 : a1;
+            hipError_t a2 = hipSuccess;
+            if constexpr (C::R2_SPLIT)
+                a2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_wr2_kernel<W>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)WR2_LDS<W>());
+            return a0 != hipSuccess ? a0 : a1 != hipSuccess ? a1 : a2;
         }();
         if (attr != hipSuccess) {
             mfn_set_error("field_bw: cannot raise the LDS limit to %d bytes", (int)C::LDS);
@@ -943,8 +1049,8 @@ int launch_bw(const void* feat, int64_t ps, const float* dirs, int64_t n, const 
                            (const _Float16*)feat, ps, dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb,
                            grad_scale, scale_dev, dL_dfeat, (float*)workspace, nonfinite, level_l1);
     if constexpr (C::R2_SPLIT)
-        hipLaunchKernelGGL(field_bw_wr2_kernel<W>, dim3(BW_BLOCKS), dim3(FIELD_BLOCK),
-                           (size_t)(Geo<W>::B4 + 4) * FRAG_HALFS * 2, stream, (const _Float16*)feat, ps, dirs, n, n_dev,
+        hipLaunchKernelGGL(field_bw_wr2_kernel<W>, dim3(BW_BLOCKS), dim3(FIELD_BLOCK), WR2_LDS<W>(), stream,
+                           (const _Float16*)feat, ps, dirs, n, n_dev,
                            (const _Float16*)packed, dL_drgb, grad_scale, scale_dev, (float*)workspace);
     if (grad_xyz)  // else deferred: mfnerf_field_bw_reduce folds the slab later
         hipLaunchKernelGGL(slab_reduce_kernel<W>, dim3((Geo<W>::N_DW + 63) / 64), dim3(256), 0, stream,

@@ -41,6 +41,19 @@ def main():
     step._level_l1.zero_()
     call("mfnerf_grid_level_l1", ptr(t.dfeat), cap, ptr(m.counter), c.L, ptr(step._level_l1), s())
 
+    side = torch.cuda.Stream(device=dev)
+
+    def two_queues():
+        main = torch.cuda.current_stream()
+        ev0, ev1 = torch.cuda.Event(), torch.cuda.Event()
+        ev0.record(main)
+        side.wait_event(ev0)
+        with torch.cuda.stream(side):
+            stages["grid_bw_coarse"]()
+            ev1.record(side)
+        stages["grid_bw_binned"]()
+        main.wait_event(ev1)
+
     stages = {
         "grid_fw": lambda: call("mfnerf_grid_encode_fw", ptr(m.xyzs), cap, ptr(m.counter), step.x_min, step.x_range,
                                 step.desc, ptr(step.p16[step.off_table:]), ptr(rowmajor), s()),
@@ -72,6 +85,8 @@ def main():
         "grid_bw_binned": lambda: call("mfnerf_grid_encode_bw_binned", ptr(m.xyzs), cap, ptr(m.counter), step.x_min,
                                        step.x_range, step.desc, ptr(t.dfeat), ptr(step.grads[step.off_table:]),
                                        ptr(t.grid_ws), step._bin_slots(), ptr(step._level_l1), 2, s()),
+        # the coarse levels on a second stream beside the partitioned levels (concurrency probe)
+        "grid_bw_2q": lambda: two_queues(),
         "grid_finish": lambda: step._grid_finish(0),
         "check": lambda: call("mfnerf_check_finite", ptr(step.grads), step.grads.numel(), ptr(step.finite_status), s()),
         "adam": lambda: step._adam(step.grads, 0, step.n_alloc, False),
