@@ -1346,11 +1346,23 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     const float k2 = ldexpf(1.0f, kbits + 15);  // the records' values are 2^-15 x table units
     for (int u0 = hw; u0 < UNITS; u0 += QF * n_hw) {
         if (u0 != hw) prefetch(u0);
+        // records 32..63 of the slots holding more (~35 % of them at the Lego config), loaded only by
+        // the lanes that have one, all issued before the first batch's adds (round 2 loaded them one
+        // slot at a time inside the add loop: a dependent round trip per slot)
+        uint2 r2[QF];
 #pragma unroll
         for (int q = 0; q < QF; ++q) {
             const int u = u0 + q * n_hw;
+            r2[q] = hl + 32 < c[q] ? base[(int64_t)u * slot + hl + 32] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int q = 0; q < QF; ++q)
             if (hl < c[q]) accum_record(img, mask, r[q], k2);
-            for (int k = hl + 32; k < c[q]; k += 32) accum_record(img, mask, base[(int64_t)u * slot + k], k2);
+#pragma unroll
+        for (int q = 0; q < QF; ++q) {
+            const int u = u0 + q * n_hw;
+            if (hl + 32 < c[q]) accum_record(img, mask, r2[q], k2);
+            for (int k = hl + 64; k < c[q]; k += 32) accum_record(img, mask, base[(int64_t)u * slot + k], k2);
         }
     }
     __syncthreads();
