@@ -217,21 +217,21 @@ int mfnerf_grid_encode_bw_finish(const mfnerf_grid_desc* desc, float* grad_table
 
 /* The fixed-point scatter (level_l1 required) by table partitions instead of memory-side atomics:
  * the hashed / shared tables are cut into partitions of up to 2048 entries; every (point, level,
- * corner row) becomes a 12-B record, sorted by partition in LDS and stored into fixed per-(partition,
+ * corner row) becomes an 8-B record, sorted by partition in LDS and stored into fixed per-(partition,
  * work unit) slots, and one workgroup per partition sums its records exactly (int64 LDS atomics)
  * and stores the partition once, rounded to the same int32 fixed point as
- * mfnerf_grid_encode_bw_scatter (one rounding per entry).  A slot overflow (pathological inputs)
- * falls back to that call's atomics on the device.  parts: 1 = the dense coarse levels only (atomics
- * into the workspace's private copies, as mfnerf_grid_encode_bw_scatter), 2 = the partitioned levels
- * only, 3 = both -- 1 and 2 may run concurrently on two streams.  The workspace prefix is the private
- * copies, so mfnerf_grid_encode_bw_finish / mfnerf_adam_step_fixed convert the result unchanged;
- * grad_table must be zero on entry.  workspace: mfnerf_grid_encode_bw_binned_workspace(desc, n_slots)
- * bytes, its copies zero on the first call (left zero by the finish); n_slots (0 or > n: n) is the
- * live sample count the record slots are sized for -- a training step passes its expected count,
- * not its capacity (rays x 1024 samples): a live count well above n_slots overflows slots, whose
- * extra records are added into grad_table by integer atomics (same sums, slower).
- * Bit-reproducible.  Replaces tcnn's hash-grid backward scatter (networks.py:36-49 encoding, half2
- * atomics there). */
+ * mfnerf_grid_encode_bw_scatter (one rounding per entry).  parts: 1 = the dense coarse levels only
+ * (atomics into the workspace's private copies, as mfnerf_grid_encode_bw_scatter), 2 = the
+ * partitioned levels only, 3 = both.  The workspace prefix is the private copies, so
+ * mfnerf_grid_encode_bw_finish / mfnerf_adam_step_fixed convert the result unchanged; grad_table must
+ * be zero on entry before the partitioned tables (the levels added by atomics), and is overwritten
+ * from there on.  workspace: mfnerf_grid_encode_bw_binned_workspace(desc, n_slots) bytes, zero on the
+ * first call (the finish and the accumulate leave it zero); n_slots (0 or > n: n) is the live sample
+ * count the record slots are sized for -- a training step passes its expected count, not its
+ * capacity (rays x 1024 samples): a live count well above n_slots overflows slots, whose extra
+ * records are added by integer atomics into the workspace's overflow words and from there into the
+ * partition's sums (same sums, slower).  Bit-reproducible.  Replaces tcnn's hash-grid backward
+ * scatter (networks.py:36-49 encoding, half2 atomics there). */
 int64_t mfnerf_grid_encode_bw_binned_workspace(const mfnerf_grid_desc* desc, int64_t n_max);
 /* Adam arguments for the fused partitioned accumulate (mfnerf_grid_encode_bw_binned_adam). */
 typedef struct {
@@ -249,6 +249,17 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
                                  const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
                                  void* workspace, int64_t n_slots, const float* level_l1, int parts,
                                  mfnerf_stream_t stream);
+/* mfnerf_grid_encode_bw_binned (parts = 3) + mfnerf_grid_encode_bw_finish in float form for an
+ * exchange before the optimizer (the data-parallel step): the accumulate writes the partitioned
+ * tables' finished sums as floats (times 1 / the table's scale, as the finish would) and one finish
+ * pass covers only the values before them.  Same floats as the two-call form.  grad_table must be
+ * zero before the partitioned tables' first value (mfnerf_grid_binned_first_value); the rest is
+ * overwritten.  Replaces tcnn's hash-grid backward (networks.py:36-49) feeding DDP's all-reduce
+ * (train.py:284). */
+int mfnerf_grid_encode_bw_binned_float(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                                       const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
+                                       void* workspace, int64_t n_slots, const float* level_l1,
+                                       mfnerf_stream_t stream);
 /* mfnerf_grid_encode_bw_binned (parts = 3) with the partitioned tables' Adam step fused into the
  * accumulate (adam: see mfnerf_adam_step_fixed_partial). */
 int mfnerf_grid_encode_bw_binned_adam(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,

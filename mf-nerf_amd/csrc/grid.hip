@@ -1021,13 +1021,14 @@ __host__ __device__ __forceinline__ int64_t slot_size(int64_t nn, const BinPlan&
 }
 
 // A record past its slot's capacity (a sample distribution far from uniform over the partitions):
-// added straight into the table gradient by 64-bit packed integer atomics (f1 * 2^32 + f0 per entry,
-// each contribution rounded once to the table's int32 unit), and the accumulate then adds the
-// partition's gradient words to its image (bin_scatter raises ovf).  Exact integer sums: the order
-// of the two paths does not matter.
-__device__ __forceinline__ void overflow_add(const BinPlan& P, int* __restrict__ grad, int bin, uint2 r) {
+// added by 64-bit packed integer atomics (f1 * 2^32 + f0 per entry, each contribution rounded once
+// to the table's int32 unit) into the workspace's overflow words (one per partitioned entry, zero
+// between steps: the accumulate zeroes what it reads), and the accumulate adds the partition's words
+// to its image (bin_scatter raises ovf).  Exact integer sums: the order of the two paths does not
+// matter.  The words are not the gradient's own, so the gradient need not be zero before a scatter.
+__device__ __forceinline__ void overflow_add(const BinPlan& P, int* __restrict__ ovw, int bin, uint2 r) {
     const int t = bin_table(P, bin);
-    const int64_t base = (int64_t)P.t_offset[t] + ((int64_t)(bin - P.t_bin0[t]) << P.shift);
+    const int64_t base = (int64_t)(P.t_offset[t] - P.t_offset[0]) + ((int64_t)(bin - P.t_bin0[t]) << P.shift);
     const uint32_t w = r.x;
     const float a = rec_value(r.y, 0) * REC_UP, b = rec_value(r.y, 1) * REC_UP;
     const float fx = (float)(w >> 17) * (1.0f / 32768.0f);
@@ -1036,7 +1037,7 @@ __device__ __forceinline__ void overflow_add(const BinPlan& P, int* __restrict__
         const int q0 = (int)rintf(wt * a), q1 = (int)rintf(wt * b);
         const long long pq = (long long)((uint64_t)(uint32_t)q1 << 32) + (long long)q0;
         if (pq != 0)
-            __hip_atomic_fetch_add(reinterpret_cast<long long*>(grad) + base + e, pq, __ATOMIC_RELAXED,
+            __hip_atomic_fetch_add(reinterpret_cast<long long*>(ovw) + base + e, pq, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
     };
     if (w & (1u << 15)) {
@@ -1068,7 +1069,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                                                                  uint2* __restrict__ rec, int32_t* __restrict__ scnt,
                                                                  uint32_t* __restrict__ smax,
                                                                  int32_t* __restrict__ ovf, int64_t n_slots,
-                                                                 int* __restrict__ grad) {
+                                                                 int* __restrict__ ovw) {
     constexpr int SPT = PAIR ? 2 : 1;  // samples per thread per tile
     __shared__ int cursor[MAX_BINS];
     __shared__ int hist[MAX_TBINS], toff[MAX_TBINS], gdst[2][MAX_TBINS];
@@ -1106,7 +1107,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                 __builtin_nontemporal_store((unsigned long long)r.x | ((unsigned long long)r.y << 32),
                                             reinterpret_cast<unsigned long long*>(dst));
             } else {
-                overflow_add(P, grad, prev_b0 + lb, r);  // a full slot: straight into the table
+                overflow_add(P, ovw, prev_b0 + lb, r);  // a full slot: into the overflow words
             }
         }
     };
@@ -1268,10 +1269,12 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
                                                                 const int32_t* __restrict__ scnt,
                                                                 const uint32_t* __restrict__ smax,
                                                                 const int32_t* __restrict__ ovf,
+                                                                int* __restrict__ ovw,
                                                                 int* __restrict__ grad, int64_t n_slots,
                                                                 const mfnerf_grid_desc D,
                                                                 const float* __restrict__ level_l1,
-                                                                const mfnerf_adam_fused A, const AdamRest X) {
+                                                                const mfnerf_adam_fused A, const AdamRest X,
+                                                                int float_out) {
     const int rest_b = X.first ? (int)blockIdx.x : (int)blockIdx.x - P.n_bins;
     if (rest_b >= 0 && rest_b < X.n_blocks) {
         // independent of the slot-overflow flag: these values never go through the partitions
@@ -1370,6 +1373,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     const int64_t e_lo = (int64_t)(bin - P.t_bin0[t]) << P.shift;
     const int n_e = (int)min<int64_t>(n_ent, (int64_t)P.t_size[t] - e_lo);
     int* dst = grad + 2 * ((int64_t)P.t_offset[t] + e_lo);
+    int2* ow = reinterpret_cast<int2*>(ovw) + ((int64_t)(P.t_offset[t] - P.t_offset[0]) + e_lo);  // overflow words
     const int rnd = kbits > 0 ? 1 << (kbits - 1) : 0;
     if (A.params) {
         // fused optimizer (mfnerf_adam_step_fixed_partial): the entry's finished int32 sums, converted
@@ -1380,12 +1384,12 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         if (add_words) {  // the overflowed records' sums join the image; the words are zeroed
             __syncthreads();
             for (int i = threadIdx.x; i < n_e; i += blockDim.x) {
-                const int2 g = reinterpret_cast<const int2*>(dst)[i];  // overflow_add's packed word
+                const int2 g = ow[i];  // overflow_add's packed word
                 const unsigned long long w = img[i];
                 const int lo = (int)(uint32_t)w, hi = (int)(uint32_t)(w >> 32) + (lo < 0);
                 const int o0 = ((lo + rnd) >> kbits) + g.x, o1 = ((hi + rnd) >> kbits) + g.y + (g.x < 0);
                 img[i] = ((unsigned long long)(uint32_t)o1 << 32) + (unsigned long long)(long long)o0;
-                reinterpret_cast<int2*>(dst)[i] = make_int2(0, 0);
+                ow[i] = make_int2(0, 0);
             }
             __syncthreads();
         }
@@ -1414,17 +1418,23 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         }
         return;
     }
+    // float_out: the finished sums as float gradients (the int32 value times 1 / the table's scale,
+    // exactly what fold_convert_kernel computes), else the int32 sums for the finish pass
+    const float sc = float_out ? table_fixed_scale(D, level_l1, P.t_level[t]) : 0.0f;
+    const float is = sc > 0.0f ? 1.0f / sc : 0.0f;
     for (int i = threadIdx.x; i < n_e; i += blockDim.x) {
         const unsigned long long v = img[i];
         const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32) + (lo < 0);
         // back to the table's unit, rounded once (|fields| <= 2^30: no overflow adding rnd)
         int2 o = make_int2((lo + rnd) >> kbits, (hi + rnd) >> kbits);
         if (add_words) {
-            const int2 g = reinterpret_cast<const int2*>(dst)[i];  // overflow_add's packed f1 * 2^32 + f0
+            const int2 g = ow[i];  // overflow_add's packed f1 * 2^32 + f0
             o.x += g.x;
             o.y += g.y + (g.x < 0);
+            ow[i] = make_int2(0, 0);
         }
-        reinterpret_cast<int2*>(dst)[i] = o;
+        if (float_out) reinterpret_cast<float2*>(dst)[i] = make_float2((float)o.x * is, (float)o.y * is);
+        else reinterpret_cast<int2*>(dst)[i] = o;
     }
 }
 
@@ -1507,18 +1517,24 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
 struct BinWorkspace {
     float* priv;
     int32_t *scnt, *ovf;
+    int* ovw;  // overflow words: one packed int64 per partitioned entry (zero between steps)
     uint32_t* smax;
     uint2* rec;
 };
 
 int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
 
-// workspace = [private copies of the dense levels | slot counts | overflow flag | record slots]
+// workspace = [private copies of the dense levels | overflow words | slot counts | overflow flag |
+// record slots]
 int64_t binned_workspace_layout(const mfnerf_grid_desc* d, int64_t n_max, char* base, BinWorkspace* W) {
     BinPlan P;
     if (bin_plan(d, &P) < 0) return -1;
     int64_t off = align256((int64_t)GRAD_COPIES * dense_entries_of(d) * 2 * (int64_t)sizeof(float));
     if (W) W->priv = reinterpret_cast<float*>(base);
+    int64_t part_entries = 0;
+    for (int t = 0; t < P.n_tables; ++t) part_entries += P.t_size[t];
+    if (W) W->ovw = reinterpret_cast<int*>(base + off);
+    off += align256(part_entries * 8);
     const int64_t nb = P.n_bins > 0 ? P.n_bins : 1;
     if (W) W->scnt = reinterpret_cast<int32_t*>(base + off);
     off += align256(nb * UNITS * 4);
@@ -1748,6 +1764,29 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
                        nullptr, stream);
 }
 
+int mfnerf_grid_encode_bw_binned_float(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                                       const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
+                                       void* workspace, int64_t n_slots, const float* level_l1,
+                                       mfnerf_stream_t stream) {
+    BinPlan P;
+    if (check_desc(desc, "grid_encode_bw_binned_float") || bin_plan(desc, &P) <= 0) {
+        mfn_set_error("grid_encode_bw_binned_float: bad desc or nothing partitioned");
+        return MFN_ERR_INVALID;
+    }
+    int st = binned_impl(x, n, n_dev, x_min, x_range, desc, dL_dout, grad_table, workspace, n_slots, level_l1, 7,
+                         nullptr, stream);
+    if (st || n == 0) return st;
+    // the values before the partitioned tables: the dense levels' copies folded, any other level's
+    // int32 sums converted (the accumulate wrote the partitioned tables' floats)
+    const int64_t head = 2 * (int64_t)P.t_offset[0];
+    if (head > 0) {
+        const int64_t fb = div_up<int64_t>(head / 4, 256);
+        hipLaunchKernelGGL(fold_convert_kernel, dim3((unsigned)(fb < 4096 ? fb : 4096)), dim3(256), 0, stream,
+                           grad_table, (int*)workspace, 2 * dense_entries_of(desc), head, *desc, level_l1);
+    }
+    return mfn_check_launch("grid_encode_bw_binned_float");
+}
+
 int mfnerf_grid_encode_bw_binned_adam(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                                       const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
                                       void* workspace, int64_t n_slots, const float* level_l1,
@@ -1841,7 +1880,10 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
     int st = check_desc(desc, "grid_encode_bw_binned");
     if (st) return st;
     if (n_slots <= 0 || n_slots > n) n_slots = n;
-    if (n < 0 || parts < 1 || parts > 3) { mfn_set_error("grid_encode_bw_binned: bad size or parts"); return MFN_ERR_INVALID; }
+    if (n < 0 || parts < 1 || parts > 7 || (parts & 4 && adam)) {
+        mfn_set_error("grid_encode_bw_binned: bad size or parts");
+        return MFN_ERR_INVALID;
+    }
     if (n == 0) return MFN_OK;
     if (!x || !dL_dout || !grad_table || !workspace || !level_l1) {
         mfn_set_error("grid_encode_bw_binned: null pointer (workspace and level_l1 are required)");
@@ -1894,13 +1936,14 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
                                : P.n_binned <= 12 ? bin_scatter_kernel<12, false>
                                                   : bin_scatter_kernel<MAX_BINNED, false>);
         hipLaunchKernelGGL(sk, dim3(UNITS), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
-                           *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.smax, W.ovf, n_slots, (int*)grad_table);
+                           *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.smax, W.ovf, n_slots, W.ovw);
         mfnerf_adam_fused A{};
         if (adam) A = *adam;
         AdamRest X{};
         if (rest) X = *rest;
         hipLaunchKernelGGL(bin_accum_kernel, dim3(P.n_bins + X.n_blocks), dim3(ACC_THREADS), 0, stream, P, n, n_dev,
-                           W.rec, W.scnt, W.smax, W.ovf, (int*)grad_table, n_slots, *desc, level_l1, A, X);
+                           W.rec, W.scnt, W.smax, W.ovf, W.ovw, (int*)grad_table, n_slots, *desc, level_l1, A, X,
+                           (parts & 4) ? 1 : 0);
     }
     return mfn_check_launch("grid_encode_bw_binned");
 }

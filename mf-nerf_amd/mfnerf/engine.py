@@ -388,7 +388,9 @@ class TrainStep:
         Np, cap = self.Np, self.cap_p
         if q == 0:
             if self.shard is not None:
-                self.grads.zero_()  # unsharded: the previous Adam pass left it zero
+                # unsharded: the previous Adam pass left it zero; sharded, the binned scatter
+                # overwrites the partitioned tables, so only the values before them are zeroed
+                self.grads[:self._grad_zero_end()].zero_()
             if c.lambda_distortion > 0:
                 self._loss_acc.zero_()
         else:
@@ -509,6 +511,28 @@ class TrainStep:
             self._grid_bw(self.mbuf[j], 0, fuse_adam=True)
             self._finish_update(partial=True)
 
+    def _grad_zero_end(self):
+        """Gradient values a step must find zero: all of them, or with the binned scatter only those
+        before the partitioned tables (the accumulate stores the rest; overflowed records go through
+        the workspace's own words)."""
+        if self._binned():
+            return self.off_table + load().mfnerf_grid_binned_first_value(self.desc)
+        return self.n_alloc
+
+    def _grid_bw_float(self, mb):
+        """Data parallel, one part: the table gradient scattered and finished to floats for the
+        exchange (binned: the accumulate writes the partitioned tables' floats and one finish pass
+        covers the rest, mfnerf_grid_encode_bw_binned_float), level_l1 zeroed after use."""
+        if not self._binned():
+            self._grid_bw(mb, 0)
+            self._grid_finish(0)
+            return
+        t, m = self.parts[0], mb.part[0]
+        call("mfnerf_grid_encode_bw_binned_float", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min,
+             self.x_range, self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws),
+             self._bin_slots(), ptr(self._level_l1), stream())
+        self._level_l1.zero_()
+
     def _grid_finish(self, q):
         """Fold part q's private copies of the coarse levels / convert the fixed-point sums."""
         call("mfnerf_grid_encode_bw_finish", self.desc, ptr(self.grads[self.off_table:]), ptr(self.parts[q].grid_ws),
@@ -625,8 +649,14 @@ class TrainStep:
         self.last_batch = batch
         self._primed = False  # a pipelined replay() must march its own batch next
         self._march(batch, mb, mark, prepped=prepped, noise=noise)
+        dp = self.shard is not None or exchange is not None
         for q in range(self.n_parts):
             self._chain(batch, mb, q, mark)
+            if dp and self.n_parts == 1:  # the data-parallel step's form (as the captured dp_pre)
+                self._grid_bw_float(mb)
+                mark("grid_bw")
+                mark("grid_finish")
+                continue
             self._grid_bw(mb, q)
             mark("grid_bw")
             self._grid_finish(q)
@@ -719,8 +749,7 @@ class TrainStep:
             def dp_pre(j, mark):
                 self._pack()  # the previous step's all-gathered / updated fp16 weights
                 self._chain(self._static[j], self.mbuf[j], 0, mark)
-                self._grid_bw(self.mbuf[j], 0)
-                self._grid_finish(0)
+                self._grid_bw_float(self.mbuf[j])
                 if amp:  # the non-finite flag rides the collective: NaN into every shard's first value
                     call("mfnerf_flag_to_shards", ptr(self.grads), n_sh, w, ptr(self.finite_status), stream())
 

@@ -10,7 +10,7 @@ import torch
 
 from conftest import ROOT
 from mfnerf import field as FLD
-from mfnerf._lib import call, load, ptr
+from mfnerf._lib import call, load, ptr, stream
 from mfnerf.grid import GridLayout
 from oracle import field_oracle as FO
 
@@ -297,6 +297,38 @@ def test_grid_encode_bw_binned_slots_sized_below_the_count(gpu, div):
     gt = torch.zeros(lay.n_params, device=gpu)
     FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=ws, binned=True, n_slots=ns)
     _assert_binned(gt.cpu(), gref, _abs_grad(x, dy, olay), 1e-4 * float(gref.abs().max()))
+
+
+@pytest.mark.parametrize("div", [1, 16])
+def test_grid_encode_bw_binned_float_matches_scatter_and_finish(gpu, div):
+    """mfnerf_grid_encode_bw_binned_float (the data-parallel step's form: the accumulate writes the
+    partitioned tables' floats, one finish pass covers the values before them) gives the same floats,
+    bit for bit, as mfnerf_grid_encode_bw_binned + mfnerf_grid_encode_bw_finish -- with the slots
+    sized for the count (div 1) and far below it (div 16: records overflow into the workspace's
+    words), and with stale values in the partitioned region of the output, which it overwrites."""
+    lay = GridLayout(16, 2, 19, 16, LEGO_B)
+    g = torch.Generator().manual_seed(23)
+    N = 20000
+    x = torch.rand(N, 3, generator=g).to(gpu)
+    dy = (torch.randn(N, 32, generator=g) * 1e-3).to(gpu)
+    desc = lay.desc()
+    ns = N // div
+    first = load().mfnerf_grid_binned_first_value(desc)
+    assert 0 < first < lay.n_params
+    ref = torch.zeros(lay.n_params, device=gpu)
+    FLD.grid_encode_bw(x, N, dy, ref, lay, desc, workspace=FLD.grid_bw_binned_workspace(desc, ns, gpu), binned=True,
+                       n_slots=ns)
+    ws = FLD.grid_bw_binned_workspace(desc, ns, gpu)
+    out = torch.zeros(lay.n_params, device=gpu)
+    for rep in range(2):  # the second call finds the first one's floats in the partitioned region
+        if rep:
+            out[:first].zero_()
+        l1 = torch.zeros(lay.L, device=gpu)
+        call("mfnerf_grid_level_l1", ptr(dy), N, None, lay.L, ptr(l1), stream())
+        call("mfnerf_grid_encode_bw_binned_float", ptr(x), N, None, 0.0, 1.0, desc, ptr(dy), ptr(out), ptr(ws), ns,
+             ptr(l1), stream())
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), f"call {rep}: {int((out != ref).sum())} values differ"
 
 
 def test_grid_encode_world_coords_normalisation(gpu):
