@@ -873,6 +873,7 @@ __device__ __forceinline__ int bin_table(const BinPlan& P, int b) {
 // MixedFeature tables, straddles) each entry gets a single record with weight sel ? fx : 1-fx.
 // a record's two values: fp16 of v * 2^-15, round to nearest even (v in the table's int32 units)
 constexpr float REC_DOWN = 1.0f / 32768.0f, REC_UP = 32768.0f;
+typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t rec_values(float a, float b) {
     const _Float16 ha = (_Float16)(a * REC_DOWN), hb = (_Float16)(b * REC_DOWN);  // (exact scaling)
     return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
@@ -908,6 +909,35 @@ __device__ __forceinline__ void level_records_geo(const mfnerf_grid_desc& D, con
         const bool pair = pair_hash && b0 == b1;
         emit(2 * yz, b0, make_uint2((i0 & mask) | (pair ? (ones << 11) : (1u << 15)) | fxq, ab));
         emit(2 * yz + 1, pair ? -1 : b1, make_uint2((i1 & mask) | (1u << 15) | (1u << 16) | fxq, ab));
+    }
+}
+
+// The PAIR layout's records (BinPlan::pair_ok: every binned level an own power-of-two hash table and
+// every x + 1 below 2^shift, so the x-pair never straddles a partition): one record per (y,z) row,
+// the hash written out (corner_index's prime hash masked to the table size, no layout branches), the
+// partition from the index's high bits, and s0 / s1 already scaled by the table unit x 2^-15 (exact:
+// a power of two), so rec_values' own scaling is gone.  Same records, bit for bit, as
+// level_records_geo.  EMIT(row, partition in the table, record).
+template <typename EMIT>
+__device__ __forceinline__ void pair_level_records(const mfnerf_grid_desc& D, const BinPlan& P, int l, float x,
+                                                   float y, float z, float s0, float s1, EMIT&& emit) {
+    const LevelGeo Lg = level_geo(D.scale[l], x, y, z);
+    const uint32_t mask = D.size[l] - 1u, emask = (1u << P.shift) - 1u;
+    const uint32_t fxq = min(32767u, (uint32_t)rintf(Lg.w[0] * 32768.0f)) << 17;
+    // trailing ones of x (< shift for every x + 1 < 2^shift, which pair_ok guarantees inside the grid;
+    // the clamp keeps a point outside it from naming an x-pair beyond its partition), and fx
+    const uint32_t ones = min((uint32_t)__builtin_ctz(~Lg.g[0]), (uint32_t)P.shift - 1u);
+    const uint32_t flags = (ones << 11) | fxq;
+    const uint32_t hy0 = Lg.g[1] * PRIME1, hz0 = Lg.g[2] * PRIME2;
+    const float wy1 = Lg.w[1], wy0 = 1.0f - wy1, wz1 = Lg.w[2], wz0 = 1.0f - wz1;
+#pragma unroll
+    for (int yz = 0; yz < 4; ++yz) {
+        const uint32_t hy = (yz & 1) ? hy0 + PRIME1 : hy0, hz = (yz >> 1) ? hz0 + PRIME2 : hz0;
+        const uint32_t i0 = (Lg.g[0] ^ hy ^ hz) & mask;
+        const float wyz = ((yz & 1) ? wy1 : wy0) * ((yz >> 1) ? wz1 : wz0);
+        const _Float16 ha = (_Float16)(wyz * s0), hb = (_Float16)(wyz * s1);
+        const uint32_t ab = (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
+        emit(yz, (int)(i0 >> P.shift), make_uint2((i0 & emask) | flags, ab));
     }
 }
 
@@ -1072,12 +1102,15 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                                                                  int* __restrict__ ovw) {
     constexpr int SPT = PAIR ? 2 : 1;  // samples per thread per tile
     __shared__ int cursor[MAX_BINS];
-    __shared__ int hist[MAX_TBINS], toff[MAX_TBINS], gdst[2][MAX_TBINS];
+    __shared__ int hist[MAX_TBINS], toff[MAX_TBINS];
+    // per bin of the staged level: {index of the stage's first record of the bin in rec[] minus its
+    // stage offset, the stage index its slot ends at} (one 8-B LDS read per stored record)
+    __shared__ int2 gdst[2][MAX_TBINS];
     __shared__ uint2 stage[SC_STAGE];
     __shared__ uint16_t sbin[SC_STAGE];
     __shared__ float fs_s[MFN_MAX_LEVELS];
     __shared__ int s_total[2];
-    uint32_t rmax = 0u;  // largest |a|, |b| of this thread's records (fp16 bits order as uints)
+    uint32_t rmax2 = 0u;  // largest |a| (low half), |b| (high half) of this thread's records, fp16 bits
     load_fixed_scales(D, level_l1, fs_s);
     for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x) cursor[b] = 0;
     for (int b = threadIdx.x; b < MAX_TBINS; b += blockDim.x) hist[b] = 0;
@@ -1096,13 +1129,13 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
     auto store_prev = [&]() {
         if (prev_b0 < 0) return;
         const int total = s_total[par ^ 1];
-        const int* gd = gdst[par ^ 1];
+        const int2* gd = gdst[par ^ 1];
         for (int k = threadIdx.x; k < total; k += SC_THREADS) {
             const int lb = sbin[k];
-            const int pos = gd[lb] + k;  // position in the unit's slot of the bin
+            const int2 g = gd[lb];
             const uint2 r = stage[k];
-            if (pos < slot) {
-                uint2* dst = rec + ((int64_t)(prev_b0 + lb) * UNITS + u) * slot + pos;
+            if (k < g.y) {  // inside the unit's slot of the bin
+                uint2* dst = rec + (uint32_t)(g.x + k);
                 // nontemporal: streamed once here, read once by the accumulate
                 __builtin_nontemporal_store((unsigned long long)r.x | ((unsigned long long)r.y << 32),
                                             reinterpret_cast<unsigned long long*>(dst));
@@ -1131,17 +1164,25 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
 #pragma unroll
             for (int q = 0; q < SPT; ++q) {
                 const SampleLevel Q = sample_level(D, P, S[q], j);
-                if (live[q] && Q.live)
+                if (!(live[q] && Q.live)) continue;
+                // the record's |a|, |b| maxima as two packed u16 (fp16 bits order like the values)
+                auto rank = [&](int k, int lb, uint2 r) {
+                    R[k].r = r;
+                    R[k].meta = (uint32_t)lb | ((uint32_t)atomicAdd(&hist[lb], 1) << 16);
+                    rmax2 = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(
+                        __builtin_bit_cast(ushort2v, rmax2), __builtin_bit_cast(ushort2v, r.y & 0x7fff7fffu)));
+                };
+                if constexpr (PAIR) {
+                    const int l = P.level[j];
+                    const float fs = fs_s[l] * REC_DOWN;
+                    pair_level_records(D, P, l, S[q].x, S[q].y, S[q].z, Q.g0 * fs, Q.g1 * fs,
+                                       [&](int yz, int lb, uint2 r) { rank(4 * q + yz, lb, r); });
+                } else {
                     level_records(D, P, j, S[q].x, S[q].y, S[q].z, Q.g0, Q.g1, fs_s[P.level[j]],
                                   [&](int sl, int bin, uint2 r) {
-                                      // PAIR: slot 2 yz + 1 never holds a record (pairs never straddle)
-                                      const int k = PAIR ? 4 * q + (sl >> 1) : sl;
-                                      if (bin < 0 || (PAIR && (sl & 1))) return;
-                                      const int lb = bin - b0;
-                                      R[k].r = r;
-                                      R[k].meta = (uint32_t)lb | ((uint32_t)atomicAdd(&hist[lb], 1) << 16);
-                                      rmax = max(rmax, max(r.y & 0x7fffu, (r.y >> 16) & 0x7fffu));
+                                      if (bin >= 0) rank(sl, bin - b0, r);
                                   });
+                }
             }
             store_prev();  // the previous level's sorted stage, beside this level's counting
             __syncthreads();
@@ -1168,7 +1209,9 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                         const int c = hist[lb];
                         toff[lb] = run;
                         const int cu = cursor[b0 + lb];
-                        gdst[par][lb] = cu - run;
+                        // record k of the sorted stage is position cu - run + k of the slot
+                        gdst[par][lb] = make_int2((int)((uint32_t)(b0 + lb) * UNITS + u) * (int)slot + cu - run,
+                                                  run + (int)slot - cu);
                         cursor[b0 + lb] = cu + c;
                         hist[lb] = 0;
                         run += c;
@@ -1196,6 +1239,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
     // sum over units of count x this max)
     {
         __shared__ uint32_t wmax[SC_THREADS / 64];
+        uint32_t rmax = max(rmax2 & 0xffffu, rmax2 >> 16);
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, off, 64));
         if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = rmax;
@@ -1543,7 +1587,9 @@ int64_t binned_workspace_layout(const mfnerf_grid_desc* d, int64_t n_max, char* 
     if (W) W->ovf = reinterpret_cast<int32_t*>(base + off);
     off += 256;
     if (W) W->rec = reinterpret_cast<uint2*>(base + off);
-    // every slot at the largest live count (the same function the kernels size them with)
+    // every slot at the largest live count (the same function the kernels size them with); the
+    // scatter addresses records with 32-bit indices
+    if (nb * UNITS * slot_size(n_max, P) >= (int64_t)1 << 31) return -1;
     off += align256(nb * UNITS * slot_size(n_max, P) * (int64_t)sizeof(uint2));
     return off;
 }
