@@ -406,10 +406,12 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_dense_kernel(const float* _
                                                                   int32_t* __restrict__ zero_flag) {
     if (zero_flag && blockIdx.x == 0 && threadIdx.x == 0) *zero_flag = 0;
     __shared__ float fs_s[MFN_MAX_LEVELS];
-    // per wave, one entry per run (+1 for a flushed carry): the 4 rows' (x0, x1) keys, and (tail
-    // prefix, head exclusive prefix) of the 16 values as 4 int4 (row r: x0f0, x0f1, x1f0, x1f1)
-    __shared__ int2 lkey[ENC_BLOCK / 64][65][4];
-    __shared__ int4 ltail[ENC_BLOCK / 64][65][4], lhead[ENC_BLOCK / 64][65][4];
+    // per wave, one entry per run: the 4 rows' (x0, x1) keys and the inclusive prefix at the run's
+    // tail of the 16 values as 4 int4 (row r: x0f0, x0f1, x1f0, x1f1).  The runs tile the chunk's
+    // valid lanes in order, so run r's exclusive prefix at its head is run r-1's tail prefix (0 for
+    // r = 0): no head list (round 3: 45 -> 28 KB of LDS per block, 3 -> 4 blocks per CU)
+    __shared__ int2 lkey[ENC_BLOCK / 64][64][4];
+    __shared__ int4 ltail[ENC_BLOCK / 64][64][4];
     // per wave and level: the run left open at the previous chunk's end (sums, keys, on/off)
     __shared__ int4 csum[ENC_BLOCK / 64][2 * NG][4];
     __shared__ int2 ckey[ENC_BLOCK / 64][2 * NG][4];
@@ -517,18 +519,12 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_dense_kernel(const float* _
                 MFN_PSTEP(0x111, 0xF) MFN_PSTEP(0x112, 0xF) MFN_PSTEP(0x114, 0xF) MFN_PSTEP(0x118, 0xF)
                 MFN_PSTEP(0x142, 0xA) MFN_PSTEP(0x143, 0xC)
 #undef MFN_PSTEP
-                // run index of each lane = heads at or before it - 1; heads write the exclusive prefix,
-                // tails the inclusive one and the keys
+                // run index of each lane = heads at or before it - 1; tails write the inclusive
+                // prefix and the keys
                 const uint64_t hb = __ballot(head);
                 const int nruns = __popcll(hb);
                 const int run = __builtin_amdgcn_mbcnt_hi((uint32_t)(hb >> 32),
                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u)) + (head ? 0 : -1);
-                if (head) {
-#pragma unroll
-                    for (int yz = 0; yz < 4; ++yz)
-                        lhead[wv][run][yz] = make_int4(P[yz][0] - q[yz][0], P[yz][1] - q[yz][1],
-                                                       P[yz][2] - q[yz][2], P[yz][3] - q[yz][3]);
-                }
                 if (tail) {
 #pragma unroll
                     for (int yz = 0; yz < 4; ++yz) {
@@ -536,47 +532,42 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_dense_kernel(const float* _
                         lkey[wv][run][yz] = make_int2(key[yz], key1[yz]);
                     }
                 }
-                if (flush && lane < 4) {  // the carried run as entry nruns
-                    ltail[wv][nruns][lane] = csum[wv][l][lane];
-                    lhead[wv][nruns][lane] = make_int4(0, 0, 0, 0);
-                    lkey[wv][nruns][lane] = ckey[wv][l][lane];
-                }
+                long long* gt = reinterpret_cast<long long*>(priv) +
+                                ((w & (GRAD_COPIES - 1)) * dense_entries + (int64_t)D.offset[l]);
+                // one run's 16 sums, 8 lanes = (row, x-corner), both features packed in one 64-bit add
+                auto issue = [&](int4 t, int2 kp, int c) {
+                    const int f0 = c ? t.z : t.x, f1 = c ? t.w : t.y;
+                    const long long pq = (long long)((uint64_t)(uint32_t)f1 << 32) + (long long)f0;
+                    if (pq != 0)
+                        __hip_atomic_fetch_add(gt + (c ? kp.y : kp.x), pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                };
+                // the run carried from the previous chunk that lane 0 did not continue: issued on its own
+                if (flush && lane < 8) issue(csum[wv][l][(lane >> 1) & 3], ckey[wv][l][(lane >> 1) & 3], lane & 1);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 __builtin_amdgcn_wave_barrier();
-                int nl = nruns + (flush ? 1 : 0);
-                // the run at lane 63 stays open when the window's next chunk follows: carried, and the
-                // list's last entry moves into its place
+                int nl = nruns;
+                // the run at lane 63 stays open when the window's next chunk follows: carried (its
+                // sums = its tail prefix minus the previous run's), and left out of this list
                 con[wv][l] = 0;
                 if (more && nruns > 0 && __shfl(tail ? 1 : 0, 63, 64)) {
                     const int r = nruns - 1;
                     if (lane < 4) {
-                        const int4 t = ltail[wv][r][lane], h = lhead[wv][r][lane];
+                        const int4 t = ltail[wv][r][lane];
+                        const int4 h = r > 0 ? ltail[wv][r - 1][lane] : make_int4(0, 0, 0, 0);
                         csum[wv][l][lane] = make_int4(t.x - h.x, t.y - h.y, t.z - h.z, t.w - h.w);
                         ckey[wv][l][lane] = lkey[wv][r][lane];
-                        if (nl - 1 != r) {  // move the flushed entry into slot r
-                            ltail[wv][r][lane] = ltail[wv][nl - 1][lane];
-                            lhead[wv][r][lane] = lhead[wv][nl - 1][lane];
-                            lkey[wv][r][lane] = lkey[wv][nl - 1][lane];
-                        }
                     }
                     con[wv][l] = 1;
                     nl -= 1;
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                 }
-                long long* gt = reinterpret_cast<long long*>(priv) +
-                                ((w & (GRAD_COPIES - 1)) * dense_entries + (int64_t)D.offset[l]);
-                // issue: 8 lanes per run = (row, x-corner); both features packed in one 64-bit add
                 for (int b = 0; b < nl; b += 8) {
-                    const int r = b + (lane >> 3), yz = (lane >> 1) & 3, c = lane & 1;
+                    const int r = b + (lane >> 3), yz = (lane >> 1) & 3;
                     if (r < nl) {
-                        const int4 t = ltail[wv][r][yz], h = lhead[wv][r][yz];
-                        const int f0 = c ? t.z - h.z : t.x - h.x, f1 = c ? t.w - h.w : t.y - h.y;
-                        const int2 kp = lkey[wv][r][yz];
-                        const int kk = c ? kp.y : kp.x;
-                        const long long pq = (long long)((uint64_t)(uint32_t)f1 << 32) + (long long)f0;
-                        if (pq != 0)
-                            __hip_atomic_fetch_add(gt + kk, pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const int4 t = ltail[wv][r][yz];
+                        const int4 h = r > 0 ? ltail[wv][r - 1][yz] : make_int4(0, 0, 0, 0);
+                        issue(make_int4(t.x - h.x, t.y - h.y, t.z - h.z, t.w - h.w), lkey[wv][r][yz], lane & 1);
                     }
                 }
                 __builtin_amdgcn_wave_barrier();  // the list is rewritten by the next level
