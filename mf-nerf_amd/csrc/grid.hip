@@ -1286,6 +1286,7 @@ __device__ __forceinline__ void accum_record(unsigned long long* img, int mask, 
 }
 
 constexpr int ACC_THREADS = 512;
+static_assert(MAX_BIN_ENTRIES % ACC_THREADS == 0, "the fused Adam's per-thread entries");
 
 // The rest of the optimizer step carried by the accumulate's launch (mfnerf_grid_encode_bw_binned_adam_all):
 // its first n_blocks workgroups run adam_fixed_body over the float4 groups [0, end4) -- the MLPs and
@@ -1435,21 +1436,32 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         const float bc1 = 1.0f - powf(A.beta1, (float)stp);
         const float bc2 = 1.0f - powf(A.beta2, (float)stp);
         const int64_t base_v = A.table_offset + 2 * ((int64_t)P.t_offset[t] + e_lo);
-        float2* pp = reinterpret_cast<float2*>(A.params + base_v);
-        float2* mm = reinterpret_cast<float2*>(A.m + base_v);
-        float2* vv = reinterpret_cast<float2*>(A.v + base_v);
-        __half2* hh = reinterpret_cast<__half2*>(reinterpret_cast<__half*>(A.p16) + base_v);
-        for (int i = threadIdx.x; i < n_e; i += blockDim.x) {
+        float2* __restrict__ pp = reinterpret_cast<float2*>(A.params + base_v);
+        float2* __restrict__ mm = reinterpret_cast<float2*>(A.m + base_v);
+        float2* __restrict__ vv = reinterpret_cast<float2*>(A.v + base_v);
+        __half2* __restrict__ hh = reinterpret_cast<__half2*>(reinterpret_cast<__half*>(A.p16) + base_v);
+        // every entry's optimizer state loaded before the first update (a load after the previous
+        // entry's stores would be one HBM round trip per entry the thread owns)
+        constexpr int IT = MAX_BIN_ENTRIES / ACC_THREADS;
+        float2 p[IT], m[IT], v[IT];
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int i = (int)threadIdx.x + k * ACC_THREADS;
+            if (i < n_e) { p[k] = pp[i]; m[k] = mm[i]; v[k] = vv[i]; }
+        }
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int i = (int)threadIdx.x + k * ACC_THREADS;
+            if (i >= n_e) break;
             const unsigned long long w = img[i];
             const int lo = (int)(uint32_t)w, hi = (int)(uint32_t)(w >> 32) + (lo < 0);
             const float g0 = (float)((lo + rd) >> kb) * is, g1 = (float)((hi + rd) >> kb) * is;
-            float2 p = pp[i], m = mm[i], v = vv[i];
-            mfn::adam_elem(p.x, m.x, v.x, g0, A.beta1, A.beta2, A.eps, lr, bc1, bc2);
-            mfn::adam_elem(p.y, m.y, v.y, g1, A.beta1, A.beta2, A.eps, lr, bc1, bc2);
-            pp[i] = p;
-            mm[i] = m;
-            vv[i] = v;
-            if (A.p16) hh[i] = __floats2half2_rn(p.x, p.y);
+            mfn::adam_elem(p[k].x, m[k].x, v[k].x, g0, A.beta1, A.beta2, A.eps, lr, bc1, bc2);
+            mfn::adam_elem(p[k].y, m[k].y, v[k].y, g1, A.beta1, A.beta2, A.eps, lr, bc1, bc2);
+            pp[i] = p[k];
+            mm[i] = m[k];
+            vv[i] = v[k];
+            if (A.p16) hh[i] = __floats2half2_rn(p[k].x, p[k].y);
         }
         return;
     }
