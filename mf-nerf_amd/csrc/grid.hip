@@ -1180,24 +1180,21 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
             // scan (one wave): bins -> sorted tile offsets; a run's k-th record goes to slot position
             // gdst + k; the counters are cleared for the next level
             if (threadIdx.x < 64) {
+                // bins q * 64 + lane per round (consecutive lanes on consecutive LDS words: no bank
+                // conflicts), each round an integer DPP wave scan plus the rounds before it (round 2:
+                // 4 bins per lane at stride 4 -- 8-way conflicts -- and a ds_bpermute scan)
                 const int lane = threadIdx.x;
                 const int per = (tb + 63) >> 6;
-                int sum = 0;
+                int carry = 0;
                 for (int q = 0; q < per; ++q) {
-                    const int lb = lane * per + q;
-                    sum += lb < tb ? hist[lb] : 0;
-                }
-                int x = sum;
-#pragma unroll
-                for (int off = 1; off < 64; off <<= 1) {
-                    const int y = __shfl_up(x, off, 64);
-                    if (lane >= off) x += y;
-                }
-                int run = x - sum;
-                for (int q = 0; q < per; ++q) {
-                    const int lb = lane * per + q;
+                    const int lb = q * 64 + lane;
+                    const int c = lb < tb ? hist[lb] : 0;
+                    int x = c;
+                    x += dppz_i<0x111, 0xF>(x); x += dppz_i<0x112, 0xF>(x);
+                    x += dppz_i<0x114, 0xF>(x); x += dppz_i<0x118, 0xF>(x);
+                    x += dppz_i<0x142, 0xA>(x); x += dppz_i<0x143, 0xC>(x);
+                    const int run = carry + x - c;
                     if (lb < tb) {
-                        const int c = hist[lb];
                         toff[lb] = run;
                         const int cu = cursor[b0 + lb];
                         // record k of the sorted stage is position cu - run + k of the slot
@@ -1205,10 +1202,10 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                                                   run + (int)slot - cu);
                         cursor[b0 + lb] = cu + c;
                         hist[lb] = 0;
-                        run += c;
                     }
+                    carry += __builtin_amdgcn_readlane(x, 63);
                 }
-                if (lane == 63) s_total[par] = x;
+                if (lane == 0) s_total[par] = carry;
             }
             __syncthreads();
             // place: the records sorted by bin into the stage
