@@ -20,6 +20,9 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "mf-nerf_amd")]
+# before the HIP runtime initialises (the same default mfnerf/__init__.py sets): graph replays
+# through the per-node launch path, ~3 us per step less
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 
 import torch  # noqa: E402
 
