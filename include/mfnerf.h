@@ -301,6 +301,10 @@ int mfnerf_field_pack_weights(const float* params_xyz, const float* params_rgb, 
                               mfnerf_stream_t stream);
 
 /* The same blob from the fp16 compute copy of the params (what packing the fp32 master gives). */
+/* tcnn SphericalHarmonics degree 4 (networks.py:60-67 dir_encoder; input (d/|d| + 1)/2 as
+ * networks.py:145-146 passes it): dirs01 (n, 3) f32 -> out (n, 16) f16.  The fused field head
+ * computes the same encoding inside mfnerf_field_fw/bw; this is the tinycudann module route's. */
+int mfnerf_sh4_fw(const float* dirs01, int64_t n, void* out_f16, mfnerf_stream_t stream);
 int mfnerf_field_pack_weights_f16(const void* params_xyz_f16, const void* params_rgb_f16, int rgb_width, void* packed,
                                   mfnerf_stream_t stream);
 

@@ -88,6 +88,43 @@ struct BwCfg {
     static_assert(SLOTS >= 2 && LDS <= 160 * 1024, "the backward's LDS must fit one CU");
 };
 
+// tcnn SphericalHarmonics degree 4 as a module of its own (the tinycudann route's dir_encoder,
+// networks.py:60-67): in = (d/|d| + 1)/2 (n, 3) f32 -> (n, 16) f16, the IEEE operations and their
+// order of mfnerf/tcnn.py sh4_torch (no contraction), rounded to f16 once.  The fused field head
+// evaluates the same polynomial in-kernel (sh4 above).
+__global__ __launch_bounds__(256) void sh4_fw_kernel(const float* __restrict__ in, int64_t n,
+                                                     __half* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = in[3 * i] * 2.0f - 1.0f, y = in[3 * i + 1] * 2.0f - 1.0f, z = in[3 * i + 2] * 2.0f - 1.0f;
+    const float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
+    float o[16];
+    o[0] = 0.28209479177387814f;
+    o[1] = -0.48860251190291987f * y;
+    o[2] = 0.48860251190291987f * z;
+    o[3] = -0.48860251190291987f * x;
+    o[4] = 1.0925484305920792f * xy;
+    o[5] = -1.0925484305920792f * yz;
+    o[6] = 0.94617469575755997f * z2 - 0.31539156525251999f;
+    o[7] = -1.0925484305920792f * xz;
+    o[8] = 0.54627421529603959f * x2 - 0.54627421529603959f * y2;
+    o[9] = 0.59004358992664352f * y * (-3.0f * x2 + y2);
+    o[10] = 2.8906114426405538f * xy * z;
+    o[11] = 0.45704579946446572f * y * (1.0f - 5.0f * z2);
+    o[12] = 0.3731763325901154f * z * (5.0f * z2 - 3.0f);
+    o[13] = 0.45704579946446572f * x * (1.0f - 5.0f * z2);
+    o[14] = 1.4453057213202769f * z * (x2 - y2);
+    o[15] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
+    // each value rounded to f32 first, as torch does: an opaque use keeps the compiler from folding a
+    // product and its f16 conversion into one v_fma_mix (a single rounding of the exact product,
+    // which differs from torch's double rounding on ~1 value in 10^6)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(o[k]));
+    __half2* dst = reinterpret_cast<__half2*>(out + 16 * i);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dst[k] = __floats2half2_rn(o[2 * k], o[2 * k + 1]);
+}
+
 template <typename TP, int W>
 __global__ void pack_kernel(const TP* __restrict__ px, const TP* __restrict__ pr, _Float16* __restrict__ out) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1075,6 +1112,14 @@ int mfnerf_field_pack_weights(const float* params_xyz, const float* params_rgb, 
     if (rgb_width == 64) launch_pack<float, 64>(params_xyz, params_rgb, packed, stream);
     else launch_pack<float, 128>(params_xyz, params_rgb, packed, stream);
     return mfn_check_launch("field_pack_weights");
+}
+
+int mfnerf_sh4_fw(const float* dirs01, int64_t n, void* out_f16, mfnerf_stream_t stream) {
+    if (n < 0 || (n > 0 && (!dirs01 || !out_f16))) { mfn_set_error("sh4_fw: bad arguments"); return MFN_ERR_INVALID; }
+    if (n == 0) return MFN_OK;
+    hipLaunchKernelGGL(sh4_fw_kernel, dim3((unsigned)div_up<int64_t>(n, 256)), dim3(256), 0, stream, dirs01, n,
+                       (__half*)out_f16);
+    return mfn_check_launch("sh4_fw");
 }
 
 int mfnerf_field_pack_weights_f16(const void* params_xyz_f16, const void* params_rgb_f16, int rgb_width, void* packed,

@@ -907,8 +907,11 @@ __device__ __forceinline__ void level_records_geo(const mfnerf_grid_desc& D, con
 // every x + 1 below 2^shift, so the x-pair never straddles a partition): one record per (y,z) row,
 // the hash written out (corner_index's prime hash masked to the table size, no layout branches), the
 // partition from the index's high bits, and s0 / s1 already scaled by the table unit x 2^-15 (exact:
-// a power of two), so rec_values' own scaling is gone.  Same records, bit for bit, as
-// level_records_geo.  EMIT(row, partition in the table, record).
+// a power of two), so rec_values' own scaling is gone.  The same records as level_records_geo but
+// for the fp16 rounding of a value: the compiler folds wyz * s0 and its conversion into one v_fma_mix
+// (the exact product rounded once to f16), where level_records_geo rounds the product to f32 first
+// (its last, exact scaling folds instead) -- the two differ only where that f32 rounding crosses an
+// f16 rounding boundary.  Still deterministic.  EMIT(row, partition in the table, record).
 template <typename EMIT>
 __device__ __forceinline__ void pair_level_records(const mfnerf_grid_desc& D, const BinPlan& P, int l, float x,
                                                    float y, float z, float s0, float s1, EMIT&& emit) {

@@ -86,6 +86,7 @@ SIGNATURES = {
     "mfnerf_grid_level_l1": (_I, [_P, _I64, _P, _I, _P, _P]),
     "mfnerf_field_packed_bytes": (_I64, [_I]),
     "mfnerf_field_pack_weights_f16": (_I, [_P, _P, _I, _P, _P]),
+    "mfnerf_sh4_fw": (_I, [_P, _I64, _P, _P]),
     "mfnerf_field_pack_weights": (_I, [_P, _P, _I, _P, _P]),
     "mfnerf_field_fw": (_I, [_P, _I64, _P, _I64, _P, _P, _I, _I, _P, _P, _P]),
     "mfnerf_field_bw_workspace": (_I64, [_I64, _I]),

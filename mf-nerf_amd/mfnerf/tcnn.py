@@ -145,7 +145,19 @@ class Encoding(torch.nn.Module):
     def forward(self, x):
         if self.kind == "grid":
             return GridEncodeFunction.apply(x, self.params, self.layout, self.desc)
+        if x.is_cuda and not (torch.is_grad_enabled() and x.requires_grad) and self.n_output_dims == 16:
+            return sh4_fw(x)  # the HIP kernel (the reference feeds it rays, which carry no gradient)
         return sh4_torch(x.float()).half()
+
+
+def sh4_fw(d01):
+    """(n, 3) directions mapped to [0, 1] -> (n, 16) f16 SH degree 4 (mfnerf_sh4_fw; the same IEEE
+    operations as sh4_torch)."""
+    lead = d01.shape[:-1]
+    x = d01.reshape(-1, 3).float().contiguous()
+    out = torch.empty(x.shape[0], 16, dtype=torch.float16, device=x.device)
+    call("mfnerf_sh4_fw", ptr(x), x.shape[0], ptr(out), stream())
+    return out.reshape(*lead, 16)
 
 
 def sh4_torch(d01):

@@ -124,3 +124,22 @@ def test_module_route_matches_fused_field(gpu):
     for (a, b) in ((gx_m[:n_net], gx_f[:n_net]), (gx_m[n_net:], gx_f[n_net:]), (gr_m, gr_f)):
         assert float((a - b).norm()) <= 3e-2 * float(b.norm())
         assert float(torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0)) > 0.999
+
+
+def test_sh4_fw_kernel_matches_the_torch_restatement(gpu):
+    """mfnerf_sh4_fw (the tinycudann route's SphericalHarmonics degree 4, networks.py:60-67) against
+    sh4_torch, bit for bit, on directions mapped to [0, 1] as networks.py:145-146 does, including
+    the axis-aligned and diagonal extremes; and the Encoding module picks the kernel."""
+    from mfnerf import tcnn as T
+    g = torch.Generator().manual_seed(5)
+    d = torch.randn(100003, 3, generator=g)
+    d = torch.cat([d, torch.eye(3), -torch.eye(3), torch.ones(1, 3), -torch.ones(1, 3)])
+    d01 = (d / d.norm(dim=-1, keepdim=True) + 1) / 2
+    ref = T.sh4_torch(d01.to(gpu).float()).half()
+    got = T.sh4_fw(d01.to(gpu))
+    torch.cuda.synchronize()
+    assert got.dtype == torch.float16 and got.shape == (d01.shape[0], 16)
+    assert torch.equal(got, ref)
+    enc = T.Encoding(3, {"otype": "SphericalHarmonics", "degree": 4})
+    with torch.no_grad():
+        assert torch.equal(enc(d01.to(gpu)), ref)
