@@ -1881,7 +1881,10 @@ int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32
     const int64_t fused_from = adam->table_offset + 2 * (int64_t)P.t_offset[0];  // the partitioned tables' first value
     if (fused_from % 4) { mfn_set_error("grid_encode_bw_binned_adam_all: partitions not float4-aligned"); return MFN_ERR_INVALID; }
     BinWorkspace W;
-    binned_workspace_layout(desc, n_slots <= 0 || n_slots > n ? n : n_slots, (char*)workspace, &W);
+    if (binned_workspace_layout(desc, n_slots <= 0 || n_slots > n ? n : n_slots, (char*)workspace, &W) < 0) {
+        mfn_set_error("grid_encode_bw_binned_adam_all: the record slots overflow 32-bit record indices");
+        return MFN_ERR_INVALID;
+    }
     // [0, fused_from) by the accumulate launch's leading workgroups (one float4 per thread, <= 256 of them)
     AdamRest X{grads, (int*)workspace, 2 * dense_entries_of(desc), total, fused_from / 4, 0, 1};
     // <= 256 workgroups, the grid's first (256 vs 64 of them 0.655 vs 0.657 ms/step; first vs last
@@ -1945,7 +1948,11 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
         return MFN_ERR_INVALID;
     }
     BinWorkspace W;
-    binned_workspace_layout(desc, n_slots, (char*)workspace, &W);
+    if (binned_workspace_layout(desc, n_slots, (char*)workspace, &W) < 0) {
+        mfn_set_error("grid_encode_bw_binned: %lld record slots per partition and unit overflow 32-bit record "
+                      "indices (size the slots for fewer samples, n_slots)", (long long)n_slots);
+        return MFN_ERR_INVALID;
+    }
     const int l_first = first_binned_level(desc);
     const int64_t want = div_up<int64_t>(div_up<int64_t>(n, 16), ENC_BLOCK / 64);
     const int64_t cap = grid_bw_block_cap();
