@@ -167,9 +167,13 @@ __global__ __launch_bounds__(OCC_BLOCK) void occ_scatter_kernel(const float* __r
     }
 }
 
+// The mean over positive cells: each decay workgroup writes its partial (sum, count); the
+// threshold kernel adds the partials in workgroup order (deterministic; round 2 added them with two
+// memory-side atomics per workgroup on one address each: 4096 serialised atomics, ~55 us).
+constexpr int DECAY_BLOCKS = 256;
 struct OccStats {
-    double sum;
-    unsigned long long count;
+    double sum[DECAY_BLOCKS];
+    unsigned long long count[DECAY_BLOCKS];
     float thr;
 };
 
@@ -196,15 +200,27 @@ __global__ __launch_bounds__(OCC_BLOCK) void occ_decay_kernel(float* __restrict_
     s = block_sum(s, lds_d);
     k = block_sum(k, lds_u);
     if (threadIdx.x == 0) {
-        atomicAdd(&st->sum, s);
-        atomicAdd(&st->count, k);
+        st->sum[blockIdx.x] = s;
+        st->count[blockIdx.x] = k;
     }
 }
 
-// thr = min(mean, threshold) with Python's min(): NaN mean (no positive cell) stays NaN
-__global__ void occ_thr_kernel(OccStats* st, float threshold) {
-    const float mean = st->count ? (float)(st->sum / (double)st->count) : __builtin_nanf("");
-    st->thr = (threshold < mean) ? threshold : mean;
+// thr = min(mean, threshold) with Python's min(): NaN mean (no positive cell) stays NaN.  One wave:
+// the partials of nb <= DECAY_BLOCKS workgroups summed in a fixed lane / tree order.
+__global__ void occ_thr_kernel(OccStats* st, int nb, float threshold) {
+    const int lane = threadIdx.x;
+    double s = 0.0;
+    unsigned long long k = 0;
+    for (int b = lane; b < nb; b += 64) { s += st->sum[b]; k += st->count[b]; }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        s += __shfl_xor(s, off, 64);
+        k += __shfl_xor(k, off, 64);
+    }
+    if (lane == 0) {
+        const float mean = k ? (float)(s / (double)k) : __builtin_nanf("");
+        st->thr = (threshold < mean) ? threshold : mean;
+    }
 }
 
 int64_t blocks_for(int64_t n, int64_t cap = 8192) {
@@ -298,13 +314,13 @@ int mfnerf_occupancy_update(float* density_grid, const float* sigmas, const int3
     ws_layout(cascades, grid_size, (char*)workspace, &w);
     const int64_t n = (int64_t)cascades * grid_size * grid_size * grid_size;
     (void)hipMemsetAsync(tmp, 0, n * sizeof(float), stream);
-    (void)hipMemsetAsync(w.stats, 0, sizeof(OccStats), stream);
     if (n_points)
         hipLaunchKernelGGL(occ_scatter_kernel, dim3(blocks_for(n_points)), dim3(OCC_BLOCK), 0, stream, sigmas, cell_idx,
                            n_points, tmp);
-    hipLaunchKernelGGL(occ_decay_kernel, dim3(blocks_for(n, 2048)), dim3(OCC_BLOCK), 0, stream, density_grid, tmp,
-                       count_grid, n, decay, w.stats);
-    hipLaunchKernelGGL(occ_thr_kernel, dim3(1), dim3(1), 0, stream, w.stats, density_threshold);
+    const int nb = (int)blocks_for(n, DECAY_BLOCKS);  // every partial written (grid-stride beyond)
+    hipLaunchKernelGGL(occ_decay_kernel, dim3(nb), dim3(OCC_BLOCK), 0, stream, density_grid, tmp, count_grid, n,
+                       decay, w.stats);
+    hipLaunchKernelGGL(occ_thr_kernel, dim3(1), dim3(64), 0, stream, w.stats, nb, density_threshold);
     int st = mfn_check_launch("occupancy_update");
     if (st) return st;
     return mfnerf_packbits(density_grid, n / 8, 0.0f, &w.stats->thr, bitfield, stream);
