@@ -385,6 +385,12 @@ int64_t mfnerf_occupancy_points(int cascades, int grid_size, int64_t n_uniform, 
 int mfnerf_occupancy_cells(const float* density_grid, int cascades, int grid_size, float scale, int64_t n_uniform,
                            int warmup, float density_threshold, uint64_t seed, uint64_t call_index, float* xyzs,
                            int32_t* cell_idx, void* workspace, mfnerf_stream_t stream);
+/* mfnerf_occupancy_cells with the call index read from (and then advanced in) device memory, so a
+ * captured refresh draws new cells on every replay: call_index_dev (uint64, device) = the value
+ * mfnerf_occupancy_cells' call_index would have; the same draws for the same index. */
+int mfnerf_occupancy_cells_dev(const float* density_grid, int cascades, int grid_size, float scale, int64_t n_uniform,
+                               int warmup, float density_threshold, uint64_t seed, uint64_t* call_index_dev,
+                               float* xyzs, int32_t* cell_idx, void* workspace, mfnerf_stream_t stream);
 int mfnerf_occupancy_update(float* density_grid, const float* sigmas, const int32_t* cell_idx, int64_t n_points,
                             int cascades, int grid_size, float decay, const float* count_grid, float density_threshold,
                             float* tmp, uint8_t* bitfield, void* workspace, mfnerf_stream_t stream);

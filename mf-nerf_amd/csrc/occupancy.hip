@@ -34,12 +34,13 @@ __device__ __forceinline__ uint32_t mix64to32(uint64_t x) {
 }
 // per-call key: the call index goes through a full avalanche (added linearly to the counter it
 // would make draw (call c, k) equal draw (call c+1, k-1))
-uint64_t splitmix64_host(uint64_t x) {
+__host__ __device__ __forceinline__ uint64_t splitmix64_host(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
     x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
     return x ^ (x >> 31);
 }
+constexpr uint64_t OCC_SEED_MIX = 0x5851F42D4C957F2Dull;
 __device__ __forceinline__ uint32_t rnd32(uint64_t key, uint64_t ctr) {
     return mix64to32(key + ctr * 0x9E3779B97F4A7C15ull);
 }
@@ -119,6 +120,8 @@ struct PointsArgs {
     int warmup;
     float scale;
     uint64_t key;
+    uint64_t seed;
+    const uint64_t* call_dev;  // non-null: key from the device-resident call index (graph replays)
 };
 
 // networks.py:253-258: s = min(2^(c-1), scale); x = (coords/(G-1)*2-1)*(s - s/G) + (2u-1)*(s/G)
@@ -126,6 +129,7 @@ __global__ __launch_bounds__(OCC_BLOCK) void occ_points_kernel(PointsArgs a, con
                                                                const int32_t* __restrict__ counts,
                                                                float* __restrict__ xyzs, int32_t* __restrict__ cell) {
     const int64_t n = (int64_t)a.cascades * a.per_cascade;
+    if (a.call_dev) a.key = splitmix64_host(splitmix64_host(a.seed ^ OCC_SEED_MIX) ^ *a.call_dev);
     for (int64_t p = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; p < n; p += (int64_t)gridDim.x * OCC_BLOCK) {
         const int c = (int)(p / a.per_cascade);
         const int64_t j = p - (int64_t)c * a.per_cascade;
@@ -254,6 +258,14 @@ int64_t ws_layout(int cascades, int G, char* base, Ws* w) {
 
 bool bad_grid(int cascades, int G) { return cascades < 1 || cascades > 16 || G < 1 || G > 1024 || ((int64_t)G * G * G) % 8; }
 
+// the refresh's call index kept on the device (mfnerf_occupancy_cells_dev): one lane, a vector store
+__global__ void occ_call_bump_kernel(uint64_t* call) {
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(call, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+int occupancy_cells_impl(const float* density_grid, int cascades, int grid_size, float scale, int64_t n_uniform,
+                         int warmup, float density_threshold, uint64_t seed, uint64_t call_index, uint64_t* call_dev,
+                         float* xyzs, int32_t* cell_idx, void* workspace, mfnerf_stream_t stream);
+
 }  // namespace
 
 extern "C" {
@@ -272,6 +284,27 @@ int64_t mfnerf_occupancy_points(int cascades, int grid_size, int64_t n_uniform, 
 int mfnerf_occupancy_cells(const float* density_grid, int cascades, int grid_size, float scale, int64_t n_uniform,
                            int warmup, float density_threshold, uint64_t seed, uint64_t call_index, float* xyzs,
                            int32_t* cell_idx, void* workspace, mfnerf_stream_t stream) {
+    return occupancy_cells_impl(density_grid, cascades, grid_size, scale, n_uniform, warmup, density_threshold, seed,
+                                call_index, nullptr, xyzs, cell_idx, workspace, stream);
+}
+
+int mfnerf_occupancy_cells_dev(const float* density_grid, int cascades, int grid_size, float scale, int64_t n_uniform,
+                               int warmup, float density_threshold, uint64_t seed, uint64_t* call_index_dev,
+                               float* xyzs, int32_t* cell_idx, void* workspace, mfnerf_stream_t stream) {
+    if (!call_index_dev) { mfn_set_error("occupancy_cells_dev: null call index"); return MFN_ERR_INVALID; }
+    const int st = occupancy_cells_impl(density_grid, cascades, grid_size, scale, n_uniform, warmup, density_threshold,
+                                        seed, 0, call_index_dev, xyzs, cell_idx, workspace, stream);
+    if (st) return st;
+    hipLaunchKernelGGL(occ_call_bump_kernel, dim3(1), dim3(64), 0, stream, call_index_dev);
+    return mfn_check_launch("occupancy_cells_dev");
+}
+
+}  // extern "C"
+
+namespace {
+int occupancy_cells_impl(const float* density_grid, int cascades, int grid_size, float scale, int64_t n_uniform,
+                         int warmup, float density_threshold, uint64_t seed, uint64_t call_index, uint64_t* call_dev,
+                         float* xyzs, int32_t* cell_idx, void* workspace, mfnerf_stream_t stream) {
     if (bad_grid(cascades, grid_size)) { mfn_set_error("occupancy_cells: bad cascades/grid_size"); return MFN_ERR_INVALID; }
     if (n_uniform < 0 || (!warmup && n_uniform == 0)) { mfn_set_error("occupancy_cells: bad n_uniform"); return MFN_ERR_INVALID; }
     if (!density_grid || !xyzs || !cell_idx || !workspace) { mfn_set_error("occupancy_cells: null pointer"); return MFN_ERR_INVALID; }
@@ -294,12 +327,17 @@ int mfnerf_occupancy_cells(const float* density_grid, int cascades, int grid_siz
     a.n_uniform = warmup ? 0 : n_uniform;
     a.warmup = warmup ? 1 : 0;
     a.scale = scale;
-    a.key = splitmix64_host(splitmix64_host(seed ^ 0x5851F42D4C957F2Dull) ^ call_index);
+    a.key = splitmix64_host(splitmix64_host(seed ^ OCC_SEED_MIX) ^ call_index);
+    a.seed = seed;
+    a.call_dev = call_dev;
     const int64_t n = (int64_t)cascades * a.per_cascade;
     hipLaunchKernelGGL(occ_points_kernel, dim3(blocks_for(n)), dim3(OCC_BLOCK), 0, stream, a, w.list, w.counts, xyzs,
                        cell_idx);
     return mfn_check_launch("occupancy_cells");
 }
+}  // namespace
+
+extern "C" {
 
 int mfnerf_occupancy_update(float* density_grid, const float* sigmas, const int32_t* cell_idx, int64_t n_points,
                             int cascades, int grid_size, float decay, const float* count_grid, float density_threshold,

@@ -972,7 +972,8 @@ class TrainStep:
             o.sigma = torch.empty(n, dtype=torch.float32, device=self.dev)
             o.tmp = torch.empty(C * G ** 3, dtype=torch.float32, device=self.dev)
             o.ws = torch.empty(lib.mfnerf_occupancy_workspace(C, G), dtype=torch.uint8, device=self.dev)
-            o.calls = 0
+            o.calls = torch.zeros(1, dtype=torch.int64, device=self.dev)  # the draws' call index (device)
+            o.graphs = {}
             self._occ = o
         return self._occ
 
@@ -980,15 +981,32 @@ class TrainStep:
     def update_density_grid(self, warmup=False, decay=0.95, count_grid=None, seed=0):
         """NGP.update_density_grid(0.01*MAX_SAMPLES/sqrt(3), warmup, erode) as five device launches
         (cells -> grid_encode_fw -> field_fw density-only -> scatter/decay/mean -> packbits); no
-        host synchronisation, so it can sit inside a captured step sequence."""
+        host synchronisation.  Without erosion (count_grid) the launches are captured once per
+        (warmup, decay, seed) and replayed as one HIP graph (the draws' call index lives on the
+        device, so every replay draws new cells): 0.45 ms of mostly launch overhead eagerly
+        (DESIGN.md 6).  MFNERF_OCC_GRAPH=0: always eager."""
+        o = self._occ_buffers()
+        if count_grid is not None or os.environ.get("MFNERF_OCC_GRAPH", "1") != "1":
+            self._occ_launches(warmup, decay, count_grid, seed)
+            return
+        key = (bool(warmup), float(decay), int(seed))
+        g = o.graphs.get(key)
+        if g is None:
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._occ_launches(warmup, decay, None, seed)
+            o.graphs[key] = g  # (capturing ran nothing)
+        g.replay()
+
+    def _occ_launches(self, warmup, decay, count_grid, seed):
         c, C, G, s = self.cfg, self.cascades, self.G, stream()
         o = self._occ_buffers()
         thr = 0.01 * MAX_SAMPLES / SQRT3
         M = G ** 3 // 4
         n = load().mfnerf_occupancy_points(C, G, M, int(warmup))
-        call("mfnerf_occupancy_cells", ptr(self.density_grid), C, G, float(c.scale), M, int(warmup), thr, seed,
-             o.calls, ptr(o.xyz), ptr(o.cell), ptr(o.ws), s)
-        o.calls += 1
+        call("mfnerf_occupancy_cells_dev", ptr(self.density_grid), C, G, float(c.scale), M, int(warmup), thr, seed,
+             ptr(o.calls), ptr(o.xyz), ptr(o.cell), ptr(o.ws), s)
         call("mfnerf_grid_encode_fw_planar", ptr(o.xyz), n, None, self.x_min, self.x_range, self.desc,
              ptr(self.p16[self.off_table:]), ptr(o.feat), o.n_max, s)
         call("mfnerf_field_fw", ptr(o.feat), o.n_max, None, n, None, ptr(self.packed), c.rgb_width, 1, ptr(o.sigma), None, s)
