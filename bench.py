@@ -202,6 +202,8 @@ def main():
     torch.cuda.set_device(dev)
 
     from mfnerf import dp, engine, synthetic
+    if args.dp_rehearse:
+        dp.rehearse(True)  # the one-rank group's collectives through RCCL (skipped otherwise)
 
     pre = dict(PRESETS[args.preset])
     if args.n_rays is not None:

@@ -828,7 +828,10 @@ int check_desc(const mfnerf_grid_desc* d, const char* what) {
 // partitions of 2^shift entries, shift in [MIN_BIN_SHIFT, MAX_BIN_SHIFT] chosen per layout so that
 // there are >= ~1024 partitions (4 workgroups per CU); 2^11 entries = 16 KB of packed int32 pairs
 constexpr int MIN_BIN_SHIFT = 8, MAX_BIN_SHIFT = 11, MAX_BIN_ENTRIES = 1 << MAX_BIN_SHIFT;
-constexpr int MAX_BINS = 4096;
+// partitions over all binned tables: the first LDS_CURSOR keep the scatter unit's running counts in
+// LDS, the rest (own tables of 2^20-2^21 entries: --T 20/21, opt.py:78) in the unit's column of the
+// slot counts in global memory, read and written by the one scanning wave
+constexpr int LDS_CURSOR = 4096, MAX_BINS = 16384;
 
 struct BinPlan {
     int n_binned;                    // levels routed through the bins
@@ -1095,7 +1098,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                                                                  int32_t* __restrict__ ovf, int64_t n_slots,
                                                                  int* __restrict__ ovw) {
     constexpr int SPT = PAIR ? 2 : 1;  // samples per thread per tile
-    __shared__ int cursor[MAX_BINS];
+    __shared__ int cursor[LDS_CURSOR];
     __shared__ int hist[MAX_TBINS], toff[MAX_TBINS];
     // per bin of the staged level: {index of the stage's first record of the bin in rec[] minus its
     // stage offset, the stage index its slot ends at} (one 8-B LDS read per stored record)
@@ -1106,7 +1109,11 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
     __shared__ int s_total[2];
     uint32_t rmax2 = 0u;  // largest |a| (low half), |b| (high half) of this thread's records, fp16 bits
     load_fixed_scales(D, level_l1, fs_s);
-    for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x) cursor[b] = 0;
+    for (int b = threadIdx.x; b < min(P.n_bins, LDS_CURSOR); b += blockDim.x) cursor[b] = 0;
+    // the running counts of the bins past LDS_CURSOR live in scnt: zeroed by the scanning wave,
+    // the only one that touches them (program order within the wave)
+    if (threadIdx.x < 64)
+        for (int b = LDS_CURSOR + (int)threadIdx.x; b < P.n_bins; b += 64) scnt[(int64_t)b * UNITS + blockIdx.x] = 0;
     for (int b = threadIdx.x; b < MAX_TBINS; b += blockDim.x) hist[b] = 0;
     if (threadIdx.x < 2) s_total[threadIdx.x] = 0;
     __syncthreads();
@@ -1199,11 +1206,14 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                     const int run = carry + x - c;
                     if (lb < tb) {
                         toff[lb] = run;
-                        const int cu = cursor[b0 + lb];
+                        const int gb = b0 + lb;
+                        int32_t* gc = scnt + (int64_t)gb * UNITS + u;  // (bins past LDS_CURSOR)
+                        const int cu = gb < LDS_CURSOR ? cursor[gb] : *gc;
                         // record k of the sorted stage is position cu - run + k of the slot
                         gdst[par][lb] = make_int2((int)((uint32_t)(b0 + lb) * UNITS + u) * (int)slot + cu - run,
                                                   run + (int)slot - cu);
-                        cursor[b0 + lb] = cu + c;
+                        if (gb < LDS_CURSOR) cursor[gb] = cu + c;
+                        else *gc = cu + c;
                         hist[lb] = 0;
                     }
                     carry += __builtin_amdgcn_readlane(x, 63);
@@ -1245,11 +1255,16 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
     // zeroed by the next step's first scatter launch); ovf[1]: their running total (never reset by
     // the kernels: mfnerf_grid_encode_bw_binned_flag_offset + 4 bytes, read by the training tools)
     int over = 0;
-    for (int b = threadIdx.x; b < P.n_bins; b += blockDim.x) {
+    for (int b = threadIdx.x; b < min(P.n_bins, LDS_CURSOR); b += blockDim.x) {
         const int c = cursor[b];
         over += c > slot ? (int)(c - slot) : 0;
         scnt[(int64_t)b * UNITS + u] = c;
     }
+    if (threadIdx.x < 64)  // the counts past LDS_CURSOR: already in scnt, read back by the wave that wrote them
+        for (int b = LDS_CURSOR + (int)threadIdx.x; b < P.n_bins; b += 64) {
+            const int c = scnt[(int64_t)b * UNITS + u];
+            over += c > slot ? (int)(c - slot) : 0;
+        }
     if (over) {
         atomicAdd(ovf, over);
         atomicAdd(ovf + 1, over);

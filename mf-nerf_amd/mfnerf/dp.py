@@ -12,6 +12,8 @@ There is no per-step buffer broadcast (DDP's broadcast_buffers moved ~40 MiB/ste
 reference); the occupancy grid is refreshed identically on every rank from identical parameters.
 Backend "nccl" is RCCL over xGMI on MI355X; "gloo" is used for the CPU tests.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -32,10 +34,21 @@ def _host_staged(fn, *ts):
         t.copy_(h)
 
 
+# A one-rank process group skips the collectives (they are identities there, and gloo would copy the
+# whole flat gradient and fp16 copy through host memory and back every step) unless a rehearsal asks
+# for them: bench.py --dp-rehearse and the one-GPU tests run the backend's single-rank path on purpose.
+_REHEARSE = os.environ.get("MFNERF_DP_REHEARSE", "0") == "1"
+
+
+def rehearse(on=True):
+    """Route the collectives through the backend even at world size 1 (measurement / tests)."""
+    global _REHEARSE
+    _REHEARSE = bool(on)
+
+
 def _on():
-    """A process group is up (world size 1 included: the collectives then still run through the
-    backend -- RCCL's single-rank path is what tests/test_gpu_dp.py drives on the one-GPU box)."""
-    return dist.is_available() and dist.is_initialized()
+    """A process group of more than one rank is up (or a one-rank group under rehearse())."""
+    return dist.is_available() and dist.is_initialized() and (_REHEARSE or dist.get_world_size() > 1)
 
 
 def allreduce_mean_(flat):

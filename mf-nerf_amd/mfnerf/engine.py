@@ -180,6 +180,7 @@ class TrainStep:
         # normal.  With the dynamic scale (default) field_bw reads amp.scale on the device instead.
         self.grad_scale = float(2.0 ** max(0, int(math.floor(math.log2(N))) - 2))
         self._primed = False
+        self._stale_pack = False  # a one-graph data-parallel replay left `packed` one update behind
         self.dataset = None
 
     def reset_loss_scale(self, scale=None):
@@ -328,6 +329,16 @@ class TrainStep:
         would produce), so it works on every rank when the fp32 master is sharded."""
         call("mfnerf_field_pack_weights_f16", ptr(self.p16), ptr(self.p16[self.off_rgb:]), self.cfg.rgb_width,
              ptr(self.packed), stream())
+
+    def _flush_pack(self):
+        """Repack if a one-graph data-parallel replay deferred it: that path's Adam runs after the
+        collective and the next dp_pre graph starts with the repack, so until then `packed` is one
+        update behind.  Everything else that reads `packed` (an eager step, the occupancy refresh,
+        the per-stage graphs) calls this first."""
+        if self._stale_pack:
+            pg = (self.graphs or {}).get("pack")
+            pg.replay() if pg is not None else self._pack()
+            self._stale_pack = False
 
     def shard_optimizer(self, rank, world, force=False):
         """Data parallel with a sharded optimizer (mfnerf.dp.sharded_update): this rank keeps Adam
@@ -640,6 +651,7 @@ class TrainStep:
         optimize=False stops after the backward and leaves the step's gradient in self.grads (no
         Adam step, no repack; for inspection)."""
         mark = mark or (lambda name: None)
+        self._flush_pack()
         mb = self.mbuf[0]
         prepped = batch is None
         if prepped:
@@ -695,6 +707,7 @@ class TrainStep:
         drawn from the step's generator (parity tests driving several processes with one draw).
         Call after at least one eager step (lazy library init happens outside capture)."""
         N = self.cfg.n_rays
+        self._flush_pack()
         if len(self.mbuf) == 1:
             self.mbuf.append(self._march_buffers())
         self._static = [_packed_batch(torch.zeros(3, N, 3, device=self.dev)) for _ in range(2)]
@@ -803,7 +816,6 @@ class TrainStep:
         self._ev_part = [torch.cuda.Event() for _ in range(P)]
         self._parity = 0
         self._primed = False
-        self._stale_pack = False  # a dp_pre step left the repack to the next step's graph
         # where the next step's march starts: under this step's grid_bw (default) or at its start
         self.march_early = os.environ.get("MFNERF_MARCH_EARLY", "0") == "1"
 
@@ -905,9 +917,7 @@ class TrainStep:
             self._primed = True
             return
         fuse_tail = g.get("finish_update") is not None and not dp_mode
-        if self._stale_pack:
-            g["pack"].replay()
-            self._stale_pack = False
+        self._flush_pack()
         early = prefetch and self.march_early
         if early:  # set 1-j was last read by the previous step, all of which precedes _ev_start
             self._march_on_side(1 - j, next_batch, self._ev_start, noise=next_noise)
@@ -986,6 +996,7 @@ class TrainStep:
         device, so every replay draws new cells): 0.45 ms of mostly launch overhead eagerly
         (DESIGN.md 6).  MFNERF_OCC_GRAPH=0: always eager."""
         o = self._occ_buffers()
+        self._flush_pack()  # the density query runs the field on `packed`
         if count_grid is not None or os.environ.get("MFNERF_OCC_GRAPH", "1") != "1":
             self._occ_launches(warmup, decay, count_grid, seed)
             return

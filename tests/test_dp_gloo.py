@@ -102,3 +102,54 @@ def test_two_rank_sharded_optimizer_matches_allreduce():
     out = mgr.dict()
     mp.spawn(_sharded_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     assert torch.equal(out[0], out[1])
+
+
+class _Counting:
+    """Counts the process-group collectives a callable issues (torch.distributed patched)."""
+
+    def __init__(self):
+        self.n = 0
+
+    def __enter__(self):
+        self._saved = {k: getattr(dist, k) for k in ("all_reduce", "reduce_scatter_tensor", "all_gather_into_tensor")}
+        for k, f in self._saved.items():
+            def wrap(*a, _f=f, **kw):
+                self.n += 1
+                return _f(*a, **kw)
+            setattr(dist, k, wrap)
+        return self
+
+    def __exit__(self, *exc):
+        for k, f in self._saved.items():
+            setattr(dist, k, f)
+
+
+def _one_rank_worker(rank, port, out):
+    import sys
+    sys.path[:0] = [ROOT, PKG]
+    from mfnerf import dp
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    x = torch.randn(4096)
+    sh, full = torch.empty(4096), x.half()
+    res = []
+    for rehearse in (False, True):
+        dp.rehearse(rehearse)
+        with _Counting() as c:
+            y = dp.allreduce_mean_(x.clone())
+            dp.reduce_scatter_mean_(sh, x)
+            dp.all_gather_(full, 0)
+        res.append((c.n, torch.equal(y, x), torch.equal(sh, x), torch.equal(full, x.half())))
+    dp.rehearse(False)
+    out["r"] = res
+    dist.destroy_process_group()
+
+
+def test_one_rank_group_skips_collectives_unless_rehearsing():
+    """A one-rank process group pays nothing per step (the collectives are identities and gloo would
+    stage the flat gradient through host memory); dp.rehearse() routes them through the backend."""
+    out = mp.Manager().dict()
+    mp.spawn(_one_rank_worker, args=(_free_port(), out), nprocs=1, join=True)
+    (n_off, *ok_off), (n_on, *ok_on) = out["r"]
+    assert n_off == 0 and all(ok_off)
+    assert n_on == 3 and all(ok_on)

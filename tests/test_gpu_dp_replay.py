@@ -73,32 +73,39 @@ def _bench_worker(rank, world, port, mode, out):
     mk = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     for k in range(1, K):
         a.replay(exchange=ex, grid_bw_events=(mk(), [mk()]) if k == 2 else None)
+    # the last replay deferred the repack to the next step's graph: an occupancy refresh and an eager
+    # step right after it must see the updated weights (they repack first)
+    a.update_density_grid()
+    a.run(exchange=ex)
     torch.cuda.synchronize()
     got = _state(a)
+    got["grid"] = a.density_grid.cpu()
     # eager DP steps on the same draws (the dataset's draw counter lives on the device)
     b = _step(dev, mode, rank, world, _dataset(rank, dev))
     for k in range(K):
         b.run(exchange=ex)
+    b.update_density_grid()
+    b.run(exchange=ex)
     torch.cuda.synchronize()
-    b._pack()
-    torch.cuda.synchronize()
-    out[(mode, rank)] = (got, _state(b))
+    ref = _state(b)
+    ref["grid"] = b.density_grid.cpu()
+    out[(mode, rank)] = (got, ref)
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("mode", ["shard", "allreduce"])
 def test_dp_replay_as_bench_matches_eager_dp(mode):
     """bench.py's replay path (dp_pre / collective / dp_post graphs, gated march, one event-timed
-    per-stage step in between) leaves every rank bit-identical to the eager DP step on the same
-    batches, and the replicas identical across ranks."""
+    per-stage step in between), then an occupancy refresh and an eager step, leaves every rank
+    bit-identical to the eager DP steps on the same batches (weights, fp16 copy, packed MLP blob,
+    density grid), and the replicas identical across ranks."""
     world = 2
     out = mp.Manager().dict()
     mp.spawn(_bench_worker, args=(world, _port(), mode, out), nprocs=world, join=True)
     for r in range(world):
         got, ref = out[(mode, r)]
-        # the replayed graphs leave the repack to the next step; the eager reference was repacked
-        assert got["steps"] == ref["steps"] == 5
-        for key in ("params", "p16"):
+        assert got["steps"] == ref["steps"] == 6
+        for key in ("params", "p16", "packed", "grid"):
             assert torch.equal(got[key], ref[key]), (mode, r, key, float((got[key].float() - ref[key].float()).abs().max()))
         assert torch.isfinite(got["params"]).all()
         g0 = out[(mode, 0)][0]
@@ -200,6 +207,7 @@ def _nccl_worker(rank, port, out):
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     from mfnerf import dp
+    dp.rehearse(True)  # a one-rank group skips its collectives unless rehearsing
     assert dist.get_backend() == "nccl"
     # the collectives' RCCL branches on device tensors
     x = torch.randn(4096, device=dev)

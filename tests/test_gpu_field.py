@@ -59,7 +59,9 @@ def test_mfma_f16_lane_maps(gpu):
 def _layouts():
     return [("lego_hash", (16, 2, 19, 16, LEGO_B, "Hash", 1)),
             ("small_T_hash", (8, 2, 10, 4, 8 ** (1 / 7), "Hash", 1)),
-            ("mixed_feature", (16, 2, 16, 16, LEGO_B, "MixedFeature", 4))]
+            ("mixed_feature", (16, 2, 16, 16, LEGO_B, "MixedFeature", 4)),
+            # --T 21 (opt.py:78): 10 x 1024 partitions, past the scatter's LDS-resident running counts
+            ("hash_T21", (16, 2, 21, 16, LEGO_B, "Hash", 1))]
 
 
 @pytest.mark.parametrize("name,args", _layouts())

@@ -28,6 +28,13 @@ GOLDEN = os.path.join(ROOT, "tests", "golden", "parity_train.json")
 # (Single logged losses are not compared: once the two trajectories part -- fp16 field vs fp32 --
 # one 256-ray batch's loss differs by ~30 % between equally good models.)
 LOSS_TOL_EPOCH = 0.10
+# the early window (steps <= 100, before the trajectories part): the pooled ratio within 1 +- this.
+# Both sides start from the same weights on the same batches, so the early losses differ only by the
+# fp16 field (~1e-3 relative per value) and the 2^-11 rounding of the table-gradient records
+# compounding over the first steps; a systematic gradient error of a few percent shows here first.
+EARLY_STEPS, LOSS_TOL_EARLY = 100, 0.02
+# where the protocol's numbers are written (per-seed diffs, mean, sd, bound, loss ratios)
+OUT = os.environ.get("MFNERF_PARITY_OUT", os.path.join(ROOT, "gpurun_out", "parity_train.json"))
 
 
 def _ngp(st, cfg):
@@ -92,9 +99,10 @@ def test_training_psnr_matches_reference(gpu):
     """Paired runs (same seeds on both sides).  ONE run's held-out PSNR still varies from seed to
     seed (0.16 dB sd over 8 seeds on this side at this protocol, tools/parity_spread.py; 0.65 dB
     without the schedule's decay), so the check is statistical: the mean over the K >= 8 seeds of
-    (ours - reference) must be within 0.2 dB plus two standard errors of that mean, and that bound
-    itself must stay <= 0.5 dB (a systematic 0.5-dB regression fails); every run must be finite,
-    skip no step, and track the reference's loss curve epoch by epoch over the whole run."""
+    (ours - reference) must be within 0.2 dB, and within 0.2 dB plus two standard errors of that
+    mean with that bound itself <= 0.35 dB; every run must be finite, skip no step, track the
+    reference's loss curve epoch by epoch over the whole run, and match it closely over the first
+    100 steps.  The numbers go to MFNERF_PARITY_OUT (JSON)."""
     refs = _reference_runs()
     assert len(refs) >= 8, "the protocol's reference side has fewer than 8 seeds"
     diffs, ours, theirs = [], [], []
@@ -123,8 +131,25 @@ def test_training_psnr_matches_reference(gpu):
         idx = [i for i, st in enumerate(steps) if e * PP.STEPS_PER_EPOCH < st <= (e + 1) * PP.STEPS_PER_EPOCH]
         if idx:
             ratios.append(sum(o[i] for o in ours for i in idx) / sum(t[i] for t in theirs for i in idx))
+    early = [i for i, st in enumerate(steps) if st <= EARLY_STEPS]
+    early_ratio = sum(o[i] for o in ours for i in early) / sum(t[i] for t in theirs for i in early)
+    early_dev = max(abs(o[i] / t[i] - 1) for o, t in zip(ours, theirs) for i in early)
     print(f"PARITY {k} seeds: mean(ours - reference) {mean:+.3f} dB, sd {sd:.3f}, bound {tol:.3f} dB; "
-          f"per-epoch loss ratio ours/reference {' '.join(f'{r:.3f}' for r in ratios)}")
-    assert tol <= 0.5, (diffs, tol)
+          f"per-epoch loss ratio ours/reference {' '.join(f'{r:.3f}' for r in ratios)}; "
+          f"steps <= {EARLY_STEPS}: pooled ratio {early_ratio:.4f}, largest single deviation {early_dev:.4f}")
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    with open(OUT, "w") as f:
+        json.dump({"protocol": {"seeds": k, "steps": PP.STEPS, "epochs": PP.EPOCHS, "n_rays": PP.N_RAYS,
+                                "n_test": PP.N_TEST, "early_steps": EARLY_STEPS},
+                   "seeds": [r["protocol"].get("run_seed", 0) for r in refs],
+                   "psnr_ours": [d + r["test_psnr"] for d, r in zip(diffs, refs)],
+                   "psnr_reference": [r["test_psnr"] for r in refs],
+                   "diffs_db": diffs, "mean_db": mean, "sd_db": sd, "bound_db": tol,
+                   "epoch_loss_ratios": ratios, "early_loss_ratio": early_ratio,
+                   "early_max_single_deviation": early_dev,
+                   "loss_steps": steps, "loss_ours": ours, "loss_reference": theirs}, f, indent=1)
+    assert tol <= 0.35, (diffs, tol)
+    assert abs(mean) <= 0.2, (diffs, mean)
     assert abs(mean) < tol, (diffs, tol)
     assert len(ratios) == PP.EPOCHS and all(abs(r - 1) < LOSS_TOL_EPOCH for r in ratios), ratios
+    assert abs(early_ratio - 1) < LOSS_TOL_EARLY, (early_ratio, early_dev)

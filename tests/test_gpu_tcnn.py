@@ -126,19 +126,25 @@ def test_module_route_matches_fused_field(gpu):
         assert float(torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0)) > 0.999
 
 
-def test_sh4_fw_kernel_matches_the_torch_restatement(gpu):
+def test_sh4_fw_kernel_matches_the_oracle(gpu):
     """mfnerf_sh4_fw (the tinycudann route's SphericalHarmonics degree 4, networks.py:60-67) against
-    sh4_torch, bit for bit, on directions mapped to [0, 1] as networks.py:145-146 does, including
-    the axis-aligned and diagonal extremes; and the Encoding module picks the kernel."""
+    the CPU oracle's sh4 (oracle/field_oracle.py, tcnn's published SH basis, one fp32 operation at a
+    time, rounded to fp16 once), bit for bit, on directions mapped to [0, 1] as networks.py:145-146
+    does, including the axis-aligned and diagonal extremes; the module's own torch restatement agrees
+    too; and the Encoding module picks the kernel."""
     from mfnerf import tcnn as T
+    from oracle import field_oracle as FO
     g = torch.Generator().manual_seed(5)
     d = torch.randn(100003, 3, generator=g)
     d = torch.cat([d, torch.eye(3), -torch.eye(3), torch.ones(1, 3), -torch.ones(1, 3)])
     d01 = (d / d.norm(dim=-1, keepdim=True) + 1) / 2
-    ref = T.sh4_torch(d01.to(gpu).float()).half()
+    oracle = FO.sh4(d01.float()).half()
     got = T.sh4_fw(d01.to(gpu))
     torch.cuda.synchronize()
     assert got.dtype == torch.float16 and got.shape == (d01.shape[0], 16)
+    bad = (got.cpu() != oracle).any(-1).nonzero().flatten()
+    assert bad.numel() == 0, (int(bad.numel()), d01[bad[:4]].tolist())
+    ref = T.sh4_torch(d01.to(gpu).float()).half()
     assert torch.equal(got, ref)
     enc = T.Encoding(3, {"otype": "SphericalHarmonics", "degree": 4})
     with torch.no_grad():

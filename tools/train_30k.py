@@ -18,6 +18,8 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "mf-nerf_amd")]
+# graph replays through the per-node launch path, as bench.py (before the HIP runtime initialises)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 import torch  # noqa: E402
 
 from mfnerf import data, synthetic  # noqa: E402
