@@ -204,6 +204,10 @@ def main():
     from mfnerf import dp, engine, synthetic
     if args.dp_rehearse:
         dp.rehearse(True)  # the one-rank group's collectives through RCCL (skipped otherwise)
+    # the exchange through a direct RCCL communicator on the step's stream, so the whole data-parallel
+    # step (collectives included) replays as one HIP graph (mfnerf/rccl.py); MFNERF_DIRECT_RCCL=0 keeps
+    # torch.distributed's collectives between two graphs per step
+    direct = dp_on and os.environ.get("MFNERF_DIRECT_RCCL", "1") == "1" and dp.use_direct_rccl()
 
     pre = dict(PRESETS[args.preset])
     if args.n_rays is not None:
@@ -330,6 +334,8 @@ def main():
                        "preset": args.preset, "global_batch": args.n_rays * world, "rm_s": round(mean_samples / args.n_rays, 2),
                        "parallelism": f"dp{world}" + ("-sharded-adam" if dp_on and args.dp == "shard" else "")
                        + ("-rehearsal" if args.dp_rehearse and world == 1 else ""),
+                       "exchange": (None if not dp_on else "rccl-direct, one graph per step" if direct
+                                    else "torch.distributed between graphs"),
                        "psnr": None},
             "roofline": {"bound": "hbm", "kernel": dom + " (" + "+".join(GRID_BW_KERNEL) + ")",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

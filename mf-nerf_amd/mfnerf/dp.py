@@ -40,6 +40,31 @@ def _host_staged(fn, *ts):
 _REHEARSE = os.environ.get("MFNERF_DP_REHEARSE", "0") == "1"
 
 
+# the direct RCCL communicator (mfnerf.rccl.Comm), when the backend is RCCL: collectives issued on the
+# caller's stream, hence capturable inside the step's HIP graph (TrainStep.capture: "dp_step")
+_COMM = None
+
+
+def use_direct_rccl(on=True):
+    """Route the exchange through a direct RCCL communicator (backend "nccl" only; a no-op
+    otherwise).  Returns whether it is in use."""
+    global _COMM
+    if not on:
+        if _COMM is not None:
+            _COMM.close()
+        _COMM = None
+        return False
+    if _COMM is None and _on() and dist.get_backend() == "nccl":
+        from .rccl import Comm
+        _COMM = Comm()
+    return _COMM is not None
+
+
+def direct_rccl():
+    """The direct communicator in use (or None)."""
+    return _COMM if _on() else None
+
+
 def rehearse(on=True):
     """Route the collectives through the backend even at world size 1 (measurement / tests)."""
     global _REHEARSE
@@ -55,6 +80,8 @@ def allreduce_mean_(flat):
     """In-place mean over ranks of one flat gradient tensor (one collective per step)."""
     if not _on():
         return flat
+    if _COMM is not None:
+        return _COMM.all_reduce_avg_(flat)
     if dist.get_backend() == "nccl":
         dist.all_reduce(flat, op=dist.ReduceOp.AVG)
     else:
@@ -72,24 +99,36 @@ def _world():
 
 
 def reduce_scatter_mean_(shard, flat):
-    """shard (flat.numel()/world,) <- this rank's slice of the mean over ranks of flat."""
+    """shard (flat.numel()/world,) <- this rank's slice of the mean over ranks of flat.  shard may be
+    flat's own slice [rank*k, (rank+1)*k) (in place: RCCL reduces into it where it lies, no copy)."""
     if not _on():
-        shard.copy_(flat)
+        if shard.data_ptr() != flat.data_ptr() + _rank() * shard.numel() * shard.element_size():
+            shard.copy_(flat[:shard.numel()])
         return shard
+    if _COMM is not None:
+        return _COMM.reduce_scatter_avg_(shard, flat)
     if dist.get_backend() == "nccl":
         dist.reduce_scatter_tensor(shard, flat, op=dist.ReduceOp.AVG)
     else:
-        def f(s_, x):
-            dist.reduce_scatter_tensor(s_, x, op=dist.ReduceOp.SUM)
-            s_.div_(dist.get_world_size())
-        _host_staged(f, shard, flat)
+        # host-staged: only the shard is written back (it may alias flat)
+        hx = flat.cpu() if flat.is_cuda else flat.clone()
+        hs = torch.empty(shard.shape, dtype=shard.dtype)
+        dist.reduce_scatter_tensor(hs, hx, op=dist.ReduceOp.SUM)
+        hs.div_(dist.get_world_size())
+        shard.copy_(hs)
     return shard
+
+
+def _rank():
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
 
 
 def all_gather_(full, rank):
     """full = concat over ranks of each rank's slice full[rank*k:(rank+1)*k] (in place)."""
     if not _on():
         return full
+    if _COMM is not None:
+        return _COMM.all_gather_(full)
     w = _world()
     k = full.numel() // w
     if dist.get_backend() == "nccl":  # in place: RCCL reads this rank's slice where it lies

@@ -354,7 +354,9 @@ class TrainStep:
         self.shard = (rank, lo, hi)
         self.m = torch.zeros(k, device=self.dev)
         self.v = torch.zeros(k, device=self.dev)
-        self.g_shard = torch.zeros(k, device=self.dev)
+        # this rank's slice of the gradient, reduced in place (RCCL in-place reduce-scatter: no
+        # second gradient-sized buffer, and a one-rank group's "reduction" is no copy)
+        self.g_shard = self.grads[lo:hi]
         self.graphs = None  # re-capture with the sharded update
 
     # ---------------------------------------------------------------- the step
@@ -777,6 +779,21 @@ class TrainStep:
                     self._adam(self.grads, 0, self.n_alloc, True)
             self.graphs["dp_pre"] = [cap(lambda j=j: dp_pre(j, signal_at or nomark)) for j in range(2)]
             self.graphs["dp_post"] = cap(dp_post)
+            from . import dp as _dp
+            if _dp.direct_rccl() is not None:
+                # RCCL on this stream (mfnerf.rccl): the collectives are captured too, and the whole
+                # data-parallel step (repack, chain, scatter, exchange, Adam, all-gather) replays as
+                # ONE graph -- no host hop between the backward and the update
+                def dp_step(j):
+                    dp_pre(j, signal_at or nomark)
+                    if self.shard is not None:
+                        _dp.reduce_scatter_mean_(self.g_shard, self.grads)
+                        dp_post()
+                        _dp.all_gather_(self.p16, self.shard[0])
+                    else:
+                        _dp.allreduce_mean_(self.grads)
+                        dp_post()
+                self.graphs["dp_step"] = [cap(lambda j=j: dp_step(j)) for j in range(2)]
         if self.shard is None and P == 1:
             tail = self._finish_update if self._fixed() else lambda: (self._grid_finish(0), self._update())
             self.graphs["finish_update"] = cap(tail)
@@ -798,7 +815,8 @@ class TrainStep:
                         self._grid_bw(self.mbuf[j], 0)
                         tail()
                 self.graphs["step"] = [cap(lambda j=j: step(j)) for j in range(2)]
-        if gated and signal_at.count != (4 if self.shard is None else 2):
+        n_gated = 2 * sum(1 for k in ("step", "dp_pre", "dp_step") if self.graphs.get(k) is not None)
+        if gated and signal_at.count != n_gated:
             # every gated graph must open the gate exactly once, or each gated march would spin for
             # GATE_TIMEOUT_US before starting
             raise RuntimeError(f"gated graphs signalled {signal_at.count} times")
@@ -901,6 +919,11 @@ class TrainStep:
             if not dp_mode:  # one graph for the step; the next march starts at its gate signal
                 g["step"][j].replay()
                 self._march_on_side(1 - j, next_batch, self._ev_start, gated=True, noise=next_noise)
+            elif g.get("dp_step") is not None and (self.shard is not None or exchange is dp.allreduce_mean_):
+                # the whole data-parallel step, collectives included, as one graph (direct RCCL)
+                g["dp_step"][j].replay()
+                self._march_on_side(1 - j, next_batch, self._ev_start, gated=True, noise=next_noise)
+                self._stale_pack = True  # the next step's graph starts with the repack
             else:
                 # [repack] chain, scatter, float gradient, flag -> collective -> Adam -> (all-gather)
                 g["dp_pre"][j].replay()

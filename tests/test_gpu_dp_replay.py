@@ -222,16 +222,22 @@ def _nccl_worker(rank, port, out):
     torch.cuda.synchronize()
     prims = (torch.equal(y, x), torch.equal(sh, x), torch.equal(z, x.half()), float(m) == 3.0)
     res = {}
-    for mode in ("shard", "allreduce"):
-        ex = dp.allreduce_mean_ if mode == "allreduce" else None
-        a = _step(dev, mode, 0, 1, _dataset(0, dev))
-        for _ in range(2):
-            a.run(exchange=ex)                     # eager: sharded_update / all-reduce over RCCL
-        a.capture()
-        for _ in range(3):
-            a.replay(exchange=ex)                  # dp_pre -> RCCL -> dp_post
-        torch.cuda.synchronize()
-        res[mode] = _state(a)
+    for direct in (False, True):
+        # torch.distributed's RCCL collectives between two graphs, then the direct communicator
+        # (mfnerf/rccl.py) whose collectives are captured: the step as one graph ("dp_step")
+        assert dp.use_direct_rccl(direct) == direct
+        for mode in ("shard", "allreduce"):
+            ex = dp.allreduce_mean_ if mode == "allreduce" else None
+            a = _step(dev, mode, 0, 1, _dataset(0, dev))
+            for _ in range(2):
+                a.run(exchange=ex)                     # eager: sharded_update / all-reduce over RCCL
+            a.capture()
+            assert (a.graphs.get("dp_step") is not None) == direct
+            for _ in range(3):
+                a.replay(exchange=ex)                  # dp_pre -> RCCL -> dp_post, or dp_step
+            torch.cuda.synchronize()
+            res[(mode, direct)] = _state(a)
+    dp.use_direct_rccl(False)
     ref = _step(dev, "none", 0, 1, _dataset(0, dev))  # no process group involved in its step
     for _ in range(5):
         ref.run()
@@ -243,7 +249,8 @@ def _nccl_worker(rank, port, out):
 def test_rccl_one_rank_matches_single_process():
     """init_process_group('nccl') at world size 1 on the one GPU: allreduce_mean_, reduce_scatter_mean_,
     all_gather_ and allreduce_max_ take their RCCL branches (identity at one rank); two eager and
-    three replayed DP steps in both modes leave the parameters bit-identical to five plain
+    three replayed DP steps in both modes, through torch.distributed and through the direct RCCL
+    communicator captured in the step graph, leave the parameters bit-identical to five plain
     single-process steps on the same draws."""
     out = mp.Manager().dict()
     mp.spawn(_nccl_worker, args=(_port(), out), nprocs=1, join=True)

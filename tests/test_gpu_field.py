@@ -533,3 +533,44 @@ def test_grid_encode_bw_fixed_point_shared_tables(gpu):
             elif scale > 0:
                 err = float((got[a:b] - gref[a:b]).abs().max()) / scale
                 assert err < 1e-4, (off, err)
+
+
+@pytest.mark.parametrize("name,args", [_layouts()[0], _layouts()[2], _layouts()[3]])
+@pytest.mark.parametrize("halves", ["1", "2"])
+def test_staged_accumulate_matches_per_slot_form(gpu, name, args, halves, monkeypatch):
+    """The staged partition accumulate (records compacted into an LDS list per round, every lane
+    busy; MFNERF_ACCUM=1, the default for PAIR layouts) and the per-slot form (MFNERF_ACCUM=0) add
+    the same integers: bit-identical table gradients, on training-shaped rays and with slots sized
+    far below the count (records past the slots through the overflow words) -- with the scatter as
+    one workgroup per unit or two (table halves, MFNERF_SCATTER_HALVES=2), each within the record
+    bound of the fp64 oracle."""
+    lay, olay = GridLayout(*args), FO.GridLayout(*args)
+    g = torch.Generator().manual_seed(41)
+    R, S = 900, 80
+    o = torch.rand(R, 1, 3, generator=g) * 0.6 + 0.2
+    d = torch.nn.functional.normalize(torch.randn(R, 1, 3, generator=g), dim=-1)
+    x = (o + d * (torch.arange(S).view(1, S, 1) * (3 ** 0.5 / 1024))).clamp(0, 1).reshape(-1, 3).contiguous()
+    N = x.shape[0]
+    dy = torch.randn(N, 2 * lay.L, generator=g) * 1e-3
+    tp = torch.zeros(lay.n_params).requires_grad_(True)
+    (FO.grid_encode(x, tp, olay).double() * dy.double()).sum().backward()
+    gref = tp.grad.double()
+    gabs = _abs_grad(x, dy, olay)
+    desc = lay.desc()
+    monkeypatch.setenv("MFNERF_SCATTER_HALVES", halves)
+    for ns in (N, N // 16):
+        out = []
+        for mode in ("0", "1"):
+            monkeypatch.setenv("MFNERF_ACCUM", mode)
+            gt = torch.zeros(lay.n_params, device=gpu)
+            FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=FLD.grid_bw_binned_workspace(desc, ns, gpu),
+                               binned=True, n_slots=ns)
+            out.append(gt.cpu())
+        assert float(out[0].abs().max()) > 0
+        assert torch.equal(out[0], out[1]), (name, ns, int((out[0] != out[1]).sum()))
+        got = out[1].double()
+        cuts = sorted(set(2 * o for o in lay.offsets)) + [lay.n_params]  # one region per table
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            scale = float(gref[a:b].abs().max())
+            if scale > 0:
+                _assert_binned(got[a:b], gref[a:b], gabs[a:b], 2e-4 * scale, what=(name, halves, ns, a))

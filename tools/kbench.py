@@ -95,6 +95,8 @@ def main():
         "adam_partial": lambda: step._finish_update(partial=True),
         "pack": step._pack,
         "march": lambda: step._march(batch, mb, lambda _n: None),
+        # the occupancy refresh (every 16 steps in train.py:165-168) as the trainer replays it
+        "occupancy": lambda: step.update_density_grid(warmup=False),
     }
     names = sys.argv[1:] or list(stages)
     cnt = m.rays_a[:, 2]
