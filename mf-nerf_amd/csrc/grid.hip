@@ -1338,6 +1338,12 @@ __device__ __forceinline__ void accum_pair(unsigned long long* img, int mask, ui
     atomicAdd(&img[e1], pack2(fx * a, fx * b));
 }
 
+// a record of any layout (accum_pair for PAIR plans, accum_record otherwise)
+__device__ __forceinline__ void accum_any(unsigned long long* img, int mask, uint2 r, float k2, bool pair) {
+    if (pair) accum_pair(img, mask, r, k2, true);
+    else accum_record(img, mask, r, k2);
+}
+
 constexpr int ACC_THREADS = 512;
 // the staged accumulate (bin_accum_kernel<1>): a round's records (half of the partition's slots) are
 // first compacted into an LDS list, then added with every lane busy
@@ -1464,12 +1470,13 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
             }
         }
     } else {
-        // Staged (PAIR layouts): per round (slots [128 rho, 128 rho + 128), QF per half-wave), the
+        // Staged: per round (slots [128 rho, 128 rho + 128), QF per half-wave), the
         // records are compacted into an LDS list at their slot's offset (an exclusive scan of the
         // round's counts), then every thread adds list entries i, i + 512, ...: full lanes, no
         // per-slot branches.  Records past the list's capacity, or past a slot's 64th, are added
         // straight from registers.  Same integer sums (order-free).
         static_assert(QF * ACC_THREADS / 32 == UNITS / 2, "two rounds of 128 slots");
+        const bool pair = P.pair_ok != 0;  // (uniform) every record a pair record
         __shared__ uint2 stg[ACC_STAGE];
         __shared__ int soff[UNITS / 2 + 1];
         for (int rho = 0; rho < 2; ++rho) {
@@ -1506,7 +1513,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
                 const int o = soff[q * n_hw + hw] + hl;
                 if (hl < c[q]) {
                     if (o < ACC_STAGE) stg[o] = r[q];
-                    else accum_pair(img, mask, r[q], k2, true);
+                    else accum_any(img, mask, r[q], k2, pair);
                 }
             }
 #pragma unroll
@@ -1515,14 +1522,14 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
                 const int o = soff[q * n_hw + hw] + hl + 32;
                 if (hl + 32 < c[q]) {
                     if (o < ACC_STAGE) stg[o] = r2[q];
-                    else accum_pair(img, mask, r2[q], k2, true);
+                    else accum_any(img, mask, r2[q], k2, pair);
                 }
-                for (int k = hl + 64; k < c[q]; k += 32) accum_pair(img, mask, base[(int64_t)u * slot + k], k2, true);
+                for (int k = hl + 64; k < c[q]; k += 32) accum_any(img, mask, base[(int64_t)u * slot + k], k2, pair);
             }
             if (rho == 0) prefetch(hw + 128);  // the next round's loads fly while this round's list is added
             __syncthreads();
             const int ns = min(total, ACC_STAGE);
-            for (int i = threadIdx.x; i < ns; i += ACC_THREADS) accum_pair(img, mask, stg[i], k2, true);
+            for (int i = threadIdx.x; i < ns; i += ACC_THREADS) accum_any(img, mask, stg[i], k2, pair);
             __syncthreads();  // the list is rewritten by the next round
         }
     }
@@ -2138,10 +2145,10 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
         if (adam) A = *adam;
         AdamRest X{};
         if (rest) X = *rest;
-        // the staged accumulate for PAIR layouts (MFNERF_ACCUM=0: the per-slot form, any layout)
+        // the staged accumulate (MFNERF_ACCUM=0: the per-slot form)
         const char* acc_env = getenv("MFNERF_ACCUM");  // (read per call: tests compare both forms)
         const int acc_mode = acc_env ? atoi(acc_env) : 1;
-        auto ak = (P.pair_ok && acc_mode == 1) ? bin_accum_kernel<1> : bin_accum_kernel<0>;
+        auto ak = acc_mode == 1 ? bin_accum_kernel<1> : bin_accum_kernel<0>;
         hipLaunchKernelGGL(ak, dim3(P.n_bins + X.n_blocks), dim3(ACC_THREADS), 0, stream, P, n, n_dev,
                            W.rec, W.scnt, W.smax, W.ovf, W.ovw, (int*)grad_table, n_slots, *desc, level_l1, A, X,
                            (parts & 4) ? 1 : 0);
