@@ -394,6 +394,28 @@ int mfnerf_occupancy_cells_dev(const float* density_grid, int cascades, int grid
 int mfnerf_occupancy_update(float* density_grid, const float* sigmas, const int32_t* cell_idx, int64_t n_points,
                             int cascades, int grid_size, float decay, const float* count_grid, float density_threshold,
                             float* tmp, uint8_t* bitfield, void* workspace, mfnerf_stream_t stream);
+/* The same probe de-duplicated (what the engine's refresh runs): of all the draws above only one
+ * sigma per cell can reach the grid (`density_grid_tmp[c, indices] = ...`, networks.py:259, an
+ * index_put whose duplicate writes land in no defined order), so the draws only mark their cells and
+ * ONE jittered point is produced per distinct drawn cell -- keyed by (seed, call, cell) -- in ascending
+ * cell order (morton within a cascade); *count_dev receives their number (<= the capacity
+ * mfnerf_occupancy_points_unique(...)).  The set of probed cells is exactly the set the plain call
+ * with the same seed and call index draws.  Deterministic.  The workspace must be zero-filled before
+ * its first use (the call leaves its byte map zeroed); cascades*G^3 must be a multiple of 16.
+ * mfnerf_occupancy_update_dev: mfnerf_occupancy_update over the first min(n_points, *n_dev) points. */
+int64_t mfnerf_occupancy_points_unique(int cascades, int grid_size, int64_t n_uniform, int warmup);
+int mfnerf_occupancy_cells_unique(const float* density_grid, int cascades, int grid_size, float scale,
+                                  int64_t n_uniform, int warmup, float density_threshold, uint64_t seed,
+                                  uint64_t call_index, float* xyzs, int32_t* cell_idx, int32_t* count_dev,
+                                  void* workspace, mfnerf_stream_t stream);
+int mfnerf_occupancy_cells_unique_dev(const float* density_grid, int cascades, int grid_size, float scale,
+                                      int64_t n_uniform, int warmup, float density_threshold, uint64_t seed,
+                                      uint64_t* call_index_dev, float* xyzs, int32_t* cell_idx, int32_t* count_dev,
+                                      void* workspace, mfnerf_stream_t stream);
+int mfnerf_occupancy_update_dev(float* density_grid, const float* sigmas, const int32_t* cell_idx, int64_t n_points,
+                                const int32_t* n_dev, int cascades, int grid_size, float decay, const float* count_grid,
+                                float density_threshold, float* tmp, uint8_t* bitfield, void* workspace,
+                                mfnerf_stream_t stream);
 
 /* ---------------------------------------------------------------- training batch */
 

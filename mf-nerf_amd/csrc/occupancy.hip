@@ -124,47 +124,159 @@ struct PointsArgs {
     const uint64_t* call_dev;  // non-null: key from the device-resident call index (graph replays)
 };
 
-// networks.py:253-258: s = min(2^(c-1), scale); x = (coords/(G-1)*2-1)*(s - s/G) + (2u-1)*(s/G)
+// draw p's cell: cascade c, morton m; ok = false for an occupied draw from an empty set
+__device__ __forceinline__ void draw_cell(const PointsArgs& a, const int32_t* __restrict__ list,
+                                          const int32_t* __restrict__ counts, int64_t p, int& c, uint32_t& m,
+                                          bool& ok) {
+    c = (int)(p / a.per_cascade);
+    const int64_t j = p - (int64_t)c * a.per_cascade;
+    ok = true;
+    if (a.warmup) {
+        m = (uint32_t)j;
+    } else if (j < a.n_uniform) {
+        const uint32_t cx = rnd_below(a.key, 8 * (uint64_t)p + 0, a.G);
+        const uint32_t cy = rnd_below(a.key, 8 * (uint64_t)p + 1, a.G);
+        const uint32_t cz = rnd_below(a.key, 8 * (uint64_t)p + 2, a.G);
+        m = morton3(cx, cy, cz);
+    } else {
+        const int cnt = counts[c];
+        ok = cnt > 0;  // empty occupied set: the reference draws no such cells
+        m = ok ? (uint32_t)list[(int64_t)c * a.cells + rnd_below(a.key, 8 * (uint64_t)p + 3, (uint32_t)cnt)] : 0u;
+    }
+}
+
+// networks.py:253-258: s = min(2^(c-1), scale); x = (coords/(G-1)*2-1)*(s - s/G) + (2u-1)*(s/G);
+// u from counters ctr + k of `key`
+__device__ __forceinline__ void cell_point(const PointsArgs& a, int c, uint32_t m, uint64_t key, uint64_t ctr,
+                                           float* __restrict__ out) {
+    const float s = fminf(ldexpf(1.0f, c - 1), a.scale);
+    const float hgs = s / (float)a.G;
+    const float span = s - hgs;
+    const float inv = (float)(a.G - 1);
+    const uint32_t q[3] = {morton3_invert(m), morton3_invert(m >> 1), morton3_invert(m >> 2)};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float base = ((float)q[k] / inv * 2.0f - 1.0f) * span;
+        const float u = rnd_unit(key, ctr + k);
+        out[k] = base + (u * 2.0f - 1.0f) * hgs;
+    }
+}
+
 __global__ __launch_bounds__(OCC_BLOCK) void occ_points_kernel(PointsArgs a, const int32_t* __restrict__ list,
                                                                const int32_t* __restrict__ counts,
                                                                float* __restrict__ xyzs, int32_t* __restrict__ cell) {
     const int64_t n = (int64_t)a.cascades * a.per_cascade;
     if (a.call_dev) a.key = splitmix64_host(splitmix64_host(a.seed ^ OCC_SEED_MIX) ^ *a.call_dev);
     for (int64_t p = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; p < n; p += (int64_t)gridDim.x * OCC_BLOCK) {
-        const int c = (int)(p / a.per_cascade);
-        const int64_t j = p - (int64_t)c * a.per_cascade;
+        int c;
         uint32_t m;
-        bool ok = true;
-        if (a.warmup) {
-            m = (uint32_t)j;
-        } else if (j < a.n_uniform) {
-            const uint32_t cx = rnd_below(a.key, 8 * (uint64_t)p + 0, a.G);
-            const uint32_t cy = rnd_below(a.key, 8 * (uint64_t)p + 1, a.G);
-            const uint32_t cz = rnd_below(a.key, 8 * (uint64_t)p + 2, a.G);
-            m = morton3(cx, cy, cz);
-        } else {
-            const int cnt = counts[c];
-            ok = cnt > 0;  // empty occupied set: the reference draws no such cells
-            m = ok ? (uint32_t)list[(int64_t)c * a.cells + rnd_below(a.key, 8 * (uint64_t)p + 3, (uint32_t)cnt)] : 0u;
-        }
-        const float s = fminf(ldexpf(1.0f, c - 1), a.scale);
-        const float hgs = s / (float)a.G;
-        const float span = s - hgs;
-        const float inv = (float)(a.G - 1);
-        const uint32_t q[3] = {morton3_invert(m), morton3_invert(m >> 1), morton3_invert(m >> 2)};
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const float base = ((float)q[k] / inv * 2.0f - 1.0f) * span;
-            const float u = rnd_unit(a.key, 8 * (uint64_t)p + 4 + k);
-            xyzs[3 * p + k] = base + (u * 2.0f - 1.0f) * hgs;
-        }
+        bool ok;
+        draw_cell(a, list, counts, p, c, m, ok);
+        cell_point(a, c, m, a.key, 8 * (uint64_t)p + 4, xyzs + 3 * p);
         cell[p] = ok ? (int32_t)((int64_t)c * a.cells + m) : -1;
+    }
+}
+
+// ---- the de-duplicated draw (mfnerf_occupancy_cells_unique*): the reference probes every draw and
+// keeps one sigma per cell (`density_grid_tmp[c, indices] = sigmas`, an index_put whose duplicate
+// writes land in no defined order), so only one jittered point per DISTINCT drawn cell can reach the
+// grid.  The draws only mark their cells in a byte map (idempotent plain stores, no atomics); the map
+// is compacted in ascending cell order (morton within a cascade: spatially coherent points for the
+// encode) and each marked cell gets one uniform jitter keyed by (call, cell).  Same distribution as
+// the reference's update -- the set of drawn cells, one uniform point per cell -- with ~60 % of the
+// points at a trained scene's occupancy, and deterministic (no write race on duplicates).
+__global__ __launch_bounds__(OCC_BLOCK) void occ_mark_kernel(PointsArgs a, const int32_t* __restrict__ list,
+                                                             const int32_t* __restrict__ counts,
+                                                             uint8_t* __restrict__ mark) {
+    const int64_t n = (int64_t)a.cascades * a.per_cascade;
+    if (a.call_dev) a.key = splitmix64_host(splitmix64_host(a.seed ^ OCC_SEED_MIX) ^ *a.call_dev);
+    for (int64_t p = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; p < n; p += (int64_t)gridDim.x * OCC_BLOCK) {
+        int c;
+        uint32_t m;
+        bool ok;
+        draw_cell(a, list, counts, p, c, m, ok);
+        if (ok) mark[(int64_t)c * a.cells + m] = 1;
+    }
+}
+
+// marked cells per 4096-cell block (16 bytes of the map per thread)
+__global__ __launch_bounds__(OCC_BLOCK) void occ_mark_count_kernel(const uint8_t* __restrict__ mark, int64_t total,
+                                                                   int32_t* __restrict__ block_counts) {
+    __shared__ int lds[OCC_BLOCK / 64];
+    const int64_t i0 = (int64_t)blockIdx.x * OCC_CELLS_PER_BLOCK + threadIdx.x * OCC_PER_THREAD;  // total % 16 == 0
+    int k = 0;
+    if (i0 < total) {
+        const uint4 v = *reinterpret_cast<const uint4*>(mark + i0);  // marks are 0 / 1
+        k = __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+    }
+    k = block_sum(k, lds);
+    if (threadIdx.x == 0) block_counts[blockIdx.x] = k;
+}
+
+// the marked cells in ascending order into list (their count into *count), the map zeroed behind
+__global__ __launch_bounds__(OCC_BLOCK) void occ_mark_compact_kernel(uint8_t* __restrict__ mark, int64_t total,
+                                                                     const int32_t* __restrict__ block_counts,
+                                                                     int32_t* __restrict__ list,
+                                                                     int32_t* __restrict__ count) {
+    __shared__ int lds[OCC_BLOCK / 64];
+    __shared__ int wave_tot[OCC_BLOCK / 64];
+    const int b = blockIdx.x, nblk = gridDim.x;
+    int pre = 0;
+    for (int i = threadIdx.x; i < b; i += OCC_BLOCK) pre += block_counts[i];
+    pre = block_sum(pre, lds);
+    const int64_t i0 = (int64_t)b * OCC_CELLS_PER_BLOCK + threadIdx.x * OCC_PER_THREAD;
+    uint32_t bits = 0;
+    if (i0 < total) {
+        uint4* src = reinterpret_cast<uint4*>(mark + i0);
+        const uint4 v = *src;
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) bits |= ((w[k >> 2] >> (8 * (k & 3))) & 1u) << k;
+        if (bits) *src = make_uint4(0u, 0u, 0u, 0u);
+    }
+    const int mine = __popc(bits);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int incl = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) wave_tot[w] = incl;
+    __syncthreads();
+    int wpre = 0;
+    for (int i = 0; i < w; ++i) wpre += wave_tot[i];
+    int pos = pre + wpre + incl - mine;
+    while (bits) {
+        const int k = __ffs(bits) - 1;
+        bits &= bits - 1;
+        list[pos++] = (int32_t)(i0 + k);
+    }
+    if (b == nblk - 1 && threadIdx.x == OCC_BLOCK - 1) *count = pos;
+}
+
+// one jittered point per listed cell: counters 4..6 of the cell's own stream (key mixed apart from
+// the draws' key, so a cell's jitter is independent of which draws chose it)
+constexpr uint64_t OCC_JITTER_MIX = 0x632BE59BD9B4E019ull;
+__global__ __launch_bounds__(OCC_BLOCK) void occ_unique_points_kernel(PointsArgs a, const int32_t* __restrict__ list,
+                                                                      const int32_t* __restrict__ count,
+                                                                      float* __restrict__ xyzs,
+                                                                      int32_t* __restrict__ cell) {
+    if (a.call_dev) a.key = splitmix64_host(splitmix64_host(a.seed ^ OCC_SEED_MIX) ^ *a.call_dev);
+    const uint64_t jkey = splitmix64_host(a.key ^ OCC_JITTER_MIX);
+    const int64_t n = *count;
+    for (int64_t i = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * OCC_BLOCK) {
+        const int32_t f = list[i];
+        const int c = (int)(f / a.cells);
+        cell_point(a, c, (uint32_t)(f - (int64_t)c * a.cells), jkey, 8 * (uint64_t)f + 4, xyzs + 3 * i);
+        cell[i] = f;
     }
 }
 
 __global__ __launch_bounds__(OCC_BLOCK) void occ_scatter_kernel(const float* __restrict__ sigma,
                                                                 const int32_t* __restrict__ cell, int64_t n,
+                                                                const int32_t* __restrict__ n_dev,
                                                                 float* __restrict__ tmp) {
+    if (n_dev) n = min<int64_t>(n, (int64_t)*n_dev);
     for (int64_t p = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; p < n; p += (int64_t)gridDim.x * OCC_BLOCK) {
         const int32_t k = cell[p];
         if (k >= 0) tmp[k] = sigma[p];
@@ -237,6 +349,9 @@ struct Ws {
     int32_t* counts;
     int32_t* list;
     OccStats* stats;
+    uint8_t* mark;        // the de-duplicated draw's byte map (zero between calls)
+    int32_t* ulist;       // its distinct cells, ascending
+    int32_t* ublock;      // marked cells per 4096-cell block
 };
 int64_t ws_layout(int cascades, int G, char* base, Ws* w) {
     const int64_t cells = (int64_t)G * G * G;
@@ -247,11 +362,17 @@ int64_t ws_layout(int cascades, int G, char* base, Ws* w) {
     char* ct = take(4 * cascades);
     char* ls = take(4 * cascades * cells);
     char* sp = take(sizeof(OccStats));
+    char* mk = take(cascades * cells);
+    char* ul = take(4 * cascades * cells);
+    char* ub = take(4 * div_up<int64_t>(cascades * cells, OCC_CELLS_PER_BLOCK));
     if (w) {
         w->block_counts = (int32_t*)bc;
         w->counts = (int32_t*)ct;
         w->list = (int32_t*)ls;
         w->stats = (OccStats*)sp;
+        w->mark = (uint8_t*)mk;
+        w->ulist = (int32_t*)ul;
+        w->ublock = (int32_t*)ub;
     }
     return off;
 }
@@ -264,7 +385,12 @@ __global__ void occ_call_bump_kernel(uint64_t* call) {
 }
 int occupancy_cells_impl(const float* density_grid, int cascades, int grid_size, float scale, int64_t n_uniform,
                          int warmup, float density_threshold, uint64_t seed, uint64_t call_index, uint64_t* call_dev,
-                         float* xyzs, int32_t* cell_idx, void* workspace, mfnerf_stream_t stream);
+                         float* xyzs, int32_t* cell_idx, void* workspace, mfnerf_stream_t stream,
+                         int32_t* unique_count = nullptr);
+
+__global__ void occ_set_count_kernel(int32_t* count, int32_t v) {
+    if (threadIdx.x == 0) *count = v;
+}
 
 }  // namespace
 
@@ -288,6 +414,33 @@ int mfnerf_occupancy_cells(const float* density_grid, int cascades, int grid_siz
                                 call_index, nullptr, xyzs, cell_idx, workspace, stream);
 }
 
+int64_t mfnerf_occupancy_points_unique(int cascades, int grid_size, int64_t n_uniform, int warmup) {
+    const int64_t n = mfnerf_occupancy_points(cascades, grid_size, n_uniform, warmup);
+    const int64_t cells = (int64_t)cascades * grid_size * grid_size * grid_size;
+    return n < 0 ? -1 : (n < cells ? n : cells);
+}
+
+int mfnerf_occupancy_cells_unique(const float* density_grid, int cascades, int grid_size, float scale,
+                                  int64_t n_uniform, int warmup, float density_threshold, uint64_t seed,
+                                  uint64_t call_index, float* xyzs, int32_t* cell_idx, int32_t* count_dev,
+                                  void* workspace, mfnerf_stream_t stream) {
+    if (!count_dev) { mfn_set_error("occupancy_cells_unique: null count"); return MFN_ERR_INVALID; }
+    return occupancy_cells_impl(density_grid, cascades, grid_size, scale, n_uniform, warmup, density_threshold, seed,
+                                call_index, nullptr, xyzs, cell_idx, workspace, stream, count_dev);
+}
+
+int mfnerf_occupancy_cells_unique_dev(const float* density_grid, int cascades, int grid_size, float scale,
+                                      int64_t n_uniform, int warmup, float density_threshold, uint64_t seed,
+                                      uint64_t* call_index_dev, float* xyzs, int32_t* cell_idx, int32_t* count_dev,
+                                      void* workspace, mfnerf_stream_t stream) {
+    if (!call_index_dev || !count_dev) { mfn_set_error("occupancy_cells_unique_dev: null pointer"); return MFN_ERR_INVALID; }
+    const int st = occupancy_cells_impl(density_grid, cascades, grid_size, scale, n_uniform, warmup, density_threshold,
+                                        seed, 0, call_index_dev, xyzs, cell_idx, workspace, stream, count_dev);
+    if (st) return st;
+    hipLaunchKernelGGL(occ_call_bump_kernel, dim3(1), dim3(64), 0, stream, call_index_dev);
+    return mfn_check_launch("occupancy_cells_unique_dev");
+}
+
 int mfnerf_occupancy_cells_dev(const float* density_grid, int cascades, int grid_size, float scale, int64_t n_uniform,
                                int warmup, float density_threshold, uint64_t seed, uint64_t* call_index_dev,
                                float* xyzs, int32_t* cell_idx, void* workspace, mfnerf_stream_t stream) {
@@ -304,7 +457,8 @@ int mfnerf_occupancy_cells_dev(const float* density_grid, int cascades, int grid
 namespace {
 int occupancy_cells_impl(const float* density_grid, int cascades, int grid_size, float scale, int64_t n_uniform,
                          int warmup, float density_threshold, uint64_t seed, uint64_t call_index, uint64_t* call_dev,
-                         float* xyzs, int32_t* cell_idx, void* workspace, mfnerf_stream_t stream) {
+                         float* xyzs, int32_t* cell_idx, void* workspace, mfnerf_stream_t stream,
+                         int32_t* unique_count) {
     if (bad_grid(cascades, grid_size)) { mfn_set_error("occupancy_cells: bad cascades/grid_size"); return MFN_ERR_INVALID; }
     if (n_uniform < 0 || (!warmup && n_uniform == 0)) { mfn_set_error("occupancy_cells: bad n_uniform"); return MFN_ERR_INVALID; }
     if (!density_grid || !xyzs || !cell_idx || !workspace) { mfn_set_error("occupancy_cells: null pointer"); return MFN_ERR_INVALID; }
@@ -331,8 +485,26 @@ int occupancy_cells_impl(const float* density_grid, int cascades, int grid_size,
     a.seed = seed;
     a.call_dev = call_dev;
     const int64_t n = (int64_t)cascades * a.per_cascade;
+    if (unique_count && !warmup) {
+        if (((int64_t)cascades * cells) % 16) {
+            mfn_set_error("occupancy_cells_unique: cascades * grid_size^3 must be a multiple of 16");
+            return MFN_ERR_INVALID;
+        }
+        // mark -> count -> compact (ascending, map re-zeroed) -> one point per distinct cell
+        const int64_t total = (int64_t)cascades * cells, ub = div_up<int64_t>(total, OCC_CELLS_PER_BLOCK);
+        hipLaunchKernelGGL(occ_mark_kernel, dim3(blocks_for(n)), dim3(OCC_BLOCK), 0, stream, a, w.list, w.counts, w.mark);
+        hipLaunchKernelGGL(occ_mark_count_kernel, dim3(ub), dim3(OCC_BLOCK), 0, stream, w.mark, total, w.ublock);
+        hipLaunchKernelGGL(occ_mark_compact_kernel, dim3(ub), dim3(OCC_BLOCK), 0, stream, w.mark, total, w.ublock, w.ulist,
+                           unique_count);
+        const int64_t cap = n < total ? n : total;
+        hipLaunchKernelGGL(occ_unique_points_kernel, dim3(blocks_for(cap)), dim3(OCC_BLOCK), 0, stream, a, w.ulist,
+                           unique_count, xyzs, cell_idx);
+        return mfn_check_launch("occupancy_cells_unique");
+    }
     hipLaunchKernelGGL(occ_points_kernel, dim3(blocks_for(n)), dim3(OCC_BLOCK), 0, stream, a, w.list, w.counts, xyzs,
                        cell_idx);
+    if (unique_count)  // warm-up: every cell once already
+        hipLaunchKernelGGL(occ_set_count_kernel, dim3(1), dim3(64), 0, stream, unique_count, (int32_t)n);
     return mfn_check_launch("occupancy_cells");
 }
 }  // namespace
@@ -342,6 +514,14 @@ extern "C" {
 int mfnerf_occupancy_update(float* density_grid, const float* sigmas, const int32_t* cell_idx, int64_t n_points,
                             int cascades, int grid_size, float decay, const float* count_grid, float density_threshold,
                             float* tmp, uint8_t* bitfield, void* workspace, mfnerf_stream_t stream) {
+    return mfnerf_occupancy_update_dev(density_grid, sigmas, cell_idx, n_points, nullptr, cascades, grid_size, decay,
+                                       count_grid, density_threshold, tmp, bitfield, workspace, stream);
+}
+
+int mfnerf_occupancy_update_dev(float* density_grid, const float* sigmas, const int32_t* cell_idx, int64_t n_points,
+                                const int32_t* n_dev, int cascades, int grid_size, float decay, const float* count_grid,
+                                float density_threshold, float* tmp, uint8_t* bitfield, void* workspace,
+                                mfnerf_stream_t stream) {
     if (bad_grid(cascades, grid_size)) { mfn_set_error("occupancy_update: bad cascades/grid_size"); return MFN_ERR_INVALID; }
     if (n_points < 0) { mfn_set_error("occupancy_update: bad n_points"); return MFN_ERR_INVALID; }
     if (!density_grid || !tmp || !bitfield || !workspace || (n_points && (!sigmas || !cell_idx))) {
@@ -354,7 +534,7 @@ int mfnerf_occupancy_update(float* density_grid, const float* sigmas, const int3
     (void)hipMemsetAsync(tmp, 0, n * sizeof(float), stream);
     if (n_points)
         hipLaunchKernelGGL(occ_scatter_kernel, dim3(blocks_for(n_points)), dim3(OCC_BLOCK), 0, stream, sigmas, cell_idx,
-                           n_points, tmp);
+                           n_points, n_dev, tmp);
     const int nb = (int)blocks_for(n, DECAY_BLOCKS);  // every partial written (grid-stride beyond)
     hipLaunchKernelGGL(occ_decay_kernel, dim3(nb), dim3(OCC_BLOCK), 0, stream, density_grid, tmp, count_grid, n,
                        decay, w.stats);

@@ -96,6 +96,11 @@ SIGNATURES = {
     "mfnerf_occupancy_cells": (_I, [_P, _I, _I, _F, _I64, _I, _F, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P]),
     "mfnerf_occupancy_cells_dev": (_I, [_P, _I, _I, _F, _I64, _I, _F, ctypes.c_uint64, _P, _P, _P, _P, _P]),
     "mfnerf_occupancy_update": (_I, [_P, _P, _P, _I64, _I, _I, _F, _P, _F, _P, _P, _P, _P]),
+    "mfnerf_occupancy_points_unique": (_I64, [_I, _I, _I64, _I]),
+    "mfnerf_occupancy_cells_unique": (_I, [_P, _I, _I, _F, _I64, _I, _F, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P,
+                                           _P, _P]),
+    "mfnerf_occupancy_cells_unique_dev": (_I, [_P, _I, _I, _F, _I64, _I, _F, ctypes.c_uint64, _P, _P, _P, _P, _P, _P]),
+    "mfnerf_occupancy_update_dev": (_I, [_P, _P, _P, _I64, _P, _I, _I, _F, _P, _F, _P, _P, _P, _P]),
     "mfnerf_sample_rays": (_I, [_P, _P, _P, _I64, _I64, _I64, _I, ctypes.c_uint64, _P, _P, _P, _P, _P]),
     "mfnerf_sample_rays_prep": (_I, [_P, _P, _P, _I64, _I64, _I64, _I, ctypes.c_uint64, _P, _P, _P, _P, _F, _P, _P,
                                      _P]),

@@ -996,7 +996,8 @@ class TrainStep:
         """Scratch for the refresh, sized for the warm-up (all cells) case, allocated once."""
         if getattr(self, "_occ", None) is None:
             lib, c, C, G = load(), self.cfg, self.cascades, self.G
-            n = max(lib.mfnerf_occupancy_points(C, G, G ** 3 // 4, 0), lib.mfnerf_occupancy_points(C, G, 0, 1))
+            # one point per distinct drawn cell (mfnerf_occupancy_cells_unique_dev): at most every cell
+            n = max(lib.mfnerf_occupancy_points_unique(C, G, G ** 3 // 4, 0), lib.mfnerf_occupancy_points(C, G, 0, 1))
             o = _State()
             o.n_max = n
             o.xyz = torch.empty(n, 3, dtype=torch.float32, device=self.dev)
@@ -1004,7 +1005,8 @@ class TrainStep:
             o.feat = torch.empty(c.L, n, c.F, dtype=torch.float16, device=self.dev)  # level planes
             o.sigma = torch.empty(n, dtype=torch.float32, device=self.dev)
             o.tmp = torch.empty(C * G ** 3, dtype=torch.float32, device=self.dev)
-            o.ws = torch.empty(lib.mfnerf_occupancy_workspace(C, G), dtype=torch.uint8, device=self.dev)
+            o.ws = torch.zeros(lib.mfnerf_occupancy_workspace(C, G), dtype=torch.uint8, device=self.dev)
+            o.count = torch.zeros(1, dtype=torch.int32, device=self.dev)  # probed (distinct) cells
             o.calls = torch.zeros(1, dtype=torch.int64, device=self.dev)  # the draws' call index (device)
             o.graphs = {}
             self._occ = o
@@ -1038,11 +1040,15 @@ class TrainStep:
         o = self._occ_buffers()
         thr = 0.01 * MAX_SAMPLES / SQRT3
         M = G ** 3 // 4
-        n = load().mfnerf_occupancy_points(C, G, M, int(warmup))
-        call("mfnerf_occupancy_cells_dev", ptr(self.density_grid), C, G, float(c.scale), M, int(warmup), thr, seed,
-             ptr(o.calls), ptr(o.xyz), ptr(o.cell), ptr(o.ws), s)
-        call("mfnerf_grid_encode_fw_planar", ptr(o.xyz), n, None, self.x_min, self.x_range, self.desc,
+        # the draws of sample_uniform_and_occupied_cells / get_all_cells reduced to one jittered point per
+        # distinct drawn cell (the only sigmas the grid can keep), in ascending cell order; count on the device
+        n = load().mfnerf_occupancy_points_unique(C, G, M, int(warmup))
+        call("mfnerf_occupancy_cells_unique_dev", ptr(self.density_grid), C, G, float(c.scale), M, int(warmup), thr,
+             seed, ptr(o.calls), ptr(o.xyz), ptr(o.cell), ptr(o.count), ptr(o.ws), s)
+        call("mfnerf_grid_encode_fw_planar", ptr(o.xyz), n, ptr(o.count), self.x_min, self.x_range, self.desc,
              ptr(self.p16[self.off_table:]), ptr(o.feat), o.n_max, s)
-        call("mfnerf_field_fw", ptr(o.feat), o.n_max, None, n, None, ptr(self.packed), c.rgb_width, 1, ptr(o.sigma), None, s)
-        call("mfnerf_occupancy_update", ptr(self.density_grid), ptr(o.sigma), ptr(o.cell), n, C, G, float(decay),
-             ptr(count_grid) if count_grid is not None else None, thr, ptr(o.tmp), ptr(self.bitfield), ptr(o.ws), s)
+        call("mfnerf_field_fw", ptr(o.feat), o.n_max, None, n, ptr(o.count), ptr(self.packed), c.rgb_width, 1,
+             ptr(o.sigma), None, s)
+        call("mfnerf_occupancy_update_dev", ptr(self.density_grid), ptr(o.sigma), ptr(o.cell), n, ptr(o.count), C, G,
+             float(decay), ptr(count_grid) if count_grid is not None else None, thr, ptr(o.tmp), ptr(self.bitfield),
+             ptr(o.ws), s)

@@ -141,6 +141,10 @@ def _one_rank_worker(rank, port, out):
             dp.all_gather_(full, 0)
         res.append((c.n, torch.equal(y, x), torch.equal(sh, x), torch.equal(full, x.half())))
     dp.rehearse(False)
+    # the direct RCCL communicator (captured collectives) exists only over an RCCL process group
+    dp.rehearse(True)
+    res.append(dp.use_direct_rccl())
+    dp.rehearse(False)
     out["r"] = res
     dist.destroy_process_group()
 
@@ -150,6 +154,7 @@ def test_one_rank_group_skips_collectives_unless_rehearsing():
     stage the flat gradient through host memory); dp.rehearse() routes them through the backend."""
     out = mp.Manager().dict()
     mp.spawn(_one_rank_worker, args=(_free_port(), out), nprocs=1, join=True)
-    (n_off, *ok_off), (n_on, *ok_on) = out["r"]
+    (n_off, *ok_off), (n_on, *ok_on), direct = out["r"]
+    assert direct is False
     assert n_off == 0 and all(ok_off)
     assert n_on == 3 and all(ok_on)

@@ -143,7 +143,8 @@ def test_update_no_positive_cell_clears_bitfield(gpu):
 
 def test_engine_refresh_end_to_end(gpu):
     """TrainStep.update_density_grid: warm-up then steady-state refreshes reproduce the restated
-    update from the points the device drew (sigma from the same fused field kernels)."""
+    update exactly from the points the device probed (one per distinct drawn cell, sigma from the
+    same fused field kernels) -- no duplicate cells, so no write-order ambiguity anywhere."""
     from mfnerf import engine, synthetic
     st = engine.TrainStep(engine.StepConfig(n_rays=512, log2_T=16), device=gpu, seed=0)
     st.set_occupancy(synthetic.ball_density_grid())
@@ -152,17 +153,57 @@ def test_engine_refresh_end_to_end(gpu):
         st.update_density_grid(warmup=warm)
         torch.cuda.synchronize()
         o = st._occ
-        n = load().mfnerf_occupancy_points(st.cascades, st.G, st.G ** 3 // 4, int(warm))
-        # duplicates may resolve to either sigma: only compare cells drawn once
+        n = int(o.count)
+        cap = load().mfnerf_occupancy_points_unique(st.cascades, st.G, st.G ** 3 // 4, int(warm))
+        assert 0 < n <= cap
         cell = o.cell[:n].cpu().long()
-        sig = o.sigma[:n].cpu()
-        ref_g, thr, _ = OO.update(before, sig, cell.int())
-        uniq, cnt = torch.unique(cell[cell >= 0], return_counts=True)
-        dup = torch.zeros(before.numel(), dtype=torch.bool)
-        dup[uniq[cnt > 1]] = True
-        got = st.density_grid.cpu().reshape(-1)
-        assert torch.equal(got[~dup], ref_g.reshape(-1)[~dup])
+        assert (cell[1:] > cell[:-1]).all()  # distinct, ascending
+        if warm:
+            assert n == st.cascades * st.G ** 3
+        ref_g, thr, ref_bf = OO.update(before, o.sigma[:n].cpu(), cell.int())
+        assert torch.equal(st.density_grid.cpu(), ref_g)
         assert OO.cell_points_ok(o.xyz[:n].cpu(), cell, st.cascades, st.G, st.cfg.scale)
+
+
+def _cells_unique(gpu, grid, C, G, scale, M, warmup, ws, seed=0, call_index=0, thr=THR):
+    lib = load()
+    n = lib.mfnerf_occupancy_points_unique(C, G, M, int(warmup))
+    xyz = torch.empty(n, 3, device=gpu)
+    cell = torch.empty(n, dtype=torch.int32, device=gpu)
+    cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
+    call("mfnerf_occupancy_cells_unique", ptr(grid), C, G, scale, M, int(warmup), thr, seed, call_index, ptr(xyz),
+         ptr(cell), ptr(cnt), ptr(ws), stream())
+    torch.cuda.synchronize()
+    k = int(cnt)
+    return xyz[:k].cpu(), cell[:k].cpu()
+
+
+@pytest.mark.parametrize("C,G,scale", [(1, 128, 0.5), (2, 32, 1.0)])
+def test_unique_draw_probes_each_drawn_cell_once(gpu, C, G, scale):
+    """mfnerf_occupancy_cells_unique: exactly the distinct cells the plain draw (same seed, call index)
+    draws, ascending, one point each inside its cell with the jitter spread over the cell; the byte
+    map is left zero (a repeat gives the same result); an empty occupied set adds no cell."""
+    g = torch.Generator().manual_seed(5)
+    grid = (torch.rand(C, G ** 3, generator=g) * 2 * THR - THR / 2).to(gpu)
+    M = G ** 3 // 4
+    _, plain, _ = _cells(gpu, grid, C, G, scale, M, False, seed=3, call_index=2)
+    ws = torch.zeros(load().mfnerf_occupancy_workspace(C, G), dtype=torch.uint8, device=gpu)
+    xyz, cell = _cells_unique(gpu, grid, C, G, scale, M, False, ws, seed=3, call_index=2)
+    want = torch.unique(plain[plain >= 0].long())
+    assert torch.equal(cell.long(), want)
+    assert cell.numel() < plain.numel()  # the duplicates are gone
+    assert OO.cell_points_ok(xyz, cell, C, G, scale)
+    ctr, half = OO.cell_centers(cell, C, G, scale)
+    assert ((xyz - ctr).abs() / half[:, None]).mean() > 0.4
+    xyz2, cell2 = _cells_unique(gpu, grid, C, G, scale, M, False, ws, seed=3, call_index=2)
+    assert torch.equal(cell2, cell) and torch.equal(xyz2, xyz)
+    # an empty occupied set: only the uniform draws' cells
+    _, plain0, _ = _cells(gpu, torch.zeros_like(grid), C, G, scale, M, False, seed=3, call_index=2)
+    _, cell0 = _cells_unique(gpu, torch.zeros_like(grid), C, G, scale, M, False, ws, seed=3, call_index=2)
+    assert torch.equal(cell0.long(), torch.unique(plain0[plain0 >= 0].long()))
+    # warm-up: every cell, in order
+    _, cw = _cells_unique(gpu, grid, C, G, scale, M, True, ws)
+    assert torch.equal(cw.long(), torch.arange(C * G ** 3))
 
 
 def test_consecutive_refreshes_draw_independent_cells(gpu):
