@@ -286,13 +286,22 @@ __global__ __launch_bounds__(OCC_BLOCK) void occ_scatter_kernel(const float* __r
 // The mean over positive cells: each decay workgroup writes its partial (sum, count); the
 // threshold kernel adds the partials in workgroup order (deterministic; round 2 added them with two
 // memory-side atomics per workgroup on one address each: 4096 serialised atomics, ~55 us).
-constexpr int DECAY_BLOCKS = 256;
+constexpr int DECAY_BLOCKS = 1024;
 struct OccStats {
     double sum[DECAY_BLOCKS];
     unsigned long long count[DECAY_BLOCKS];
     float thr;
 };
 
+__device__ __forceinline__ float decay_cell(float v, float t, const float* __restrict__ count_grid, int64_t i,
+                                            float decay) {
+    if (v < 0.0f) return v;
+    float d = decay;
+    if (count_grid) d = clampf(powf(decay, 1.0f / count_grid[i]), 0.1f, 0.95f);  // erode (networks.py:262)
+    return fmaxf(v * d, t);
+}
+
+// four cells per thread per step (float4), every load of a thread's slice issued before the math
 __global__ __launch_bounds__(OCC_BLOCK) void occ_decay_kernel(float* __restrict__ grid, const float* __restrict__ tmp,
                                                               const float* __restrict__ count_grid, int64_t n,
                                                               float decay, OccStats* __restrict__ st) {
@@ -300,18 +309,23 @@ __global__ __launch_bounds__(OCC_BLOCK) void occ_decay_kernel(float* __restrict_
     __shared__ unsigned long long lds_u[OCC_BLOCK / 64];
     double s = 0.0;
     unsigned long long k = 0;
-    for (int64_t i = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * OCC_BLOCK) {
-        float v = grid[i];
-        if (!(v < 0.0f)) {
-            float d = decay;
-            if (count_grid) d = clampf(powf(decay, 1.0f / count_grid[i]), 0.1f, 0.95f);  // erode (networks.py:262)
-            v = fmaxf(v * d, tmp[i]);
-            grid[i] = v;
-        }
-        if (v > 0.0f) {
-            s += (double)v;
-            ++k;
-        }
+    float4* g4 = reinterpret_cast<float4*>(grid);
+    const float4* t4 = reinterpret_cast<const float4*>(tmp);
+    for (int64_t i = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; i < n / 4; i += (int64_t)gridDim.x * OCC_BLOCK) {
+        float4 v = g4[i];
+        const float4 t = t4[i];
+        v.x = decay_cell(v.x, t.x, count_grid, 4 * i, decay);
+        v.y = decay_cell(v.y, t.y, count_grid, 4 * i + 1, decay);
+        v.z = decay_cell(v.z, t.z, count_grid, 4 * i + 2, decay);
+        v.w = decay_cell(v.w, t.w, count_grid, 4 * i + 3, decay);
+        g4[i] = v;
+        const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (e[q] > 0.0f) {
+                s += (double)e[q];
+                ++k;
+            }
     }
     s = block_sum(s, lds_d);
     k = block_sum(k, lds_u);
