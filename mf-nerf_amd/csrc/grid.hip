@@ -145,6 +145,7 @@ __device__ __forceinline__ void planar_level(const mfnerf_grid_desc& D, const __
     const uint32_t size = D.size[l], res = D.res[l];
     const bool dense = D.table_kind[l] == 0 && (uint64_t)res * res * res <= size;
     const bool pow2 = (size & (size - 1)) == 0;
+    const bool quad = (reinterpret_cast<uintptr_t>(tab) & 15) == 0;  // 16-B gathers need an aligned level
     __half2 v[8];
     // The two x-corners of a (y,z) row are adjacent entries -- dense levels: idx+1 (one
     // unaligned 8-B load unless it wraps past the table end); hashed power-of-two levels
@@ -163,6 +164,16 @@ __device__ __forceinline__ void planar_level(const mfnerf_grid_desc& D, const __
             const bool lo = (i0 & 1) == 0;
             v[2 * yz] = *reinterpret_cast<const __half2*>(lo ? &u.x : &u.y);
             v[2 * yz + 1] = *reinterpret_cast<const __half2*>(lo ? &u.y : &u.x);
+        } else if (!dense && pow2 && quad && D.table_kind[l] == 0 && (L.g[0] & 3) == 1 && size >= 4) {
+            // x = 1 (mod 4): x + 1 = x ^ 3, so idx(x+1) = idx(x) ^ 3 -- both in the aligned 4-entry
+            // block of idx(x): one 16-B gather instead of two 4-B ones (the kernel is bound by
+            // per-lane gather requests, not bytes)
+            const uint4 u = *reinterpret_cast<const uint4*>(tab + (i0 & ~3u));
+            const uint32_t k0 = i0 & 3u, k1 = k0 ^ 3u;
+            const uint32_t a = k0 == 0 ? u.x : k0 == 1 ? u.y : k0 == 2 ? u.z : u.w;
+            const uint32_t b = k1 == 0 ? u.x : k1 == 1 ? u.y : k1 == 2 ? u.z : u.w;
+            v[2 * yz] = __builtin_bit_cast(__half2, a);
+            v[2 * yz + 1] = __builtin_bit_cast(__half2, b);
         } else {
             v[2 * yz] = tab[i0];
             v[2 * yz + 1] = tab[corner_index(D, l, L.g[0] + 1, gy, gz)];
