@@ -1125,7 +1125,9 @@ __global__ __launch_bounds__(SC_THREADS / NH) void bin_scatter_kernel(const floa
         return c;
     }();
     __shared__ int cursor[LCUR];  // running counts by the half's own bin index (t_lbin0)
-    __shared__ int hist[MAX_TBINS], toff[MAX_TBINS];
+    // per-level bin counts, double-buffered by level parity (a level's counts are read by the scan
+    // and cleared during its placement, while the next level counts into the other buffer)
+    __shared__ int hist2[2][MAX_TBINS], toff[MAX_TBINS];
     // per bin of the staged level: {index of the stage's first record of the bin in rec[] minus its
     // stage offset, the stage index its slot ends at} (one 8-B LDS read per stored record)
     __shared__ int2 gdst[2][MAX_TBINS];
@@ -1142,7 +1144,7 @@ __global__ __launch_bounds__(SC_THREADS / NH) void bin_scatter_kernel(const floa
         for (int t = hh; t < P.n_tables; t += NH)
             for (int b = P.t_bin0[t] + (int)threadIdx.x; b < P.t_bin0[t + 1]; b += 64)
                 if (P.t_lbin0[t] + b - P.t_bin0[t] >= LCUR) scnt[(int64_t)b * UNITS + u] = 0;
-    for (int b = threadIdx.x; b < MAX_TBINS; b += blockDim.x) hist[b] = 0;
+    for (int b = threadIdx.x; b < 2 * MAX_TBINS; b += blockDim.x) hist2[b >> 10][b & (MAX_TBINS - 1)] = 0;
     if (threadIdx.x < 2) s_total[threadIdx.x] = 0;
     __syncthreads();
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
@@ -1197,7 +1199,7 @@ __global__ __launch_bounds__(SC_THREADS / NH) void bin_scatter_kernel(const floa
                 // the record's |a|, |b| maxima as two packed u16 (fp16 bits order like the values)
                 auto rank = [&](int k, int lb, uint2 r) {
                     R[k].r = r;
-                    R[k].meta = (uint32_t)lb | ((uint32_t)atomicAdd(&hist[lb], 1) << 16);
+                    R[k].meta = (uint32_t)lb | ((uint32_t)atomicAdd(&hist2[par][lb], 1) << 16);
                     rmax2 = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(
                         __builtin_bit_cast(ushort2v, rmax2), __builtin_bit_cast(ushort2v, r.y & 0x7fff7fffu)));
                 };
@@ -1215,18 +1217,26 @@ __global__ __launch_bounds__(SC_THREADS / NH) void bin_scatter_kernel(const floa
             }
             store_prev();  // the previous level's sorted stage, beside this level's counting
             __syncthreads();
-            // scan (one wave): bins -> sorted tile offsets; a run's k-th record goes to slot position
-            // gdst + k; the counters are cleared for the next level
-            if (threadIdx.x < 64) {
-                // bins q * 64 + lane per round (consecutive lanes on consecutive LDS words: no bank
-                // conflicts), each round an integer DPP wave scan plus the rounds before it (round 2:
-                // 4 bins per lane at stride 4 -- 8-way conflicts -- and a ds_bpermute scan)
-                const int lane = threadIdx.x;
+            // scan: bins -> sorted tile offsets; a run's k-th record goes to slot position gdst + k.
+            // Chunk q of 64 bins (consecutive lanes on consecutive LDS words: no bank conflicts) is
+            // scanned by wave q % waves with an integer DPP wave scan; its carry (the bins of the
+            // chunks before it) is each lane's column sum over those chunks, reduced once -- the
+            // chunks in parallel instead of one wave walking them in turn (round 3: 2.1 k cycles of
+            // one wave per level while the others waited)
+            {
+                static_assert(MAX_TBINS == 1024, "hist2 indexing");
+                const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
                 const int per = (tb + 63) >> 6;
-                int carry = 0;
-                for (int q = 0; q < per; ++q) {
+                const int* hs = hist2[par];
+                for (int q = wv; q < per; q += TH / 64) {
+                    int col = 0;  // chunks before q are whole (q < per - 1 ... < tb)
+                    for (int q2 = 0; q2 < q; ++q2) col += hs[q2 * 64 + lane];
+                    col += dppz_i<0x111, 0xF>(col); col += dppz_i<0x112, 0xF>(col);
+                    col += dppz_i<0x114, 0xF>(col); col += dppz_i<0x118, 0xF>(col);
+                    col += dppz_i<0x142, 0xA>(col); col += dppz_i<0x143, 0xC>(col);
+                    const int carry = __builtin_amdgcn_readlane(col, 63);
                     const int lb = q * 64 + lane;
-                    const int c = lb < tb ? hist[lb] : 0;
+                    const int c = lb < tb ? hs[lb] : 0;
                     int x = c;
                     x += dppz_i<0x111, 0xF>(x); x += dppz_i<0x112, 0xF>(x);
                     x += dppz_i<0x114, 0xF>(x); x += dppz_i<0x118, 0xF>(x);
@@ -1242,14 +1252,14 @@ __global__ __launch_bounds__(SC_THREADS / NH) void bin_scatter_kernel(const floa
                                                   run + (int)slot - cu);
                         if (cl < LCUR) cursor[cl] = cu + c;
                         else *gc = cu + c;
-                        hist[lb] = 0;
                     }
-                    carry += __builtin_amdgcn_readlane(x, 63);
+                    if (q == per - 1 && lane == 63) s_total[par] = carry + x;
                 }
-                if (lane == 0) s_total[par] = carry;
             }
             __syncthreads();
-            // place: the records sorted by bin into the stage
+            // place: the records sorted by bin into the stage (and this level's counts cleared for
+            // the level after next, which counts into the same buffer)
+            for (int b = threadIdx.x; b < tb; b += TH) hist2[par][b] = 0;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 if (R[k].meta == ~0u) continue;
