@@ -1509,10 +1509,12 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
                 const int u = u0 + q * n_hw;
                 r2[q] = hl + 32 < c[q] ? base[(int64_t)u * slot + hl + 32] : make_uint2(0u, 0u);
             }
-            // the round's slot offsets: slot s = q * 16 + hw holds c[q] records (uniform in the half-wave)
+            // the round's slot offsets: slot s = q * 16 + hw stages its first min(c[q], 64) records
+            // (uniform in the half-wave; records past the 64th are added straight from memory, so
+            // they take no list positions -- the list has no holes)
             if (hl == 0) {
 #pragma unroll
-                for (int q = 0; q < QF; ++q) soff[q * n_hw + hw] = c[q];
+                for (int q = 0; q < QF; ++q) soff[q * n_hw + hw] = min(c[q], 64);
             }
             __syncthreads();
             if (threadIdx.x < 64) {  // one wave scans the 128 counts (2 per lane)
