@@ -66,30 +66,43 @@ def _bench_worker(rank, world, port, mode, out):
     torch.cuda.set_device(dev)
     ex = dp.allreduce_mean_ if mode == "allreduce" else None
     K = 5
-    # replayed, as bench.py: eager warm-up step, capture, replays (step 2 event-timed: per-stage graphs)
-    a = _step(dev, mode, rank, world, _dataset(rank, dev))
-    a.run(exchange=ex)
-    a.capture()
-    mk = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
-    for k in range(1, K):
-        a.replay(exchange=ex, grid_bw_events=(mk(), [mk()]) if k == 2 else None)
-    # the last replay deferred the repack to the next step's graph: an occupancy refresh and an eager
-    # step right after it must see the updated weights (they repack first)
+    xb = _batches(1, N_RAYS, dev)[0]  # an explicit batch for the eager step after the replays
+    xn = torch.rand(N_RAYS, generator=torch.Generator().manual_seed(rank + 11)).to(dev)
+
+    def replayed():
+        # as bench.py: eager warm-up step, capture, replays (step 2 event-timed: per-stage graphs);
+        # the last one-graph replay defers its MLP repack to the next step's graph
+        a = _step(dev, mode, rank, world, _dataset(rank, dev))
+        a.run(exchange=ex)
+        a.capture()
+        mk = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+        for k in range(1, K):
+            a.replay(exchange=ex, grid_bw_events=(mk(), [mk()]) if k == 2 else None)
+        return a
+
+    def eager():
+        b = _step(dev, mode, rank, world, _dataset(rank, dev))
+        for k in range(K):
+            b.run(exchange=ex)
+        return b
+
+    res = {}
+    # (1) an eager step right after the replays (it must repack first)
+    a, b = replayed(), eager()
+    a.run(xb, exchange=ex, noise=xn)
+    b.run(xb, exchange=ex, noise=xn)
+    torch.cuda.synchronize()
+    res["run"] = (_state(a), _state(b))
+    # (2) an occupancy refresh right after the replays: its density query runs the field on the
+    # packed weights, so the refreshed grid shows whether they were current
+    a, b = replayed(), eager()
     a.update_density_grid()
-    a.run(exchange=ex)
-    torch.cuda.synchronize()
-    got = _state(a)
-    got["grid"] = a.density_grid.cpu()
-    # eager DP steps on the same draws (the dataset's draw counter lives on the device)
-    b = _step(dev, mode, rank, world, _dataset(rank, dev))
-    for k in range(K):
-        b.run(exchange=ex)
     b.update_density_grid()
-    b.run(exchange=ex)
     torch.cuda.synchronize()
-    ref = _state(b)
-    ref["grid"] = b.density_grid.cpu()
-    out[(mode, rank)] = (got, ref)
+    sa, sb = _state(a), _state(b)
+    sa["grid"], sb["grid"] = a.density_grid.cpu(), b.density_grid.cpu()
+    res["refresh"] = (sa, sb)
+    out[(mode, rank)] = res
     dist.destroy_process_group()
 
 
@@ -103,13 +116,14 @@ def test_dp_replay_as_bench_matches_eager_dp(mode):
     out = mp.Manager().dict()
     mp.spawn(_bench_worker, args=(world, _port(), mode, out), nprocs=world, join=True)
     for r in range(world):
-        got, ref = out[(mode, r)]
-        assert got["steps"] == ref["steps"] == 6
-        for key in ("params", "p16", "packed", "grid"):
-            assert torch.equal(got[key], ref[key]), (mode, r, key, float((got[key].float() - ref[key].float()).abs().max()))
-        assert torch.isfinite(got["params"]).all()
-        g0 = out[(mode, 0)][0]
-        assert torch.equal(got["params"], g0["params"]) and torch.equal(got["p16"], g0["p16"])
+        for case, (got, ref) in out[(mode, r)].items():
+            assert got["steps"] == ref["steps"] == (6 if case == "run" else 5), (case, got["steps"], ref["steps"])
+            for key in ("params", "p16", "packed") + (("grid",) if case == "refresh" else ()):
+                assert torch.equal(got[key], ref[key]), (mode, r, case, key,
+                                                         float((got[key].float() - ref[key].float()).abs().max()))
+            assert torch.isfinite(got["params"]).all()
+            g0 = out[(mode, 0)][case][0]
+            assert torch.equal(got["params"], g0["params"]) and torch.equal(got["p16"], g0["p16"])
 
 
 def _batches(k, n2, dev):
