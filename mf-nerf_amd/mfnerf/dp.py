@@ -56,7 +56,12 @@ def use_direct_rccl(on=True):
         return False
     if _COMM is None and _on() and dist.get_backend() == "nccl":
         from .rccl import Comm
-        _COMM = Comm()
+        try:
+            _COMM = Comm()
+        except (OSError, RuntimeError) as e:  # e.g. no RCCL symbols: keep torch.distributed's collectives
+            import warnings
+            warnings.warn(f"direct RCCL communicator unavailable ({e}); using torch.distributed collectives")
+            _COMM = None
     return _COMM is not None
 
 

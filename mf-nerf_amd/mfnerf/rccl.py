@@ -70,10 +70,12 @@ class Comm:
         uid = _UniqueId()
         if self.rank == 0:
             _check(lib.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
-        box = [bytes(uid.internal) if self.rank == 0 else None]
+        # the raw 128 bytes (the c_char array field would stop at the first NUL byte)
+        box = [ctypes.string_at(ctypes.addressof(uid), 128) if self.rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
-        uid = _UniqueId()
-        ctypes.memmove(ctypes.addressof(uid), box[0], 128)
+        if len(box[0]) != 128:
+            raise RuntimeError("rccl.Comm: malformed unique id")
+        uid = _UniqueId.from_buffer_copy(box[0])
         self.comm = ctypes.c_void_p()
         torch.cuda.synchronize()
         _check(lib.ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, self.rank), "ncclCommInitRank")
