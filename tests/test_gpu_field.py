@@ -33,6 +33,25 @@ def _abs_grad(x, dy, olay):
     return ta.grad.double()
 
 
+def _table_unit_bound(x, dy, lay, olay):
+    """Per parameter: half the fixed-point unit of its table times the number of contributions it
+    receives -- the rounding of a partition summed at its table's own unit (a partition whose slot
+    overflowed: every contribution rounded once to 2^(e-30), the table's L1 < 2^e)."""
+    cnt = torch.zeros(olay.n_params // 2, dtype=torch.float64)
+    l1 = (dy.abs().double().view(dy.shape[0], lay.L, 2).sum(2)).sum(0)  # per level
+    for lv in FO._corners(x, olay):
+        for idx, _ in lv:
+            cnt += torch.bincount(idx, minlength=cnt.numel()).double()
+    bound = torch.zeros(olay.n_params // 2, dtype=torch.float64)
+    for l in range(lay.L):
+        t_l1 = float(sum(l1[k] for k in range(lay.L) if lay.offsets[k] == lay.offsets[l]))
+        if t_l1 > 0:
+            unit = 2.0 ** (math.frexp(t_l1)[1] - 30)
+            a, b = lay.offsets[l], lay.offsets[l] + lay.sizes[l]
+            bound[a:b] = 0.5 * unit * cnt[a:b]
+    return bound.repeat_interleave(2)
+
+
 def _assert_binned(got, gref, gabs, atol, rtol=0.0, what=None):
     """|got - ref| <= 2^-11 x (sum of |contributions|) + the fixed-point path's own tolerance."""
     got, gref = got.double(), gref.double()
@@ -569,8 +588,12 @@ def test_staged_accumulate_matches_per_slot_form(gpu, name, args, halves, monkey
         assert float(out[0].abs().max()) > 0
         assert torch.equal(out[0], out[1]), (name, ns, int((out[0] != out[1]).sum()))
         got = out[1].double()
+        # slots 16x too small: most partitions overflow and sum at their table's unit (the shared
+        # MixedFeature tables' unit follows the L1 of every level sharing them)
+        unit = _table_unit_bound(x, dy, lay, olay) if ns < N else torch.zeros(lay.n_params, dtype=torch.float64)
         cuts = sorted(set(2 * o for o in lay.offsets)) + [lay.n_params]  # one region per table
         for a, b in zip(cuts[:-1], cuts[1:]):
             scale = float(gref[a:b].abs().max())
             if scale > 0:
-                _assert_binned(got[a:b], gref[a:b], gabs[a:b], 2e-4 * scale, what=(name, halves, ns, a))
+                _assert_binned(got[a:b], gref[a:b], gabs[a:b], 2e-4 * scale + unit[a:b] * 1.0001,
+                               what=(name, halves, ns, a))
