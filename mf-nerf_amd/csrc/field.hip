@@ -868,6 +868,268 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
     }
 }
 
+// ---------------------------------------------------------------- cooperative backward (W = 64)
+// field_bw_kernel holds all 12 weight-gradient tiles in each wave (192 accumulator registers + ~170
+// for the chain): one wave per SIMD, nothing hides the chain's dependencies (PMC: waiting 56 % of
+// its cycles).  Here the 12 tiles are split over the workgroup's 4 waves -- 3 each, 48 accumulator
+// registers -- so a wave fits 256 registers and TWO workgroups share a CU (76 KB of LDS each: the
+// 44 fragments + 4 transpose images per wave), two waves per SIMD.  Each wave still runs the
+// forward and the data-gradient chain of its own 32-sample tile; the weight-gradient operands (the
+// transposed T chunks, t_put) are written stage by stage into the wave's 4 images, the workgroup
+// synchronises, and each wave accumulates ITS tiles of that stage over all four waves' sample tiles
+// (waves 0..3 in order: a fixed summation order, deterministic).  Tiles per wave:
+//   wave 0: dWr3[0], dWr2[0][0], dW2[0]      wave 2: dWr1[0], dWr2[1][0], dW1[0]
+//   wave 1: dWr3[1], dWr2[0][1], dW2[1]      wave 3: dWr1[1], dWr2[1][1], dW1[1]
+// Stages (images per wave): S1 dO, R2 x2 | S2 dR2 x2, R1 x2 | S3 dR1 x2, [SH;h] | S4 dh, Y1 x2 |
+// S5 dY1 x2, X; the chain's next MFMAs are issued between a stage's writes and its products.
+constexpr int COOP_SLOTS = 4;      // transpose images per wave live at once (stage 2)
+constexpr int COOP_BLOCKS = 512;   // two workgroups per CU (persistent)
+constexpr size_t COOP_LDS = (size_t)Geo<64>::N * FRAG_HALFS * 2 + (size_t)4 * COOP_SLOTS * TILE_BYTES;
+static_assert(COOP_LDS <= 80 * 1024, "two cooperative workgroups per CU");
+
+template <bool PLANAR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void field_bw_coop_kernel(
+    const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n,
+    const int32_t* __restrict__ n_dev, const _Float16* __restrict__ packed, const float* __restrict__ dL_dsigma,
+    const float* __restrict__ dL_drgb, float grad_scale, const float* __restrict__ scale_dev,
+    float* __restrict__ dL_dfeat, float* __restrict__ slab, int32_t* __restrict__ nonfinite, float* __restrict__ level_l1) {
+    constexpr int W = 64;
+    using G = Geo<W>;
+    constexpr int MT = G::MT;
+    constexpr int oR1 = N_XYZ_PARAMS, oR2 = oR1 + W * 32, oR3 = oR2 + W * W;
+    constexpr size_t IMG_OFF = (size_t)G::N * FRAG_HALFS * 2;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    _Float16* lds_base = reinterpret_cast<_Float16*>(smem);
+    load_frags_bw<W, 4>(lds_base, packed);
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform)
+    const int r = lane & 31, h = lane >> 5;
+    const float S = scale_dev ? *scale_dev : grad_scale, invS = 1.0f / S;
+    const f32x16 z = {};
+    f32x16 acc0 = z, acc1 = z, acc2 = z;  // this wave's three tiles (table above)
+    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
+    const int64_t tiles = div_up<int64_t>(nn, 32);
+    const int64_t groups = div_up<int64_t>(tiles, 4);  // group g = tiles 4g .. 4g+3, one per wave
+    struct BwIn { TileIn I; float gs, g0, g1, g2; bool live; };
+    BwIn nx;
+    // as field_bw_kernel: every lane loads (index clamped), the incoming gradients are zeroed where
+    // the sample is out of range or on lanes h == 1 -- an idle wave's tile contributes exact zeros
+    auto fetch = [&](int64_t tile, BwIn& o) {
+        const int64_t s = tile * 32 + r;
+        const bool v = s < nn && h == 0;
+        const int64_t sc = max<int64_t>(0, min<int64_t>(s, nn - 1));
+        if constexpr (PLANAR) {
+            const uint32_t* Pp = reinterpret_cast<const uint32_t*>(feat);
+            uint32_t u[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                u[k] = Pp[(int64_t)(4 * h + k) * plane_stride + sc];
+                u[4 + k] = Pp[(int64_t)(8 + 4 * h + k) * plane_stride + sc];
+            }
+            o.I.x[0] = *reinterpret_cast<const half8*>(&u[0]);
+            o.I.x[1] = *reinterpret_cast<const half8*>(&u[4]);
+        } else {
+            const half8* row = reinterpret_cast<const half8*>(feat + sc * 32);
+            o.I.x[0] = row[h];
+            o.I.x[1] = row[2 + h];
+        }
+        o.I.d[0] = dirs[3 * sc]; o.I.d[1] = dirs[3 * sc + 1]; o.I.d[2] = dirs[3 * sc + 2];
+        o.gs = dL_dsigma[sc]; o.g0 = dL_drgb[3 * sc]; o.g1 = dL_drgb[3 * sc + 1]; o.g2 = dL_drgb[3 * sc + 2];
+        o.live = v;
+    };
+    auto zero_grads = [&](BwIn& o) {
+        o.gs = o.live ? o.gs : 0.0f;
+        o.g0 = o.live ? o.g0 : 0.0f;
+        o.g1 = o.live ? o.g1 : 0.0f;
+        o.g2 = o.live ? o.g2 : 0.0f;
+    };
+    if ((int64_t)blockIdx.x < groups) fetch(4 * (int64_t)blockIdx.x + wid, nx);
+    bool bad = false;
+    float l1a[4] = {0.f, 0.f, 0.f, 0.f}, l1b[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t g = blockIdx.x; g < groups; g += gridDim.x) {
+        int opaque = 0;
+        asm volatile("" : "+s"(opaque));
+        const _Float16* lds = lds_base + opaque;
+        _Float16* area = lds_base + opaque + IMG_OFF / 2;
+        auto slot = [&](int u, int k) { return area + (u * COOP_SLOTS + k) * TILE_HALFS; };
+        auto put2 = [&](_Float16* sl, const half8* v) {  // a 32-channel tile as two perm chunks
+            t_put(sl, lane, v[0], 0, true);
+            t_put(sl, lane, v[1], 4, true);
+        };
+        // this wave's tile of the group; the next group's inputs are loaded while it computes
+        const int64_t tile = 4 * g + wid;
+        BwIn in = nx;
+        zero_grads(in);
+        fetch(4 * (g + (int64_t)gridDim.x) + wid, nx);  // (clamped past the end)
+        const bool valid = tile * 32 + r < nn;
+        FwdTile<W> T;
+        forward_tiles<W, false, 1>(lds, lane, &in.I, &valid, &T);
+        half8 dOb;
+        {
+            f32x16 dO = z;
+            dO[0] = in.g0 * S * T.rgb[0] * (1.0f - T.rgb[0]);
+            dO[1] = in.g1 * S * T.rgb[1] * (1.0f - T.rgb[1]);
+            dO[2] = in.g2 * S * T.rgb[2] * (1.0f - T.rgb[2]);
+            dOb = pack8<0, false>(dO);
+        }
+        //    dR2 = Wr3^T dO, masked by R2 > 0
+        half8 dr2p[MT][2];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const f32x16 a = mfma(lds_frag(lds, G::B5 + mt, lane), dOb, z);
+            dr2p[mt][0] = relu_mask8(pack8<0, false>(a), T.r2[mt][0]);
+            dr2p[mt][1] = relu_mask8(pack8<8, false>(a), T.r2[mt][1]);
+        }
+        // ---- S1: dO, R2 -> dWr3 (waves 0, 1)
+        t_put(slot(wid, 0), lane, dOb, 0, true);  // (channels 16..31 stale: rows 16..31 of dWr3, dropped)
+        put2(slot(wid, 1), T.r2[0]);
+        put2(slot(wid, 2), T.r2[1]);
+        __syncthreads();
+        if (wid < 2) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc_tile(acc0, s_get(slot(u, 0), lane), s_get(slot(u, 1 + wid), lane));
+        }
+        //    dR1 = Wr2^T dR2, masked by R1 > 0
+        half8 dr1p[MT][2];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            f32x16 a = z;
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) a = mfma(lds_frag(lds, G::B4 + mt * G::KC + t * 2 + k, lane), dr2p[t][k], a);
+            dr1p[mt][0] = relu_mask8(pack8<0, false>(a), T.r1[mt][0]);
+            dr1p[mt][1] = relu_mask8(pack8<8, false>(a), T.r1[mt][1]);
+        }
+        __syncthreads();
+        // ---- S2: dR2, R1 -> dWr2 (one tile per wave)
+        put2(slot(wid, 0), dr2p[0]);
+        put2(slot(wid, 1), dr2p[1]);
+        put2(slot(wid, 2), T.r1[0]);
+        put2(slot(wid, 3), T.r1[1]);
+        //    d[SH;h] = Wr1^T dR1 (rows 16..31 = dh) + TruncExp backward into h[0]
+        half8 dhb;
+        {
+            f32x16 dsh = z;
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) dsh = mfma(lds_frag(lds, G::B3 + t * 2 + k, lane), dr1p[t][k], dsh);
+            const float dh0 = in.gs * S * __expf(fminf(fmaxf(T.h0, -15.0f), 15.0f));
+            dsh[8] = h == 0 ? dsh[8] + dh0 : dsh[8];
+            dhb = pack8<8, false>(dsh);
+        }
+        __syncthreads();
+        {
+            const int o = wid >> 1, i = wid & 1;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc_tile(acc1, s_get(slot(u, o), lane), s_get(slot(u, 2 + i), lane));
+        }
+        //    dY1 = W2^T dh, masked by Y1 > 0; dX = W1^T dY1
+        half8 dy1p[2][2];
+        f32x16 dx = z;
+        {
+            const f32x16 a0 = mfma(lds_frag(lds, G::B2 + 0, lane), dhb, z);
+            const f32x16 a1 = mfma(lds_frag(lds, G::B2 + 1, lane), dhb, z);
+            dy1p[0][0] = relu_mask8(pack8<0, false>(a0), T.y1[0][0]);
+            dy1p[0][1] = relu_mask8(pack8<8, false>(a0), T.y1[0][1]);
+            dy1p[1][0] = relu_mask8(pack8<0, false>(a1), T.y1[1][0]);
+            dy1p[1][1] = relu_mask8(pack8<8, false>(a1), T.y1[1][1]);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) dx = mfma(lds_frag(lds, G::B1 + t * 2 + k, lane), dy1p[t][k], dx);
+        }
+        __syncthreads();
+        // ---- S3: dR1, [SH;h] -> dWr1 (waves 2, 3)
+        put2(slot(wid, 0), dr1p[0]);
+        put2(slot(wid, 1), dr1p[1]);
+        t_put(slot(wid, 2), lane, T.sh, 0, false);
+        t_put(slot(wid, 2), lane, T.hb, 4, true);
+        __syncthreads();
+        if (wid >= 2) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc_tile(acc0, s_get(slot(u, wid - 2), lane), s_get(slot(u, 2), lane));
+        }
+        // dX = W1^T dY1 -> global fp32 (features (i&3)+8(i>>2)+4h), this wave's own tile
+        {
+            const int64_t s = tile * 32 + r;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 o = make_float4(dx[4 * q] * invS, dx[4 * q + 1] * invS, dx[4 * q + 2] * invS, dx[4 * q + 3] * invS);
+                bad |= !(isfinite(o.x) && isfinite(o.y) && isfinite(o.z) && isfinite(o.w));
+                if (s < nn) reinterpret_cast<float4*>(dL_dfeat + s * 32)[2 * q + h] = o;
+                l1a[q] += fabsf(o.x) + fabsf(o.y);
+                l1b[q] += fabsf(o.z) + fabsf(o.w);
+            }
+        }
+        __syncthreads();
+        // ---- S4: dh, Y1 -> dW2 (waves 0, 1)
+        t_put(slot(wid, 0), lane, dhb, 0, true);  // (channels 16..31 stale: rows of dW2 dropped)
+        put2(slot(wid, 1), T.y1[0]);
+        put2(slot(wid, 2), T.y1[1]);
+        __syncthreads();
+        if (wid < 2) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc_tile(acc2, s_get(slot(u, 0), lane), s_get(slot(u, 1 + wid), lane));
+        }
+        __syncthreads();
+        // ---- S5: dY1, X -> dW1 (waves 2, 3)
+        put2(slot(wid, 0), dy1p[0]);
+        put2(slot(wid, 1), dy1p[1]);
+        t_put(slot(wid, 2), lane, T.x[0], 0, false);
+        t_put(slot(wid, 2), lane, T.x[1], 4, false);
+        __syncthreads();
+        if (wid >= 2) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc_tile(acc2, s_get(slot(u, wid - 2), lane), s_get(slot(u, 2), lane));
+        }
+        __syncthreads();  // the images are rewritten by the next group's S1
+    }
+    if (nonfinite && __any(bad) && lane == 0) atomicOr(nonfinite, 1);
+
+    // ---- epilogue: each tile stored by its owner wave (disjoint) -> one slab row per workgroup
+    float* row = slab + (int64_t)blockIdx.x * G::N_DW;
+    {
+        constexpr int N_IMG = G::N_DW;
+        static_assert((size_t)N_IMG * 4 + 64 <= IMG_OFF, "reduction image must fit the fragment area");
+        xdl_drain();
+        __syncthreads();
+        float* img = reinterpret_cast<float*>(smem);
+        float* l1_part = img + N_IMG;
+        if (threadIdx.x < 16) l1_part[threadIdx.x] = 0.0f;
+        __syncthreads();
+        if (level_l1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float a = l1a[q], b = l1b[q];
+#pragma unroll
+                for (int off = 16; off > 0; off >>= 1) { a += __shfl_xor(a, off, 64); b += __shfl_xor(b, off, 64); }
+                if (r == 0) { atomicAdd(l1_part + 4 * q + 2 * h, a); atomicAdd(l1_part + 4 * q + 2 * h + 1, b); }
+            }
+        }
+        if (wid == 0) {
+            dw_add32(img + oR3, acc0, 0, 0, 16, W, lane, true);
+            dw_add32(img + oR2, acc1, 0, 0, W, W, lane, true);
+            dw_add32(img + 64 * 32, acc2, 0, 0, 16, 64, lane, true);
+        } else if (wid == 1) {
+            dw_add32(img + oR3, acc0, 0, 1, 16, W, lane, true);
+            dw_add32(img + oR2, acc1, 0, 1, W, W, lane, true);
+            dw_add32(img + 64 * 32, acc2, 0, 1, 16, 64, lane, true);
+        } else if (wid == 2) {
+            dw_add32(img + oR1, acc0, 0, 0, W, 32, lane, true);
+            dw_add32(img + oR2, acc1, 1, 0, W, W, lane, true);
+            dw_add32(img, acc2, 0, 0, 64, 32, lane, true);
+        } else {
+            dw_add32(img + oR1, acc0, 1, 0, W, 32, lane, true);
+            dw_add32(img + oR2, acc1, 1, 1, W, W, lane, true);
+            dw_add32(img, acc2, 1, 0, 64, 32, lane, true);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < G::N_DW; i += blockDim.x) row[i] = img[i] * invS;
+        if (level_l1 && threadIdx.x < 16) atomicAdd(level_l1 + threadIdx.x, l1_part[threadIdx.x]);
+    }
+}
+
 // Second backward pass at W = 128: dWr2 (W x W) = sum over samples of dR2^T R1, with all 16 tiles in
 // registers.  Recomputes the forward and dR2 = relu'(R2) * Wr3^T dO (what field_bw_kernel does before
 // it), and writes the dWr2 segment of the same slab rows.
@@ -1025,6 +1287,17 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 
 constexpr int BW_BLOCKS = 256;  // one workgroup per CU (persistent)
 
+// W = 64 through field_bw_coop_kernel (two waves per SIMD) unless MFNERF_FIELD_BW_COOP=0; read once
+// per process (the workspace's slab rows and the deferred fold must agree with the kernel that ran)
+bool coop64() {
+    static const bool on = [] {
+        const char* e = getenv("MFNERF_FIELD_BW_COOP");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+int bw_rows(int w) { return (w == 64 && coop64()) ? COOP_BLOCKS : BW_BLOCKS; }
+
 bool width_ok(int w) { return w == 64 || w == 128; }
 
 int bad_width(int w) {
@@ -1060,6 +1333,29 @@ int launch_bw(const void* feat, int64_t ps, const float* dirs, int64_t n, const 
               float* grad_xyz, float* grad_rgb, void* workspace, int32_t* nonfinite, float* level_l1,
               mfnerf_stream_t stream) {
     using C = BwCfg<W, NW>;
+    if constexpr (W == 64) {
+        if (coop64()) {
+            static const hipError_t attr = [] {
+                const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_coop_kernel<false>),
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)COOP_LDS);
+                const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_coop_kernel<true>),
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)COOP_LDS);
+                return a0 != hipSuccess ? a0 : a1;
+            }();
+            if (attr != hipSuccess) {
+                mfn_set_error("field_bw: cannot raise the LDS limit to %d bytes", (int)COOP_LDS);
+                return MFN_ERR_INVALID;
+            }
+            auto k = ps > 0 ? field_bw_coop_kernel<true> : field_bw_coop_kernel<false>;
+            hipLaunchKernelGGL(k, dim3(COOP_BLOCKS), dim3(256), COOP_LDS, stream, (const _Float16*)feat, ps, dirs, n,
+                               n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb, grad_scale, scale_dev, dL_dfeat,
+                               (float*)workspace, nonfinite, level_l1);
+            if (grad_xyz)
+                hipLaunchKernelGGL(slab_reduce_kernel<W>, dim3((Geo<W>::N_DW + 63) / 64), dim3(256), 0, stream,
+                                   (const float*)workspace, COOP_BLOCKS, grad_xyz, grad_rgb, nonfinite);
+            return MFN_OK;
+        }
+    }
     if constexpr (C::LDS > 65536) {  // more than the default dynamic-LDS limit
         static const hipError_t attr = [] {
             const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_kernel<W, NW, false>),
@@ -1149,7 +1445,7 @@ int mfnerf_field_fw(const void* feat_f16, int64_t feat_plane_stride, const float
 
 int64_t mfnerf_field_bw_workspace(int64_t n, int rgb_width) {
     (void)n;
-    if (rgb_width == 64) return (int64_t)BW_BLOCKS * Geo<64>::N_DW * 4;
+    if (rgb_width == 64) return (int64_t)bw_rows(64) * Geo<64>::N_DW * 4;
     if (rgb_width == 128) return (int64_t)BW_BLOCKS * Geo<128>::N_DW * 4;
     return -1;
 }
@@ -1187,7 +1483,7 @@ int mfnerf_field_bw_reduce(int rgb_width, const void* workspace, float* grad_xyz
     if (!workspace || !grad_xyz || !grad_rgb) { mfn_set_error("field_bw_reduce: null pointer"); return MFN_ERR_INVALID; }
     if (rgb_width == 64)
         hipLaunchKernelGGL(slab_reduce_kernel<64>, dim3((Geo<64>::N_DW + 63) / 64), dim3(256), 0, stream,
-                           (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
+                           (const float*)workspace, bw_rows(64), grad_xyz, grad_rgb, nonfinite);
     else
         hipLaunchKernelGGL(slab_reduce_kernel<128>, dim3((Geo<128>::N_DW + 63) / 64), dim3(256), 0, stream,
                            (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
