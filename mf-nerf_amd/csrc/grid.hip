@@ -145,7 +145,6 @@ __device__ __forceinline__ void planar_level(const mfnerf_grid_desc& D, const __
     const uint32_t size = D.size[l], res = D.res[l];
     const bool dense = D.table_kind[l] == 0 && (uint64_t)res * res * res <= size;
     const bool pow2 = (size & (size - 1)) == 0;
-    const bool quad = (reinterpret_cast<uintptr_t>(tab) & 15) == 0;  // 16-B gathers need an aligned level
     __half2 v[8];
     // The two x-corners of a (y,z) row are adjacent entries -- dense levels: idx+1 (one
     // unaligned 8-B load unless it wraps past the table end); hashed power-of-two levels
@@ -164,16 +163,6 @@ __device__ __forceinline__ void planar_level(const mfnerf_grid_desc& D, const __
             const bool lo = (i0 & 1) == 0;
             v[2 * yz] = *reinterpret_cast<const __half2*>(lo ? &u.x : &u.y);
             v[2 * yz + 1] = *reinterpret_cast<const __half2*>(lo ? &u.y : &u.x);
-        } else if (!dense && pow2 && quad && D.table_kind[l] == 0 && (L.g[0] & 3) == 1 && size >= 4) {
-            // x = 1 (mod 4): x + 1 = x ^ 3, so idx(x+1) = idx(x) ^ 3 -- both in the aligned 4-entry
-            // block of idx(x): one 16-B gather instead of two 4-B ones (the kernel is bound by
-            // per-lane gather requests, not bytes)
-            const uint4 u = *reinterpret_cast<const uint4*>(tab + (i0 & ~3u));
-            const uint32_t k0 = i0 & 3u, k1 = k0 ^ 3u;
-            const uint32_t a = k0 == 0 ? u.x : k0 == 1 ? u.y : k0 == 2 ? u.z : u.w;
-            const uint32_t b = k1 == 0 ? u.x : k1 == 1 ? u.y : k1 == 2 ? u.z : u.w;
-            v[2 * yz] = __builtin_bit_cast(__half2, a);
-            v[2 * yz + 1] = __builtin_bit_cast(__half2, b);
         } else {
             v[2 * yz] = tab[i0];
             v[2 * yz + 1] = tab[corner_index(D, l, L.g[0] + 1, gy, gz)];
@@ -856,10 +845,7 @@ struct BinPlan {
     uint32_t t_offset[MFN_MAX_LEVELS], t_size[MFN_MAX_LEVELS];
     int t_bin0[MFN_MAX_LEVELS + 1];  // first bin of each table; t_bin0[n_tables] = n_bins
     int t_level[MFN_MAX_LEVELS];     // a level of each table (its fixed-point scale)
-    // the scatter's workgroups per unit (1 or 2: table halves t % halves, bin_scatter_kernel<.., NH>)
-    // and each table's first bin in its half's own bin list (= t_bin0 with one half)
-    int halves;
-    int t_lbin0[MFN_MAX_LEVELS];
+    int scan_waves;                  // waves scanning a level's bin chunks (MFNERF_SCAN_WAVES; A/B)
 };
 
 __device__ __forceinline__ int bin_table(const BinPlan& P, int b) {
@@ -1053,7 +1039,6 @@ constexpr int UNITS = 256;       // scatter workgroups, each owning a contiguous
 constexpr int SC_THREADS = 1024;
 constexpr int MAX_TBINS = 1024;  // bins of one table
 constexpr int SC_STAGE = SC_THREADS * 8;  // staged records per tile (8 per thread)
-constexpr int SCATTER_HALVES_DEFAULT = 1;
 
 // records per (partition, unit) slot at live count nn; non-decreasing in nn, so the workspace sized
 // with slot_size(n_max) (binned_workspace_layout) holds every slot of any nn <= n_max
@@ -1103,11 +1088,8 @@ struct BinRec {
     uint32_t meta;  // bin in the table (bits 0-15) | rank in the bin's run (bits 16-31); ~0u: none
 };
 
-// NH = 2: two workgroups of 512 threads per unit (blocks u and u + UNITS, one XCD), each routing the
-// records of half the tables (t % 2) with half the LDS, so two units' phases -- the counting
-// atomics, the one-wave scan, the placement, the barriers between them -- interleave on a CU.
-template <int MAXB, bool PAIR, int NH>
-__global__ __launch_bounds__(SC_THREADS / NH) void bin_scatter_kernel(const float* __restrict__ X, int64_t n,
+template <int MAXB, bool PAIR>
+__global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __restrict__ X, int64_t n,
                                                                  const int32_t* __restrict__ n_dev, float x_min,
                                                                  float x_range, const mfnerf_grid_desc D,
                                                                  const BinPlan P, const float* __restrict__ dy,
@@ -1117,14 +1099,9 @@ __global__ __launch_bounds__(SC_THREADS / NH) void bin_scatter_kernel(const floa
                                                                  int32_t* __restrict__ ovf, int64_t n_slots,
                                                                  int* __restrict__ ovw) {
     constexpr int SPT = PAIR ? 2 : 1;  // samples per thread per tile
-    constexpr int TH = SC_THREADS / NH, STG = SC_STAGE / NH, LCUR = LDS_CURSOR / NH;
-    const int u = (int)blockIdx.x % UNITS, hh = (int)blockIdx.x / UNITS;  // unit, table half
-    const int my_bins = NH == 1 ? P.n_bins : [&] {
-        int c = 0;
-        for (int t = hh; t < P.n_tables; t += NH) c += P.t_bin0[t + 1] - P.t_bin0[t];
-        return c;
-    }();
-    __shared__ int cursor[LCUR];  // running counts by the half's own bin index (t_lbin0)
+    constexpr int TH = SC_THREADS, STG = SC_STAGE, LCUR = LDS_CURSOR;
+    const int u = blockIdx.x;
+    __shared__ int cursor[LCUR];  // the unit's running count per bin
     // per-level bin counts, double-buffered by level parity (a level's counts are read by the scan
     // and cleared during its placement, while the next level counts into the other buffer)
     __shared__ int hist2[2][MAX_TBINS], toff[MAX_TBINS];
@@ -1137,13 +1114,11 @@ __global__ __launch_bounds__(SC_THREADS / NH) void bin_scatter_kernel(const floa
     __shared__ int s_total[2];
     uint32_t rmax2 = 0u;  // largest |a| (low half), |b| (high half) of this thread's records, fp16 bits
     load_fixed_scales(D, level_l1, fs_s);
-    for (int b = threadIdx.x; b < min(my_bins, LCUR); b += blockDim.x) cursor[b] = 0;
+    for (int b = threadIdx.x; b < min(P.n_bins, LCUR); b += blockDim.x) cursor[b] = 0;
     // the running counts of the bins past LCUR live in scnt: zeroed by the scanning wave, the only
     // one that touches them (program order within the wave)
     if (threadIdx.x < 64)
-        for (int t = hh; t < P.n_tables; t += NH)
-            for (int b = P.t_bin0[t] + (int)threadIdx.x; b < P.t_bin0[t + 1]; b += 64)
-                if (P.t_lbin0[t] + b - P.t_bin0[t] >= LCUR) scnt[(int64_t)b * UNITS + u] = 0;
+        for (int b = LCUR + (int)threadIdx.x; b < P.n_bins; b += 64) scnt[(int64_t)b * UNITS + u] = 0;
     for (int b = threadIdx.x; b < 2 * MAX_TBINS; b += blockDim.x) hist2[b >> 10][b & (MAX_TBINS - 1)] = 0;
     if (threadIdx.x < 2) s_total[threadIdx.x] = 0;
     __syncthreads();
@@ -1186,8 +1161,7 @@ __global__ __launch_bounds__(SC_THREADS / NH) void bin_scatter_kernel(const floa
         }
         for (int j = 0; j < P.n_binned; ++j) {
             const int t = P.table_of[P.level[j]];
-            if (NH > 1 && t % NH != hh) continue;  // the other workgroup's table (uniform)
-            const int b0 = P.t_bin0[t], tb = P.t_bin0[t + 1] - b0, l0 = P.t_lbin0[t];
+            const int b0 = P.t_bin0[t], tb = P.t_bin0[t + 1] - b0;
             // count: each record computed once, ranked in its bin by the LDS counter
             BinRec R[8];
 #pragma unroll
@@ -1228,7 +1202,8 @@ __global__ __launch_bounds__(SC_THREADS / NH) void bin_scatter_kernel(const floa
                 const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
                 const int per = (tb + 63) >> 6;
                 const int* hs = hist2[par];
-                for (int q = wv; q < per; q += TH / 64) {
+                const int nw = P.scan_waves;
+                for (int q = wv < nw ? wv : per; q < per; q += nw) {
                     int col = 0;  // chunks before q are whole (q < per - 1 ... < tb)
                     for (int q2 = 0; q2 < q; ++q2) col += hs[q2 * 64 + lane];
                     col += dppz_i<0x111, 0xF>(col); col += dppz_i<0x112, 0xF>(col);
@@ -1244,7 +1219,7 @@ __global__ __launch_bounds__(SC_THREADS / NH) void bin_scatter_kernel(const floa
                     const int run = carry + x - c;
                     if (lb < tb) {
                         toff[lb] = run;
-                        const int gb = b0 + lb, cl = l0 + lb;
+                        const int gb = b0 + lb, cl = gb;
                         int32_t* gc = scnt + (int64_t)gb * UNITS + u;  // (bins past LCUR)
                         const int cu = cl < LCUR ? cursor[cl] : *gc;
                         // record k of the sorted stage is position cu - run + k of the slot
@@ -1286,31 +1261,23 @@ __global__ __launch_bounds__(SC_THREADS / NH) void bin_scatter_kernel(const floa
         if (threadIdx.x == 0) {
             uint32_t mx = 0u;
             for (int k = 0; k < TH / 64; ++k) mx = max(mx, wmax[k]);
-            // as a float in table units; per (table half, unit): the bound of a partition adds the
-            // maxima of the workgroups that routed its records
-            smax[hh * UNITS + u] = __float_as_uint(rec_value(mx, 0) * REC_UP);
+            smax[u] = __float_as_uint(rec_value(mx, 0) * REC_UP);  // as a float in table units
         }
     }
     // ovf[0]: this step's overflowed records (the accumulate adds the gradient words when non-zero;
     // zeroed by the next step's first scatter launch); ovf[1]: their running total (never reset by
     // the kernels: mfnerf_grid_encode_bw_binned_flag_offset + 4 bytes, read by the training tools)
     int over = 0;
-    for (int t = hh; t < P.n_tables; t += NH) {
-        for (int b = P.t_bin0[t] + (int)threadIdx.x; b < P.t_bin0[t + 1]; b += blockDim.x) {
-            const int cl = P.t_lbin0[t] + b - P.t_bin0[t];
-            if (cl < LCUR) {
-                const int c = cursor[cl];
-                over += c > slot ? (int)(c - slot) : 0;
-                scnt[(int64_t)b * UNITS + u] = c;
-            }
-        }
-        if (threadIdx.x < 64)  // the counts past LCUR: already in scnt, read back by the wave that wrote them
-            for (int b = P.t_bin0[t] + (int)threadIdx.x; b < P.t_bin0[t + 1]; b += 64)
-                if (P.t_lbin0[t] + b - P.t_bin0[t] >= LCUR) {
-                    const int c = scnt[(int64_t)b * UNITS + u];
-                    over += c > slot ? (int)(c - slot) : 0;
-                }
+    for (int b = threadIdx.x; b < min(P.n_bins, LCUR); b += blockDim.x) {
+        const int c = cursor[b];
+        over += c > slot ? (int)(c - slot) : 0;
+        scnt[(int64_t)b * UNITS + u] = c;
     }
+    if (threadIdx.x < 64)  // the counts past LCUR: already in scnt, read back by the wave that wrote them
+        for (int b = LCUR + (int)threadIdx.x; b < P.n_bins; b += 64) {
+            const int c = scnt[(int64_t)b * UNITS + u];
+            over += c > slot ? (int)(c - slot) : 0;
+        }
     if (over) {
         atomicAdd(ovf, over);
         atomicAdd(ovf + 1, over);
@@ -1346,29 +1313,7 @@ __device__ __forceinline__ void accum_record(unsigned long long* img, int mask, 
     }
 }
 
-// a PAIR-layout record (every record a pair: BinPlan::pair_ok), no branches: lanes without a record
-// pass live = false and add zero to entry 0 (an LDS atomic of zero changes nothing)
-__device__ __forceinline__ void accum_pair(unsigned long long* img, int mask, uint2 r, float k2, bool live) {
-    const uint32_t w = live ? r.x : 0u;
-    const float a = live ? rec_value(r.y, 0) * k2 : 0.0f, b = live ? rec_value(r.y, 1) * k2 : 0.0f;
-    const float fx = (float)(w >> 17) * (1.0f / 32768.0f);
-    const int e0 = w & mask;
-    const int e1 = e0 ^ ((2 << ((w >> 11) & 15)) - 1);
-    const float w0 = 1.0f - fx;
-    atomicAdd(&img[e0], pack2(w0 * a, w0 * b));
-    atomicAdd(&img[e1], pack2(fx * a, fx * b));
-}
-
-// a record of any layout (accum_pair for PAIR plans, accum_record otherwise)
-__device__ __forceinline__ void accum_any(unsigned long long* img, int mask, uint2 r, float k2, bool pair) {
-    if (pair) accum_pair(img, mask, r, k2, true);
-    else accum_record(img, mask, r, k2);
-}
-
 constexpr int ACC_THREADS = 512;
-// the staged accumulate (bin_accum_kernel<1>): a round's records (half of the partition's slots) are
-// first compacted into an LDS list, then added with every lane busy
-constexpr int ACC_STAGE = 4096;
 static_assert(MAX_BIN_ENTRIES % ACC_THREADS == 0, "the fused Adam's per-thread entries");
 
 // The rest of the optimizer step carried by the accumulate's launch (mfnerf_grid_encode_bw_binned_adam_all):
@@ -1382,7 +1327,6 @@ struct AdamRest {
     int first;           // 1: the grid's first n_blocks workgroups (dispatched early), 0: its last
 };
 
-template <int MODE>
 __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, int64_t n,
                                                                 const int32_t* __restrict__ n_dev,
                                                                 const uint2* __restrict__ rec,
@@ -1445,7 +1389,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     __shared__ float wsum[ACC_THREADS / 64];
     float term = 0.0f;
     bool full = false;  // a slot of this partition overflowed (its extra records: overflow_add)
-    const uint32_t* sm = smax + (bin_table(P, bin) % P.halves) * UNITS;  // the routing workgroups' maxima
+    const uint32_t* sm = smax;
     if ((int)threadIdx.x < UNITS) {
         const int u = threadIdx.x;
         term = (float)min(cnt[u], (int32_t)slot) * __uint_as_float(sm[u]);
@@ -1468,92 +1412,25 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         kbits = max(0, min(30, 30 - e));
     }
     const float k2 = ldexpf(1.0f, kbits + 15);  // the records' values are 2^-15 x table units
-    if constexpr (MODE == 0) {
-        for (int u0 = hw; u0 < UNITS; u0 += QF * n_hw) {
-            if (u0 != hw) prefetch(u0);
-            // records 32..63 of the slots holding more (~35 % of them at the Lego config), loaded only by
-            // the lanes that have one, all issued before the first batch's adds (round 2 loaded them one
-            // slot at a time inside the add loop: a dependent round trip per slot)
-            uint2 r2[QF];
+    for (int u0 = hw; u0 < UNITS; u0 += QF * n_hw) {
+        if (u0 != hw) prefetch(u0);
+        // records 32..63 of the slots holding more (~35 % of them at the Lego config), loaded only by
+        // the lanes that have one, all issued before the first batch's adds (round 2 loaded them one
+        // slot at a time inside the add loop: a dependent round trip per slot)
+        uint2 r2[QF];
 #pragma unroll
-            for (int q = 0; q < QF; ++q) {
-                const int u = u0 + q * n_hw;
-                r2[q] = hl + 32 < c[q] ? base[(int64_t)u * slot + hl + 32] : make_uint2(0u, 0u);
-            }
-#pragma unroll
-            for (int q = 0; q < QF; ++q)
-                if (hl < c[q]) accum_record(img, mask, r[q], k2);
-#pragma unroll
-            for (int q = 0; q < QF; ++q) {
-                const int u = u0 + q * n_hw;
-                if (hl + 32 < c[q]) accum_record(img, mask, r2[q], k2);
-                for (int k = hl + 64; k < c[q]; k += 32) accum_record(img, mask, base[(int64_t)u * slot + k], k2);
-            }
+        for (int q = 0; q < QF; ++q) {
+            const int u = u0 + q * n_hw;
+            r2[q] = hl + 32 < c[q] ? base[(int64_t)u * slot + hl + 32] : make_uint2(0u, 0u);
         }
-    } else {
-        // Staged: per round (slots [128 rho, 128 rho + 128), QF per half-wave), the
-        // records are compacted into an LDS list at their slot's offset (an exclusive scan of the
-        // round's counts), then every thread adds list entries i, i + 512, ...: full lanes, no
-        // per-slot branches.  Records past the list's capacity, or past a slot's 64th, are added
-        // straight from registers.  Same integer sums (order-free).
-        static_assert(QF * ACC_THREADS / 32 == UNITS / 2, "two rounds of 128 slots");
-        const bool pair = P.pair_ok != 0;  // (uniform) every record a pair record
-        __shared__ uint2 stg[ACC_STAGE];
-        __shared__ int soff[UNITS / 2 + 1];
-        for (int rho = 0; rho < 2; ++rho) {
-            const int u0 = hw + 128 * rho;  // (round 1's counts and first records were prefetched below)
-            // records 32..63 of the slots holding more, in flight during the scan
-            uint2 r2[QF];
 #pragma unroll
-            for (int q = 0; q < QF; ++q) {
-                const int u = u0 + q * n_hw;
-                r2[q] = hl + 32 < c[q] ? base[(int64_t)u * slot + hl + 32] : make_uint2(0u, 0u);
-            }
-            // the round's slot offsets: slot s = q * 16 + hw stages its first min(c[q], 64) records
-            // (uniform in the half-wave; records past the 64th are added straight from memory, so
-            // they take no list positions -- the list has no holes)
-            if (hl == 0) {
+        for (int q = 0; q < QF; ++q)
+            if (hl < c[q]) accum_record(img, mask, r[q], k2);
 #pragma unroll
-                for (int q = 0; q < QF; ++q) soff[q * n_hw + hw] = min(c[q], 64);
-            }
-            __syncthreads();
-            if (threadIdx.x < 64) {  // one wave scans the 128 counts (2 per lane)
-                const int a0 = soff[2 * threadIdx.x], a1 = soff[2 * threadIdx.x + 1];
-                int x = a0 + a1;
-                x += dppz_i<0x111, 0xF>(x); x += dppz_i<0x112, 0xF>(x);
-                x += dppz_i<0x114, 0xF>(x); x += dppz_i<0x118, 0xF>(x);
-                x += dppz_i<0x142, 0xA>(x); x += dppz_i<0x143, 0xC>(x);
-                const int ex = x - a0 - a1;
-                __builtin_amdgcn_wave_barrier();
-                soff[2 * threadIdx.x] = ex;
-                soff[2 * threadIdx.x + 1] = ex + a0;
-                if (threadIdx.x == 63) soff[UNITS / 2] = x;
-            }
-            __syncthreads();
-            const int total = soff[UNITS / 2];
-#pragma unroll
-            for (int q = 0; q < QF; ++q) {
-                const int o = soff[q * n_hw + hw] + hl;
-                if (hl < c[q]) {
-                    if (o < ACC_STAGE) stg[o] = r[q];
-                    else accum_any(img, mask, r[q], k2, pair);
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < QF; ++q) {
-                const int u = u0 + q * n_hw;
-                const int o = soff[q * n_hw + hw] + hl + 32;
-                if (hl + 32 < c[q]) {
-                    if (o < ACC_STAGE) stg[o] = r2[q];
-                    else accum_any(img, mask, r2[q], k2, pair);
-                }
-                for (int k = hl + 64; k < c[q]; k += 32) accum_any(img, mask, base[(int64_t)u * slot + k], k2, pair);
-            }
-            if (rho == 0) prefetch(hw + 128);  // the next round's loads fly while this round's list is added
-            __syncthreads();
-            const int ns = min(total, ACC_STAGE);
-            for (int i = threadIdx.x; i < ns; i += ACC_THREADS) accum_any(img, mask, stg[i], k2, pair);
-            __syncthreads();  // the list is rewritten by the next round
+        for (int q = 0; q < QF; ++q) {
+            const int u = u0 + q * n_hw;
+            if (hl + 32 < c[q]) accum_record(img, mask, r2[q], k2);
+            for (int k = hl + 64; k < c[q]; k += 32) accum_record(img, mask, base[(int64_t)u * slot + k], k2);
         }
     }
     __syncthreads();
@@ -1680,8 +1557,8 @@ int bin_plan(const mfnerf_grid_desc* d, BinPlan* P) {
     }
     P->t_bin0[P->n_tables] = nb;
     P->n_bins = nb;
-    P->halves = 1;  // (binned_impl may split the scatter's tables into two halves)
-    for (int t = 0; t < P->n_tables; ++t) P->t_lbin0[t] = P->t_bin0[t];
+    const char* sw = getenv("MFNERF_SCAN_WAVES");
+    P->scan_waves = sw && atoi(sw) >= 1 && atoi(sw) <= SC_THREADS / 64 ? atoi(sw) : SC_THREADS / 64;
     if (P->n_binned > MAX_BINNED) return -1;
     for (int j = 1; j < P->n_binned; ++j)  // the binned levels are contiguous (staged dL/dy rows)
         if (P->level[j] != P->level[0] + j) return -1;
@@ -1740,7 +1617,7 @@ int64_t binned_workspace_layout(const mfnerf_grid_desc* d, int64_t n_max, char* 
     if (W) W->scnt = reinterpret_cast<int32_t*>(base + off);
     off += align256(nb * UNITS * 4);
     if (W) W->smax = reinterpret_cast<uint32_t*>(base + off);
-    off += align256(2 * UNITS * 4);  // per (table half, unit)
+    off += align256(UNITS * 4);
     if (W) W->ovf = reinterpret_cast<int32_t*>(base + off);
     off += 256;
     if (W) W->rec = reinterpret_cast<uint2*>(base + off);
@@ -2138,41 +2015,24 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
         // shared tables bin more)
         // the smallest staging that holds the partitioned levels: fewer registers leave room on each
         // CU for the side stream's march kernels
-        // two workgroups per unit (table halves) unless MFNERF_SCATTER_HALVES=1
-        const char* he = getenv("MFNERF_SCATTER_HALVES");
-        const int NH = (he && atoi(he) == 1) || P.n_tables < 2 ? 1 : (he && atoi(he) == 2 ? 2 : SCATTER_HALVES_DEFAULT);
-        P.halves = NH;
-        {
-            int c[2] = {0, 0};
-            for (int t = 0; t < P.n_tables; ++t) {
-                P.t_lbin0[t] = c[t % NH];
-                c[t % NH] += P.t_bin0[t + 1] - P.t_bin0[t];
-            }
-        }
-#define MFN_SK(B, PR) (NH == 2 ? bin_scatter_kernel<B, PR, 2> : bin_scatter_kernel<B, PR, 1>)
         // the staged dL/dy rows sized for the binned levels (8 at the Lego layout; MixedFeature's
         // shared tables bin more)
         // the smallest staging that holds the partitioned levels: fewer registers leave room on each
         // CU for the side stream's march kernels
-        auto sk = P.pair_ok ? (P.n_binned <= 8    ? MFN_SK(8, true)
-                               : P.n_binned <= 10 ? MFN_SK(10, true)
-                               : P.n_binned <= 12 ? MFN_SK(12, true)
-                                                  : MFN_SK(MAX_BINNED, true))
-                            : (P.n_binned <= 8    ? MFN_SK(8, false)
-                               : P.n_binned <= 12 ? MFN_SK(12, false)
-                                                  : MFN_SK(MAX_BINNED, false));
-#undef MFN_SK
-        hipLaunchKernelGGL(sk, dim3(UNITS * NH), dim3(SC_THREADS / NH), 0, stream, x, n, n_dev, x_min, x_range,
+        auto sk = P.pair_ok ? (P.n_binned <= 8    ? bin_scatter_kernel<8, true>
+                               : P.n_binned <= 10 ? bin_scatter_kernel<10, true>
+                               : P.n_binned <= 12 ? bin_scatter_kernel<12, true>
+                                                  : bin_scatter_kernel<MAX_BINNED, true>)
+                            : (P.n_binned <= 8    ? bin_scatter_kernel<8, false>
+                               : P.n_binned <= 12 ? bin_scatter_kernel<12, false>
+                                                  : bin_scatter_kernel<MAX_BINNED, false>);
+        hipLaunchKernelGGL(sk, dim3(UNITS), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
                            *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.smax, W.ovf, n_slots, W.ovw);
         mfnerf_adam_fused A{};
         if (adam) A = *adam;
         AdamRest X{};
         if (rest) X = *rest;
-        // the staged accumulate (MFNERF_ACCUM=0: the per-slot form)
-        const char* acc_env = getenv("MFNERF_ACCUM");  // (read per call: tests compare both forms)
-        const int acc_mode = acc_env ? atoi(acc_env) : 1;
-        auto ak = acc_mode == 1 ? bin_accum_kernel<1> : bin_accum_kernel<0>;
-        hipLaunchKernelGGL(ak, dim3(P.n_bins + X.n_blocks), dim3(ACC_THREADS), 0, stream, P, n, n_dev,
+        hipLaunchKernelGGL(bin_accum_kernel, dim3(P.n_bins + X.n_blocks), dim3(ACC_THREADS), 0, stream, P, n, n_dev,
                            W.rec, W.scnt, W.smax, W.ovf, W.ovw, (int*)grad_table, n_slots, *desc, level_l1, A, X,
                            (parts & 4) ? 1 : 0);
     }

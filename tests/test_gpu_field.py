@@ -555,14 +555,12 @@ def test_grid_encode_bw_fixed_point_shared_tables(gpu):
 
 
 @pytest.mark.parametrize("name,args", [_layouts()[0], _layouts()[2], _layouts()[3]])
-@pytest.mark.parametrize("halves", ["1", "2"])
-def test_staged_accumulate_matches_per_slot_form(gpu, name, args, halves, monkeypatch):
-    """The staged partition accumulate (records compacted into an LDS list per round, every lane
-    busy; MFNERF_ACCUM=1, the default for PAIR layouts) and the per-slot form (MFNERF_ACCUM=0) add
-    the same integers: bit-identical table gradients, on training-shaped rays and with slots sized
-    far below the count (records past the slots through the overflow words) -- with the scatter as
-    one workgroup per unit or two (table halves, MFNERF_SCATTER_HALVES=2), each within the record
-    bound of the fp64 oracle."""
+def test_partitioned_scatter_on_rays_with_overflowing_slots(gpu, name, args):
+    """The partitioned scatter on training-shaped rays (Lego layout, MixedFeature's shared tables,
+    --T 21's 10 x 1024 partitions) with its record slots sized for the count and 16x below it (most
+    partitions overflow: their records go through the overflow words and the partition sums at its
+    table's unit): within the record bound of the fp64 oracle plus that unit's rounding, and
+    bit-reproducible."""
     lay, olay = GridLayout(*args), FO.GridLayout(*args)
     g = torch.Generator().manual_seed(41)
     R, S = 900, 80
@@ -576,11 +574,9 @@ def test_staged_accumulate_matches_per_slot_form(gpu, name, args, halves, monkey
     gref = tp.grad.double()
     gabs = _abs_grad(x, dy, olay)
     desc = lay.desc()
-    monkeypatch.setenv("MFNERF_SCATTER_HALVES", halves)
     for ns in (N, N // 16):
         out = []
-        for mode in ("0", "1"):
-            monkeypatch.setenv("MFNERF_ACCUM", mode)
+        for _ in range(2):
             gt = torch.zeros(lay.n_params, device=gpu)
             FLD.grid_encode_bw(x.to(gpu), N, dy.to(gpu), gt, lay, desc, workspace=FLD.grid_bw_binned_workspace(desc, ns, gpu),
                                binned=True, n_slots=ns)
@@ -595,5 +591,4 @@ def test_staged_accumulate_matches_per_slot_form(gpu, name, args, halves, monkey
         for a, b in zip(cuts[:-1], cuts[1:]):
             scale = float(gref[a:b].abs().max())
             if scale > 0:
-                _assert_binned(got[a:b], gref[a:b], gabs[a:b], 2e-4 * scale + unit[a:b] * 1.0001,
-                               what=(name, halves, ns, a))
+                _assert_binned(got[a:b], gref[a:b], gabs[a:b], 2e-4 * scale + unit[a:b] * 1.0001, what=(name, ns, a))

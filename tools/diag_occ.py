@@ -12,8 +12,18 @@ from oracle import occupancy_oracle as OO  # noqa: E402
 gpu = torch.device("cuda:0")
 st = engine.TrainStep(engine.StepConfig(n_rays=512, log2_T=16), device=gpu, seed=0)
 st.set_occupancy(synthetic.ball_density_grid())
+poison = "--poison" in sys.argv  # fill the refresh's buffers with garbage first (uninitialised reads)
+st.update_density_grid(warmup=True)  # allocates the buffers
+st.set_occupancy(synthetic.ball_density_grid())
 for warm in (True, False, False):
     before = st.density_grid.clone().cpu()
+    if poison:
+        o = st._occ
+        o.sigma.fill_(1.5e27)
+        o.xyz.fill_(float("nan"))
+        o.cell.fill_(12345)
+        o.feat.fill_(float("nan"))
+        o.tmp.fill_(7.0)
     st.update_density_grid(warmup=warm)
     torch.cuda.synchronize()
     o = st._occ
