@@ -7,6 +7,8 @@
 // accumulates in half; the difference is inside the fp16 output rounding).
 // Backward: see grid_bw_kernel (request-shaped float atomics with in-wave run merging).
 #include <cstdlib>
+#include <type_traits>
+#include <utility>
 
 #include "common.hpp"
 #include "field_pack.hpp"
@@ -2011,14 +2013,9 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
     }
     if ((parts & 2) && P.n_bins > 0) {
         if (!((parts & 1) && l_first > 0)) (void)hipMemsetAsync(W.ovf, 0, sizeof(int32_t), stream);
-        // the staged dL/dy rows sized for the binned levels (8 at the Lego layout; MixedFeature's
-        // shared tables bin more)
-        // the smallest staging that holds the partitioned levels: fewer registers leave room on each
-        // CU for the side stream's march kernels
-        // the staged dL/dy rows sized for the binned levels (8 at the Lego layout; MixedFeature's
-        // shared tables bin more)
-        // the smallest staging that holds the partitioned levels: fewer registers leave room on each
-        // CU for the side stream's march kernels
+        // the staged dL/dy rows sized for the binned levels (10 at the Lego layout; MixedFeature's
+        // shared tables bin more): the smallest staging that holds them leaves room on each CU for
+        // the side stream's march kernels
         auto sk = P.pair_ok ? (P.n_binned <= 8    ? bin_scatter_kernel<8, true>
                                : P.n_binned <= 10 ? bin_scatter_kernel<10, true>
                                : P.n_binned <= 12 ? bin_scatter_kernel<12, true>
@@ -2028,6 +2025,7 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
                                                   : bin_scatter_kernel<MAX_BINNED, false>);
         hipLaunchKernelGGL(sk, dim3(UNITS), dim3(SC_THREADS), 0, stream, x, n, n_dev, x_min, x_range,
                            *desc, P, dL_dout, level_l1, W.rec, W.scnt, W.smax, W.ovf, n_slots, W.ovw);
+
         mfnerf_adam_fused A{};
         if (adam) A = *adam;
         AdamRest X{};

@@ -3,7 +3,8 @@
 this repo's CPU oracle injected as vren / tinycudann exactly as make_golden.py does) under the
 protocol of tests/parity_protocol.py -- BASELINE config 1's shape: 64x64 views, 256 rays per batch,
 Lego's default field (Hash L16 F2 T2^19, rgb 64x2), Adam(lr 1e-2, eps 1e-15) as train.py:136
-configures FusedAdam, fp32 on the CPU.  It records the loss every LOG_EVERY steps and the test-time
+configures FusedAdam, fp32 on the CPU.  It records every step's batch loss (and the train PSNR
+every LOG_EVERY steps) and the test-time
 PSNR (rendering.py:46-118, render(test_time=True)) of the held-out views at the end.
 tests/test_gpu_parity_train.py trains this repo's fused MI355X step from the same weights, rays and
 perturbations and checks the held-out PSNR against these numbers (north_star: within 0.2 dB).
@@ -55,7 +56,7 @@ def main(seed=0):
     opt = torch.optim.Adam([model.xyz_encoder.params, model.rgb_net.params], lr=PP.LR, eps=1e-15)
     loss_fn = NeRFLoss(lambda_distortion=0)
     train, test = PP.scene()
-    hist = []
+    hist, every = [], []
     t0 = time.time()
     real_rand_like = torch.rand_like
     for step in range(PP.STEPS):
@@ -74,6 +75,7 @@ def main(seed=0):
         opt.zero_grad()
         loss.backward()
         opt.step()
+        every.append(float(loss))
         if (step + 1) % PP.LOG_EVERY == 0:
             pred = res["rgb"].detach()
             hist.append({"step": step + 1, "loss": float(loss), "train_psnr": PP.psnr(pred, rgb)})
@@ -91,7 +93,7 @@ def main(seed=0):
                         "lr": PP.LR, "lr_schedule": "cosine per epoch, eta_min lr/100 (train.py:136-142)", "init_seed": PP.INIT_SEED, "run_seed": seed,
                         "field": "Hash L16 F2 T2^19 rgb64x2",
                         "occupancy": "fixed ball union", "precision": "fp32 (reference on CPU, oracle kernels)"},
-           "history": hist, "test_psnr_views": views, "test_psnr": sum(views) / len(views),
+           "history": hist, "loss_every_step": every, "test_psnr_views": views, "test_psnr": sum(views) / len(views),
            "seconds": round(time.time() - t0, 1)}
     name = "parity_train.json" if seed == 0 else f"parity_train_s{seed}.json"
     with open(os.path.join(HERE, name), "w") as f:
