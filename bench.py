@@ -190,6 +190,12 @@ def cpu_baseline(n_rays, log2_T, seconds, grid="Hash", n_tables=1, width=64, lr=
 
 def main():
     args = parse()
+    # the driver reads ONE JSON line from stdout: everything else the process prints there (RCCL's
+    # version banner at communicator init, library chatter) goes to stderr; the line itself is
+    # written to the original stdout
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
+    sys.stdout = os.fdopen(os.dup(2), "w")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -353,7 +359,8 @@ def main():
             "value_with_occupancy_refresh": round(rays_total / (elapsed + args.steps / 16 * density_ms * 1e-3), 1),
             "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
+        with os.fdopen(out_fd, "w") as f:
+            f.write(json.dumps(out) + "\n")
     if dp_on:
         torch.distributed.destroy_process_group()
 

@@ -135,7 +135,7 @@ extern "C" int mfnerf_adam_step(float* params, float* grads, float* m, float* v,
 extern "C" int mfnerf_check_finite(const float* x, int64_t n, int32_t* status, mfnerf_stream_t stream) {
     if (n < 0 || !status || (n > 0 && !x)) { mfn_set_error("check_finite: bad arguments"); return MFN_ERR_INVALID; }
     if (((uintptr_t)x) & 15) { mfn_set_error("check_finite: x must be 16-byte aligned"); return MFN_ERR_INVALID; }
-    (void)hipMemsetAsync(status, 0, sizeof(int32_t), stream);
+    mfn_zero_async(status, sizeof(int32_t), stream);
     if (n > 0) {
         const int64_t want = mfn::div_up<int64_t>(mfn::div_up<int64_t>(n, 4), 256);
         hipLaunchKernelGGL(finite_kernel, dim3((unsigned)(want < 2048 ? (want < 1 ? 1 : want) : 2048)), dim3(256), 0,

@@ -23,6 +23,23 @@ int mfn_check_launch(const char* what) {
     return MFN_OK;
 }
 
+// Zero-fill as a KERNEL, never hipMemsetAsync, for every buffer a captured graph clears: a memset
+// node in a replayed graph was seen not to run (round 4, test_engine_refresh_end_to_end in the full
+// GPU suite: the occupancy refresh's scratch kept the previous refresh's sigmas at ~735 k cells),
+// and a kernel node is what every other step of the graphs already relies on.
+__global__ void mfn_zero_kernel(uint32_t* __restrict__ p, int64_t n_words) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_words; i += stride) p[i] = 0u;
+}
+
+void mfn_zero_async(void* p, int64_t bytes, hipStream_t stream) {
+    if (bytes <= 0) return;
+    const int64_t words = bytes / 4;  // callers clear whole 32-bit words
+    const int64_t want = (words + 255) / 256;
+    hipLaunchKernelGGL(mfn_zero_kernel, dim3((unsigned)(want < 2048 ? (want < 1 ? 1 : want) : 2048)), dim3(256), 0,
+                       stream, (uint32_t*)p, words);
+}
+
 extern "C" {
 
 const char* mfnerf_last_error(void) { return g_err; }

@@ -148,3 +148,5 @@ __device__ __forceinline__ void amp_step_end_last_block(int32_t* step_dev, mfner
 // Error plumbing shared by every C-ABI entry point.
 void mfn_set_error(const char* fmt, ...);
 int mfn_check_launch(const char* what);
+// zero `bytes` (a multiple of 4) with a kernel launch: safe inside a captured graph (capi.cpp)
+void mfn_zero_async(void* p, int64_t bytes, hipStream_t stream);

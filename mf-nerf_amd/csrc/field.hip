@@ -454,6 +454,15 @@ __device__ __forceinline__ void xdl_drain() { asm volatile("s_nop 7\n\ts_nop 7\n
 // add one 32x32 dW tile (row = out 32*ot + (i&3)+8(i>>2)+4h, col = in 32*it + lane&31) into a
 // row-major fp32 LDS image of a (rows x cols) matrix; rows/cols are compile-time at every call, so
 // the register rows that can never be in range are dropped statically
+// A workgroup's slab row holds non-finite values: raise the step's flag now.  Every row finite
+// bounds every slab sum: |row value| <= (samples of one workgroup) x 65504^2 (fp16 operands,
+// f32 accumulation) ~ 1e13, 512 rows ~ 5e15, far below the f32 range -- so with the rows checked
+// here the flag is final when field_bw returns, even with the fold deferred past the table's Adam
+// (mfnerf_grid_encode_bw_binned_adam_all's slab tail).
+__device__ __forceinline__ void slab_row_flag(int32_t* nonfinite, bool bad) {
+    if (nonfinite && __any(bad) && (threadIdx.x & 63) == 0) atomicOr(nonfinite, 1);
+}
+
 __device__ __forceinline__ void dw_add32(float* img, const f32x16& a, int ot, int it, int rows, int cols, int lane,
                                          bool store = false) {
     const int col = 32 * it + (lane & 31), h = lane >> 5;
@@ -860,10 +869,14 @@ __global__ __launch_bounds__(64 * NW) void field_bw_kernel(
             }
             __syncthreads();
         }
+        bool rbad = false;  // a non-finite weight-gradient partial (see slab_row_flag)
         for (int i = threadIdx.x; i < G::N_DW; i += blockDim.x) {
             if (C::R2_SPLIT && i >= oR2 && i < oR3) continue;  // written by field_bw_wr2_kernel
-            row[i] = img[i] * invS;
+            const float val = img[i] * invS;
+            row[i] = val;
+            rbad |= !isfinite(val);
         }
+        slab_row_flag(nonfinite, rbad);
         if (level_l1 && threadIdx.x < 16) atomicAdd(level_l1 + threadIdx.x, l1_part[threadIdx.x]);
     }
 }
@@ -1125,7 +1138,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
             dw_add32(img, acc2, 1, 0, 64, 32, lane, true);
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < G::N_DW; i += blockDim.x) row[i] = img[i] * invS;
+        bool rbad = false;  // a non-finite weight-gradient partial (see slab_row_flag)
+        for (int i = threadIdx.x; i < G::N_DW; i += blockDim.x) {
+            const float val = img[i] * invS;
+            row[i] = val;
+            rbad |= !isfinite(val);
+        }
+        slab_row_flag(nonfinite, rbad);
         if (level_l1 && threadIdx.x < 16) atomicAdd(level_l1 + threadIdx.x, l1_part[threadIdx.x]);
     }
 }
@@ -1141,7 +1160,7 @@ template <int W>
 __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_wr2_kernel(
     const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n,
     const int32_t* __restrict__ n_dev, const _Float16* __restrict__ packed, const float* __restrict__ dL_drgb,
-    float grad_scale, const float* __restrict__ scale_dev, float* __restrict__ slab) {
+    float grad_scale, const float* __restrict__ scale_dev, float* __restrict__ slab, int32_t* __restrict__ nonfinite) {
     using G = Geo<W>;
     constexpr int MT = G::MT;
     constexpr int NF = G::B4;  // forward fragments + Wr3^T (B5)
@@ -1236,7 +1255,13 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_wr2_kernel(
         __syncthreads();
     }
     float* row = slab + (int64_t)blockIdx.x * G::N_DW + oR2;
-    for (int i = threadIdx.x; i < W * W; i += blockDim.x) row[i] = img[i] * invS;
+    bool rbad = false;
+    for (int i = threadIdx.x; i < W * W; i += blockDim.x) {
+        const float val = img[i] * invS;
+        row[i] = val;
+        rbad |= !isfinite(val);
+    }
+    slab_row_flag(nonfinite, rbad);
 }
 
 // grad[p] += sum over slab rows (fixed order: deterministic).  64 columns x 4 row groups per block.
@@ -1255,9 +1280,20 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
     if (p < N_DW) {
         const float4* src = reinterpret_cast<const float4*>(slab + p);
         constexpr int RS = N_DW / 4;  // row stride in float4
-        for (int b = rg; b < rows; b += 16) {
-            const float4 v = src[(int64_t)b * RS];
-            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        // 8 rows' loads issued before their adds (same order of adds): 512 slab rows (the coop
+        // backward) are 4 round trips per thread instead of 32 -- measured 42 us beside the side
+        // stream's march (r4e timeline), whose waves make every dependent round trip longer
+        constexpr int U = 8;
+        for (int b0 = rg; b0 < rows; b0 += 16 * U) {
+            float4 v[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int b = b0 + 16 * k;
+                v[k] = b < rows ? src[(int64_t)b * RS] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                if (b0 + 16 * k < rows) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
         }
     }
     part[rg][c] = acc;
@@ -1384,7 +1420,7 @@ int launch_bw(const void* feat, int64_t ps, const float* dirs, int64_t n, const 
     if constexpr (C::R2_SPLIT)
         hipLaunchKernelGGL(field_bw_wr2_kernel<W>, dim3(BW_BLOCKS), dim3(FIELD_BLOCK), WR2_LDS<W>(), stream,
                            (const _Float16*)feat, ps, dirs, n, n_dev,
-                           (const _Float16*)packed, dL_drgb, grad_scale, scale_dev, (float*)workspace);
+                           (const _Float16*)packed, dL_drgb, grad_scale, scale_dev, (float*)workspace, nonfinite);
     if (grad_xyz)  // else deferred: mfnerf_field_bw_reduce folds the slab later
         hipLaunchKernelGGL(slab_reduce_kernel<W>, dim3((Geo<W>::N_DW + 63) / 64), dim3(256), 0, stream,
                            (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
@@ -1441,6 +1477,10 @@ int mfnerf_field_fw(const void* feat_f16, int64_t feat_plane_stride, const float
     if (rgb_width == 64) launch_fw<64>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, density_only, sigma, rgb, stream);
     else launch_fw<128>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, density_only, sigma, rgb, stream);
     return mfn_check_launch("field_fw");
+}
+
+int mfnerf_field_bw_slab_rows(int rgb_width) {
+    return rgb_width == 64 ? bw_rows(64) : rgb_width == 128 ? BW_BLOCKS : -1;
 }
 
 int64_t mfnerf_field_bw_workspace(int64_t n, int rgb_width) {

@@ -848,6 +848,8 @@ struct BinPlan {
     int t_bin0[MFN_MAX_LEVELS + 1];  // first bin of each table; t_bin0[n_tables] = n_bins
     int t_level[MFN_MAX_LEVELS];     // a level of each table (its fixed-point scale)
     int scan_waves;                  // waves scanning a level's bin chunks (MFNERF_SCAN_WAVES; A/B)
+    int lane_map;                    // 1: the accumulate's slots rotated over its lanes' registers; 0: not
+                                     // (MFNERF_BIN_LANEMAP; A/B)
 };
 
 __device__ __forceinline__ int bin_table(const BinPlan& P, int b) {
@@ -871,6 +873,8 @@ __device__ __forceinline__ int bin_table(const BinPlan& P, int b) {
 // a record's two values: fp16 of v * 2^-15, round to nearest even (v in the table's int32 units)
 constexpr float REC_DOWN = 1.0f / 32768.0f, REC_UP = 32768.0f;
 typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t rec_values(float a, float b) {
     const _Float16 ha = (_Float16)(a * REC_DOWN), hb = (_Float16)(b * REC_DOWN);  // (exact scaling)
     return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
@@ -935,8 +939,10 @@ __device__ __forceinline__ void pair_level_records(const mfnerf_grid_desc& D, co
         const uint32_t hy = (yz & 1) ? hy0 + PRIME1 : hy0, hz = (yz >> 1) ? hz0 + PRIME2 : hz0;
         const uint32_t i0 = (Lg.g[0] ^ hy ^ hz) & mask;
         const float wyz = ((yz & 1) ? wy1 : wy0) * ((yz >> 1) ? wz1 : wz0);
-        const _Float16 ha = (_Float16)(wyz * s0), hb = (_Float16)(wyz * s1);
-        const uint32_t ab = (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
+        // both values rounded to f32, then packed to f16 pairs by one v_cvt_pk_f16_f32 (the
+        // rounding of level_records_geo; one conversion instead of two fma_mix + the packing)
+        const float2v v = {wyz * s0, wyz * s1};
+        const uint32_t ab = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, half2v));
         emit(yz, (int)(i0 >> P.shift), make_uint2((i0 & emask) | flags, ab));
     }
 }
@@ -1090,6 +1096,16 @@ struct BinRec {
     uint32_t meta;  // bin in the table (bits 0-15) | rank in the bin's run (bits 16-31); ~0u: none
 };
 
+// f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>)
+template <typename F, int... J>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, J...>) {
+    (f(std::integral_constant<int, J>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 template <int MAXB, bool PAIR>
 __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __restrict__ X, int64_t n,
                                                                  const int32_t* __restrict__ n_dev, float x_min,
@@ -1154,6 +1170,10 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
     for (int64_t base = 0; base < m; base += (int64_t)SPT * TH) {
         StagedSample<MAXB> S[SPT];
         bool live[SPT];
+        // (round 4 measured lane l of wave w taking position w of chunk l + 64 q instead, so that one
+        // instruction's lanes hold 64 different rays: the counting atomics' address conflicts fell
+        // from 22 to 5.5 % of the LDS-active cycles, the bank conflicts stayed at 53 %, and the
+        // scattered staging loads made the kernel slower, 98 -> 102 us: not kept)
 #pragma unroll
         for (int q = 0; q < SPT; ++q) {
             const int64_t k = base + (int64_t)q * TH + threadIdx.x;
@@ -1161,7 +1181,8 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
             live[q] = k < m && i < nn;
             if (live[q]) stage_sample(D, P, X, x_min, x_range, dy, i, S[q]);
         }
-        for (int j = 0; j < P.n_binned; ++j) {
+        // one level's pass over the tile; G(q) = sample q's dL/dy pair at level j
+        auto pass = [&](int j, auto G) __attribute__((always_inline)) {
             const int t = P.table_of[P.level[j]];
             const int b0 = P.t_bin0[t], tb = P.t_bin0[t + 1] - b0;
             // count: each record computed once, ranked in its bin by the LDS counter
@@ -1170,7 +1191,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
             for (int k = 0; k < 8; ++k) R[k].meta = ~0u;
 #pragma unroll
             for (int q = 0; q < SPT; ++q) {
-                const SampleLevel Q = sample_level(D, P, S[q], j);
+                const SampleLevel Q = G(q);
                 if (!(live[q] && Q.live)) continue;
                 // the record's |a|, |b| maxima as two packed u16 (fp16 bits order like the values)
                 auto rank = [&](int k, int lb, uint2 r) {
@@ -1248,6 +1269,24 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
             __syncthreads();
             prev_b0 = b0;
             par ^= 1;
+        };
+        if constexpr (PAIR && MAXB <= 10) {
+            // the level loop written out: j a constant in every copy, so the staged pair is a plain
+            // register (sample_level's select costs 2 MAXB v_cndmask per sample and level)
+            auto each = [&](auto jc) __attribute__((always_inline)) {
+                constexpr int j = decltype(jc)::value;
+                if (j < P.n_binned)
+                    pass(j, [&](int q) {
+                        SampleLevel r;
+                        r.g0 = S[q].g[2 * j];
+                        r.g1 = S[q].g[2 * j + 1];
+                        r.live = !(r.g0 == 0.0f && r.g1 == 0.0f);
+                        return r;
+                    });
+            };
+            static_for<MAXB>(each);
+        } else {
+            for (int j = 0; j < P.n_binned; ++j) pass(j, [&](int q) { return sample_level(D, P, S[q], j); });
         }
     }
     store_prev();
@@ -1318,6 +1357,86 @@ __device__ __forceinline__ void accum_record(unsigned long long* img, int mask, 
 constexpr int ACC_THREADS = 512;
 static_assert(MAX_BIN_ENTRIES % ACC_THREADS == 0, "the fused Adam's per-thread entries");
 
+// The MLPs' part of the collective-free step's optimizer, run after the table's (the slab tail of
+// mfnerf_grid_encode_bw_binned_adam_all_slab): field_bw left its weight gradients as per-workgroup
+// slab rows (deferred fold), so slab_reduce_kernel's reduction runs HERE, after the scatter, instead
+// of right after field_bw, where it sat beside the next step's march (39 us there, r4f timeline).
+// Workgroup cg sums parameters [64 cg, 64 cg + 64) over the rows in slab_reduce_kernel's order and
+// applies Adam to them at once (the non-finite flag is final: field_bw checks its rows,
+// slab_row_flag).  The repack and the bookkeeping follow as adam_fixed_kernel's tail pass (a
+// last-workgroup repack here needs an agent-scope release per workgroup -- an L2 writeback each:
+// 58 us for this kernel in the r4g timeline).  Bit-identical to slab_reduce (into zeroed
+// gradients) + adam_fixed_kernel.
+template <int W>
+__global__ __launch_bounds__(256) void mlp_slab_tail_kernel(const float* __restrict__ slab, int rows,
+                                                            float* __restrict__ p, float* __restrict__ m,
+                                                            float* __restrict__ v, __half* __restrict__ p16,
+                                                            float lr,
+                                                            float b1, float b2, float eps,
+                                                            int32_t* __restrict__ step_dev,
+                                                            const float* __restrict__ lr_dev,
+                                                            const mfnerf_amp_state* __restrict__ amp) {
+    constexpr int N_DW = mfn_field::Geo<W>::N_DW;
+    static_assert(N_DW % 4 == 0, "float4 columns");
+    __shared__ float4 part[16][16];
+    const int c = threadIdx.x & 15, rg = threadIdx.x >> 4;
+    const int q0 = blockIdx.x * 64 + 4 * c;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (q0 < N_DW) {
+        const float4* src = reinterpret_cast<const float4*>(slab + q0);
+        constexpr int RS = N_DW / 4;
+        constexpr int U = 8;
+        for (int r0 = rg; r0 < rows; r0 += 16 * U) {
+            float4 x[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int r = r0 + 16 * k;
+                x[k] = r < rows ? src[(int64_t)r * RS] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                if (r0 + 16 * k < rows) { acc.x += x[k].x; acc.y += x[k].y; acc.z += x[k].z; acc.w += x[k].w; }
+        }
+    }
+    part[rg][c] = acc;
+    __syncthreads();
+    if (rg == 0 && q0 < N_DW) {
+        float4 t[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) t[k] = part[k][c];
+#pragma unroll
+        for (int w = 8; w > 0; w >>= 1)
+#pragma unroll
+            for (int k = 0; k < w; ++k) {
+                t[k].x += t[k + w].x; t[k].y += t[k + w].y; t[k].z += t[k + w].z; t[k].w += t[k + w].w;
+            }
+        const bool skipped = amp && amp->nonfinite;
+        if (!skipped) {
+            const int st = *step_dev + 1;
+            if (lr_dev) lr = *lr_dev;
+            const float bc1 = 1.0f - powf(b1, (float)st);
+            const float bc2 = 1.0f - powf(b2, (float)st);
+            // the gradient the unfused path's Adam reads: 0 + the sum (slab_reduce adds into zeros)
+            const float g[4] = {0.0f + t[0].x, 0.0f + t[0].y, 0.0f + t[0].z, 0.0f + t[0].w};
+            float4 pp = *reinterpret_cast<float4*>(p + q0);
+            float4 mm = *reinterpret_cast<float4*>(m + q0);
+            float4 vv = *reinterpret_cast<float4*>(v + q0);
+            mfn::adam_elem(pp.x, mm.x, vv.x, g[0], b1, b2, eps, lr, bc1, bc2);
+            mfn::adam_elem(pp.y, mm.y, vv.y, g[1], b1, b2, eps, lr, bc1, bc2);
+            mfn::adam_elem(pp.z, mm.z, vv.z, g[2], b1, b2, eps, lr, bc1, bc2);
+            mfn::adam_elem(pp.w, mm.w, vv.w, g[3], b1, b2, eps, lr, bc1, bc2);
+            *reinterpret_cast<float4*>(p + q0) = pp;
+            *reinterpret_cast<float4*>(m + q0) = mm;
+            *reinterpret_cast<float4*>(v + q0) = vv;
+            if (p16) {
+                __half2 a = __floats2half2_rn(pp.x, pp.y), b = __floats2half2_rn(pp.z, pp.w);
+                uint2 u; u.x = *reinterpret_cast<uint32_t*>(&a); u.y = *reinterpret_cast<uint32_t*>(&b);
+                *reinterpret_cast<uint2*>(p16 + q0) = u;
+            }
+        }
+    }
+}
+
 // The rest of the optimizer step carried by the accumulate's launch (mfnerf_grid_encode_bw_binned_adam_all):
 // its first n_blocks workgroups run adam_fixed_body over the float4 groups [0, end4) -- the MLPs and
 // the dense levels, whose gradients are final before the scatter -- beside the partitions' workgroups.
@@ -1327,6 +1446,7 @@ struct AdamRest {
     int64_t dense_vals, total_vals, end4;
     int n_blocks;        // 0: none
     int first;           // 1: the grid's first n_blocks workgroups (dispatched early), 0: its last
+    int64_t lo4;         // first float4 group (0; the MLPs' count when their update rides the slab tail)
 };
 
 __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, int64_t n,
@@ -1353,7 +1473,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         const float bc2 = 1.0f - powf(A.beta2, (float)stp);
         adam_fixed_body(A.params, X.g, A.m, A.v, reinterpret_cast<__half*>(A.p16), A.table_offset, X.priv,
                         X.dense_vals, X.total_vals, TR, lr, A.beta1, A.beta2, A.eps, bc1, bc2, skipped,
-                        (int64_t)rest_b * blockDim.x + threadIdx.x, X.end4, (int64_t)X.n_blocks * blockDim.x);
+                        X.lo4 + (int64_t)rest_b * blockDim.x + threadIdx.x, X.end4, (int64_t)X.n_blocks * blockDim.x);
         return;
     }
     const bool add_words = *ovf != 0;  // a slot overflowed: its records are in the gradient words
@@ -1369,19 +1489,43 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     // Measured in round 2: 4 -> 16 -> 8 slots per round 0.709 -> 0.693 -> 0.683 ms/step; the records
     // 32-63 loaded in the same round as well 0.711 (double the record reads); exact loads after the
     // counts (round 3, 106 VGPRs, 2 workgroups per CU) 157 vs 108 us.
+    //
+    // Round 4: the records are loaded as above (a slot's 32 consecutive records per half-wave: a few
+    // whole lines per load), then ROTATED across the QF registers per lane -- lane hl's register q
+    // takes the record of slot (q + hl) mod QF -- so one LDS-add instruction carries records of QF
+    // different units' slots instead of 32 consecutive records of one.  A unit's slot holds a ray's
+    // consecutive samples in one cell as consecutive records (the same entry): in one instruction
+    // those were same-address LDS atomics, serialised (PMC r4e: address conflicts 59 % of the
+    // LDS-active cycles, 10.9 LDS-active cycles per LDS instruction).  Rotating the slot ASSIGNMENT
+    // instead (r4g) ended the conflicts but made each load touch 8 slots' lines: slower.  Here it
+    // is a 3-stage register barrel shift (v_cndmask) after coalesced loads.  Same records, same adds.
     const int hw = threadIdx.x >> 5, hl = threadIdx.x & 31, n_hw = ACC_THREADS / 32;
     const int32_t* cnt = scnt + (int64_t)bin * UNITS;
     const uint2* base = rec + (int64_t)bin * UNITS * slot;
     constexpr int QF = 8;
+    static_assert((QF & (QF - 1)) == 0, "slot rotation");
     uint2 r[QF];
-    int c[QF];
+    int c[QF];  // the count of slot q of the batch (uniform over the half-wave)
     auto prefetch = [&](int u0) {
 #pragma unroll
         for (int q = 0; q < QF; ++q) {
             const int u = u0 + q * n_hw;
             c[q] = u < UNITS ? min(cnt[u], (int32_t)slot) : 0;  // (records past a full slot: overflow_add)
-            const uint2* sl = base + (int64_t)(u < UNITS ? u : 0) * slot;
-            r[q] = sl[hl];
+            // 32-bit record offsets in the partition (the scalar base + a 32-bit vector offset)
+            r[q] = base[(uint32_t)(u < UNITS ? u : 0) * (uint32_t)slot + (uint32_t)hl];
+        }
+    };
+    const int rot = P.lane_map ? (hl & (QF - 1)) : 0;
+    // r[q] <- r[(q + rot) mod QF]: log2(QF) conditional register rotations by 1, 2, 4
+    auto rotate = [&]() {
+#pragma unroll
+        for (int b = 1; b < QF; b <<= 1) {
+            const bool sh = (rot & b) != 0;
+            uint2 t[QF];
+#pragma unroll
+            for (int q = 0; q < QF; ++q) t[q] = r[q];
+#pragma unroll
+            for (int q = 0; q < QF; ++q) r[q] = sh ? t[(q + b) & (QF - 1)] : t[q];
         }
     };
     prefetch(hw);  // the first round's loads overlap the image zeroing and the partition's bound
@@ -1420,19 +1564,27 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         // the lanes that have one, all issued before the first batch's adds (round 2 loaded them one
         // slot at a time inside the add loop: a dependent round trip per slot)
         uint2 r2[QF];
+        // which of this lane's records are live (bit q: record hl of slot q), rotated like r (before
+        // the second records' loads: their registers are not live across the rotation)
+        uint32_t live = 0;
+#pragma unroll
+        for (int q = 0; q < QF; ++q) live |= (uint32_t)(hl < c[q]) << q;
+        live = ((live | (live << QF)) >> rot) & ((1u << QF) - 1);
+        rotate();
 #pragma unroll
         for (int q = 0; q < QF; ++q) {
             const int u = u0 + q * n_hw;
-            r2[q] = hl + 32 < c[q] ? base[(int64_t)u * slot + hl + 32] : make_uint2(0u, 0u);
+            r2[q] = hl + 32 < c[q] ? base[(uint32_t)u * (uint32_t)slot + (uint32_t)(hl + 32)] : make_uint2(0u, 0u);
         }
 #pragma unroll
         for (int q = 0; q < QF; ++q)
-            if (hl < c[q]) accum_record(img, mask, r[q], k2);
+            if ((live >> q) & 1u) accum_record(img, mask, r[q], k2);
 #pragma unroll
         for (int q = 0; q < QF; ++q) {
             const int u = u0 + q * n_hw;
             if (hl + 32 < c[q]) accum_record(img, mask, r2[q], k2);
-            for (int k = hl + 64; k < c[q]; k += 32) accum_record(img, mask, base[(int64_t)u * slot + k], k2);
+            for (int k = hl + 64; k < c[q]; k += 32)
+                accum_record(img, mask, base[(uint32_t)u * (uint32_t)slot + (uint32_t)k], k2);
         }
     }
     __syncthreads();
@@ -1561,6 +1713,8 @@ int bin_plan(const mfnerf_grid_desc* d, BinPlan* P) {
     P->n_bins = nb;
     const char* sw = getenv("MFNERF_SCAN_WAVES");
     P->scan_waves = sw && atoi(sw) >= 1 && atoi(sw) <= SC_THREADS / 64 ? atoi(sw) : SC_THREADS / 64;
+    const char* lm = getenv("MFNERF_BIN_LANEMAP");
+    P->lane_map = lm ? (atoi(lm) != 0) : 1;
     if (P->n_binned > MAX_BINNED) return -1;
     for (int j = 1; j < P->n_binned; ++j)  // the binned levels are contiguous (staged dL/dy rows)
         if (P->level[j] != P->level[0] + j) return -1;
@@ -1882,11 +2036,18 @@ int mfnerf_grid_encode_bw_binned_adam(const float* x, int64_t n, const int32_t* 
                        adam, stream);
 }
 
-int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
-                                          const mfnerf_grid_desc* desc, const float* dL_dout, float* grads,
-                                          int64_t n_params, void* workspace, int64_t n_slots, float* level_l1,
-                                          const mfnerf_adam_fused* adam, int32_t* step_dev, mfnerf_amp_state* amp,
-                                          void* packed, int rgb_width, mfnerf_stream_t stream) {
+}  // extern "C"
+
+namespace {
+int adam_all_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                  const mfnerf_grid_desc* desc, const float* dL_dout, float* grads, int64_t n_params,
+                  void* workspace, int64_t n_slots, float* level_l1, const mfnerf_adam_fused* adam,
+                  int32_t* step_dev, mfnerf_amp_state* amp, void* packed, int rgb_width, const float* slab,
+                  int slab_rows, mfnerf_stream_t stream) {
+    if (slab && ((rgb_width != 64 && rgb_width != 128) || slab_rows <= 0 || !adam || !adam->params)) {
+        mfn_set_error("grid_encode_bw_binned_adam_all_slab: bad slab (rgb_width 64 or 128, rows > 0)");
+        return MFN_ERR_INVALID;
+    }
     if (packed && ((rgb_width != 64 && rgb_width != 128) || !adam || !adam->p16)) {
         mfn_set_error("grid_encode_bw_binned_adam_all: the repack needs rgb_width 64 or 128 and adam->p16");
         return MFN_ERR_INVALID;
@@ -1918,16 +2079,28 @@ int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32
         mfn_set_error("grid_encode_bw_binned_adam_all: the record slots overflow 32-bit record indices");
         return MFN_ERR_INVALID;
     }
-    // [0, fused_from) by the accumulate launch's leading workgroups (one float4 per thread, <= 256 of them)
-    AdamRest X{grads, (int*)workspace, 2 * dense_entries_of(desc), total, fused_from / 4, 0, 1};
+    // [0, fused_from) by the accumulate launch's leading workgroups (one float4 per thread, <= 256 of
+    // them); with the slab tail the MLPs' values [0, N_DW) are left to it
+    const int64_t n_dw = !slab ? 0 : rgb_width == 64 ? mfn_field::Geo<64>::N_DW : mfn_field::Geo<128>::N_DW;
+    if (n_dw % 4 || n_dw > adam->table_offset) {
+        mfn_set_error("grid_encode_bw_binned_adam_all_slab: the MLP weights must precede the table");
+        return MFN_ERR_INVALID;
+    }
+    AdamRest X{grads, (int*)workspace, 2 * dense_entries_of(desc), total, fused_from / 4, 0, 1, n_dw / 4};
     // <= 256 workgroups, the grid's first (256 vs 64 of them 0.655 vs 0.657 ms/step; first vs last
     // in the grid within noise)
-    const int64_t want = div_up<int64_t>(fused_from / 4, ACC_THREADS);
+    const int64_t want = div_up<int64_t>((fused_from - n_dw) / 4, ACC_THREADS);
     X.n_blocks = (int)(want < 1 ? 1 : (want < 256 ? want : 256));
     X.first = 1;
     st = binned_impl(x, n, n_dev, x_min, x_range, desc, dL_dout, grads + adam->table_offset, workspace, n_slots,
                      level_l1, 3, adam, stream, &X);
     if (st) return st;
+    if (slab) {  // the MLPs: their slab rows reduced + Adam (the tail pass below repacks them)
+        auto tk = rgb_width == 64 ? mlp_slab_tail_kernel<64> : mlp_slab_tail_kernel<128>;
+        hipLaunchKernelGGL(tk, dim3((unsigned)div_up<int64_t>(n_dw, 64)), dim3(256), 0, stream, slab, slab_rows,
+                           adam->params, adam->m, adam->v, (__half*)adam->p16, adam->lr, adam->beta1, adam->beta2,
+                           adam->eps, step_dev, adam->lr_dev, amp);
+    }
     // the MLP repack and the step's bookkeeping (step count, loss scale, level_l1 zeroed) by the last
     // workgroup -- after every workgroup of the accumulate has read them
     hipLaunchKernelGGL(adam_fixed_kernel, dim3(64), dim3(256), 0, stream, adam->params, grads, adam->m, adam->v,
@@ -1939,6 +2112,33 @@ int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32
     if (!amp)
         hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, amp, level_l1, desc->n_levels);
     return mfn_check_launch("grid_encode_bw_binned_adam_all");
+}
+}  // namespace
+
+extern "C" {
+
+int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
+                                          const mfnerf_grid_desc* desc, const float* dL_dout, float* grads,
+                                          int64_t n_params, void* workspace, int64_t n_slots, float* level_l1,
+                                          const mfnerf_adam_fused* adam, int32_t* step_dev, mfnerf_amp_state* amp,
+                                          void* packed, int rgb_width, mfnerf_stream_t stream) {
+    return adam_all_impl(x, n, n_dev, x_min, x_range, desc, dL_dout, grads, n_params, workspace, n_slots, level_l1,
+                         adam, step_dev, amp, packed, rgb_width, nullptr, 0, stream);
+}
+
+int mfnerf_grid_encode_bw_binned_adam_all_slab(const float* x, int64_t n, const int32_t* n_dev, float x_min,
+                                               float x_range, const mfnerf_grid_desc* desc, const float* dL_dout,
+                                               float* grads, int64_t n_params, void* workspace, int64_t n_slots,
+                                               float* level_l1, const mfnerf_adam_fused* adam, int32_t* step_dev,
+                                               mfnerf_amp_state* amp, void* packed, int rgb_width,
+                                               const void* field_workspace, mfnerf_stream_t stream) {
+    if (!field_workspace) {
+        mfn_set_error("grid_encode_bw_binned_adam_all_slab: null field workspace");
+        return MFN_ERR_INVALID;
+    }
+    return adam_all_impl(x, n, n_dev, x_min, x_range, desc, dL_dout, grads, n_params, workspace, n_slots, level_l1,
+                         adam, step_dev, amp, packed, rgb_width, (const float*)field_workspace,
+                         mfnerf_field_bw_slab_rows(rgb_width), stream);
 }
 
 int64_t mfnerf_grid_binned_first_value(const mfnerf_grid_desc* desc) {
@@ -2012,7 +2212,7 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
                            (parts & 2) ? W.ovf : (int32_t*)nullptr);
     }
     if ((parts & 2) && P.n_bins > 0) {
-        if (!((parts & 1) && l_first > 0)) (void)hipMemsetAsync(W.ovf, 0, sizeof(int32_t), stream);
+        if (!((parts & 1) && l_first > 0)) mfn_zero_async(W.ovf, sizeof(int32_t), stream);
         // the staged dL/dy rows sized for the binned levels (10 at the Lego layout; MixedFeature's
         // shared tables bin more): the smallest staging that holds them leaves room on each CU for
         // the side stream's march kernels

@@ -545,7 +545,7 @@ int mfnerf_occupancy_update_dev(float* density_grid, const float* sigmas, const 
     Ws w;
     ws_layout(cascades, grid_size, (char*)workspace, &w);
     const int64_t n = (int64_t)cascades * grid_size * grid_size * grid_size;
-    (void)hipMemsetAsync(tmp, 0, n * sizeof(float), stream);
+    mfn_zero_async(tmp, n * sizeof(float), stream);
     if (n_points)
         hipLaunchKernelGGL(occ_scatter_kernel, dim3(blocks_for(n_points)), dim3(OCC_BLOCK), 0, stream, sigmas, cell_idx,
                            n_points, n_dev, tmp);

@@ -233,11 +233,9 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
 }
 __device__ __forceinline__ int ffs64(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
 
-__global__ __launch_bounds__(256) void march_wave_kernel(MarchParams p, int64_t n_rays, int32_t* __restrict__ counts,
-                                                         float* __restrict__ tbuf) {
+__device__ __forceinline__ void march_wave_ray(const MarchParams& p, int64_t r, int32_t* __restrict__ counts,
+                                               float* __restrict__ tbuf) {
     const int lane = threadIdx.x & 63;
-    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (r >= n_rays) return;  // wave-uniform
     const int limit = p.max_samples;
     float* tr = tbuf + r * (int64_t)p.max_samples;
     const float gsi = 1.0f / (float)p.grid_size;
@@ -300,6 +298,16 @@ __global__ __launch_bounds__(256) void march_wave_kernel(MarchParams p, int64_t 
     }
     if (lane == 0) counts[r] = n;
 }
+
+// one ray per wave per trip; a wave takes rays w, w + W, ... (W = the grid's waves): with fewer waves
+// than rays the march leaves wave slots to the kernels it runs beside (MFNERF_MARCH_RPW)
+__global__ __launch_bounds__(256) void march_wave_kernel(MarchParams p, int64_t n_rays, int32_t* __restrict__ counts,
+                                                         float* __restrict__ tbuf) {
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < n_rays; r += nw)  // wave-uniform
+        march_wave_ray(p, r, counts, tbuf);
+}
+
 
 // The compacted samples of ray r (one wave): its first rays_a[r].count t values from march_wave.
 __global__ __launch_bounds__(256) void march_expand_kernel(MarchParams p, int64_t n_rays,
@@ -542,7 +550,8 @@ __global__ __launch_bounds__(256) void composite_fused_wave_kernel(
     const float* __restrict__ target, int64_t n_mean, float lambda_o, float bg0, float bg1, float bg2,
     int64_t* __restrict__ total_samples, float* __restrict__ opacity, float* __restrict__ depth,
     float* __restrict__ rgb, float* __restrict__ ws, float* __restrict__ dL_drgb, float* __restrict__ dL_dop,
-    float* __restrict__ dL_dsigmas, float* __restrict__ dL_drgbs, float* __restrict__ loss_part) {
+    float* __restrict__ dL_dsigmas, float* __restrict__ dL_drgbs, float* __restrict__ loss_part,
+    int32_t* __restrict__ gate) {
     __shared__ float lsum[4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t n = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -644,6 +653,16 @@ __global__ __launch_bounds__(256) void composite_fused_wave_kernel(
     if (lane == 0) lsum[wid] = l;
     __syncthreads();
     if (threadIdx.x == 0 && loss_part) loss_part[blockIdx.x] = (lsum[0] + lsum[1]) + (lsum[2] + lsum[3]);
+    // gate (gate.hip's {signals, waits, ticket}): the workgroup that finishes last opens it -- the
+    // signal rides this launch instead of a one-thread kernel of its own (~6 us on the step's
+    // critical path, r4f timeline).  Scheduling only: the gated work reads nothing written here.
+    if (gate && threadIdx.x == 0) {
+        const int prev = __hip_atomic_fetch_add(gate + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == (int)gridDim.x - 1) {
+            __hip_atomic_store(gate + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(gate, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 __global__ void composite_test_kernel(const float* __restrict__ sigmas, const float* __restrict__ rgbs,
@@ -808,7 +827,7 @@ int mfnerf_raymarching_train(const float* rays_o, const float* rays_d, const flo
         mfn_set_error("raymarching_train: bad arguments"); return MFN_ERR_INVALID;
     }
     if (!counter) { mfn_set_error("raymarching_train: null counter"); return MFN_ERR_INVALID; }
-    if (n_rays == 0) { (void)hipMemsetAsync(counter, 0, 8, stream); return mfn_check_launch("raymarching_train"); }
+    if (n_rays == 0) { mfn_zero_async(counter, 8, stream); return mfn_check_launch("raymarching_train"); }
     if (!rays_o || !rays_d || !hits_t || !bitfield || !noise || !rays_a || !workspace ||
         (capacity > 0 && (!xyzs || !dirs || !deltas || !ts))) {
         mfn_set_error("raymarching_train: null pointer"); return MFN_ERR_INVALID;
@@ -819,7 +838,8 @@ int mfnerf_raymarching_train(const float* rays_o, const float* rays_d, const flo
     float* tbuf = reinterpret_cast<float*>((char*)workspace + ((n_rays * 4 + 255) / 256) * 256);
     const unsigned nb = blocks_for(n_rays, RAY_BLOCK);
     const bool wave = exp_step_factor == 0.0f;  // constant dt: the wave-per-ray marcher applies
-    const unsigned nbw = (unsigned)div_up<int64_t>(n_rays, 4);
+    static const int rpw = [] { const char* e = getenv("MFNERF_MARCH_RPW"); return e && atoi(e) > 0 ? atoi(e) : 1; }();
+    const unsigned nbw = (unsigned)div_up<int64_t>(n_rays, 4 * (int64_t)rpw);
     if (wave)
         hipLaunchKernelGGL(march_wave_kernel, dim3(nbw), dim3(256), 0, stream, p, n_rays, counts, tbuf);
     else
@@ -894,6 +914,18 @@ int mfnerf_composite_train_fused(const float* sigmas, const float* rgbs, const f
                                  float bg_b, int64_t* total_samples, float* opacity, float* depth, float* rgb,
                                  float* ws, float* dL_drgb, float* dL_dopacity, float* dL_dsigmas, float* dL_drgbs,
                                  float* loss_partials, mfnerf_stream_t stream) {
+    return mfnerf_composite_train_fused_gated(sigmas, rgbs, deltas, ts, rays_a, n_rays, n_samples, T_threshold,
+                                              target, n_mean, lambda_opacity, bg_r, bg_g, bg_b, total_samples,
+                                              opacity, depth, rgb, ws, dL_drgb, dL_dopacity, dL_dsigmas, dL_drgbs,
+                                              loss_partials, nullptr, stream);
+}
+
+int mfnerf_composite_train_fused_gated(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
+                                       const int64_t* rays_a, int64_t n_rays, int64_t n_samples, float T_threshold,
+                                       const float* target, int64_t n_mean, float lambda_opacity, float bg_r,
+                                       float bg_g, float bg_b, int64_t* total_samples, float* opacity, float* depth,
+                                       float* rgb, float* ws, float* dL_drgb, float* dL_dopacity, float* dL_dsigmas,
+                                       float* dL_drgbs, float* loss_partials, int32_t* gate, mfnerf_stream_t stream) {
     if (n_rays < 0 || n_samples < 0 || n_mean < 0 || (n_mean > 0 && n_mean < n_rays)) {
         mfn_set_error("composite_train_fused: bad sizes"); return MFN_ERR_INVALID;
     }
@@ -906,7 +938,7 @@ int mfnerf_composite_train_fused(const float* sigmas, const float* rgbs, const f
     hipLaunchKernelGGL(composite_fused_wave_kernel, dim3(blocks_for(n_rays, 4)), dim3(256), 0, stream, sigmas, rgbs,
                        deltas, ts, rays_a, n_rays, T_threshold, target, n_mean, lambda_opacity, bg_r, bg_g, bg_b,
                        total_samples, opacity, depth, rgb, ws, dL_drgb, dL_dopacity, dL_dsigmas, dL_drgbs,
-                       loss_partials);
+                       loss_partials, gate);
     return mfn_check_launch("composite_train_fused");
 }
 
@@ -934,7 +966,7 @@ int mfnerf_distortion_loss_fw(const float* ws, const float* deltas, const float*
     if (!rays_a || !loss || (n_samples > 0 && (!ws || !deltas || !ts || !ws_incl || !wts_incl))) {
         mfn_set_error("distortion_loss_fw: null pointer"); return MFN_ERR_INVALID;
     }
-    (void)hipMemsetAsync(loss, 0, n_rays * sizeof(float), stream);
+    mfn_zero_async(loss, n_rays * sizeof(float), stream);
     hipLaunchKernelGGL(distortion_fw_kernel, dim3(blocks_for(n_rays, RAY_BLOCK)), dim3(RAY_BLOCK), 0, stream, ws,
                        deltas, ts, rays_a, n_rays, loss, ws_incl, wts_incl);
     return mfn_check_launch("distortion_loss_fw");
@@ -948,7 +980,7 @@ int mfnerf_distortion_loss_bw(const float* dL_dloss, const float* ws_incl, const
     if (!dL_dloss || !rays_a || (n_samples > 0 && (!ws_incl || !wts_incl || !ws || !deltas || !ts || !dL_dws))) {
         mfn_set_error("distortion_loss_bw: null pointer"); return MFN_ERR_INVALID;
     }
-    if (n_samples > 0) (void)hipMemsetAsync(dL_dws, 0, n_samples * sizeof(float), stream);
+    if (n_samples > 0) mfn_zero_async(dL_dws, n_samples * sizeof(float), stream);
     hipLaunchKernelGGL(distortion_bw_kernel, dim3(blocks_for(n_rays, RAY_BLOCK)), dim3(RAY_BLOCK), 0, stream,
                        dL_dloss, ws_incl, wts_incl, ws, deltas, ts, rays_a, n_rays, dL_dws);
     return mfn_check_launch("distortion_loss_bw");

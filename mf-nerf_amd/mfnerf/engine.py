@@ -393,9 +393,10 @@ class TrainStep:
         self.samples_marched.add_(mb.counters[0, 0] if self.n_parts == 1 else mb.counters[:, 0].sum())
         mark("march")
 
-    def _chain(self, batch: Batch, mb, q, mark):
+    def _chain(self, batch: Batch, mb, q, mark, defer_fold=False):
         """Part q: encode -> field -> composite -> loss -> composite bw -> field bw (no grid bw).
-        Part 0 also zeroes the gradient (every part's writes come after it)."""
+        Part 0 also zeroes the gradient (every part's writes come after it).  defer_fold: field_bw
+        leaves the MLP weight gradients as its slab rows (folded by the slab tail, _fused_tail)."""
         c, s = self.cfg, stream()
         t, m = self.parts[q], mb.part[q]
         Np, cap = self.Np, self.cap_p
@@ -418,10 +419,15 @@ class TrainStep:
         target = ptr(batch.rgb[q * Np:(q + 1) * Np])
         if c.lambda_distortion <= 0:
             # composite fw -> bg blend + NeRFLoss -> composite bw in one wave-per-ray launch
-            call("mfnerf_composite_train_fused", ptr(t.sigma), ptr(t.rgb_s), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a),
-                 Np, cap, c.T_threshold, target, c.n_rays, c.lambda_opacity, bg, bg, bg, ptr(t.total),
-                 ptr(t.opacity), ptr(t.depth), ptr(t.rgb), ptr(t.ws), ptr(t.dL_drgb), ptr(t.dL_dop), ptr(t.dsig),
-                 ptr(t.drgb_s), ptr(self.loss_parts[q * self._nb_part:]), s)
+            args = (ptr(t.sigma), ptr(t.rgb_s), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a), Np, cap, c.T_threshold,
+                    target, c.n_rays, c.lambda_opacity, bg, bg, bg, ptr(t.total), ptr(t.opacity), ptr(t.depth),
+                    ptr(t.rgb), ptr(t.ws), ptr(t.dL_drgb), ptr(t.dL_dop), ptr(t.dsig), ptr(t.drgb_s),
+                    ptr(self.loss_parts[q * self._nb_part:]))
+            gate = getattr(mark, "ride", lambda _n: None)("composite")  # the gate signal riding the launch
+            if gate is not None:
+                call("mfnerf_composite_train_fused_gated", *args, gate, s)
+            else:
+                call("mfnerf_composite_train_fused", *args, s)
             mark("composite")
         else:
             call("mfnerf_composite_train_fw", ptr(t.sigma), ptr(t.rgb_s), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a),
@@ -440,8 +446,9 @@ class TrainStep:
                  ptr(t.depth), ptr(t.rgb), Np, cap, c.T_threshold, ptr(t.dsig), ptr(t.drgb_s), s)
             mark("composite_bw")
         call("mfnerf_field_bw", ptr(t.feat), cap, ptr(m.dirs), cap, ptr(m.counter), ptr(self.packed), c.rgb_width,
-             ptr(t.dsig), ptr(t.drgb_s), 0.0 if c.dynamic_loss_scale else self.grad_scale, ptr(t.dfeat), ptr(t.mlp_grad),
-             ptr(t.mlp_grad[self.off_rgb:]), ptr(t.field_ws),
+             ptr(t.dsig), ptr(t.drgb_s), 0.0 if c.dynamic_loss_scale else self.grad_scale, ptr(t.dfeat),
+             None if defer_fold else ptr(t.mlp_grad), None if defer_fold else ptr(t.mlp_grad[self.off_rgb:]),
+             ptr(t.field_ws),
              self._amp_ptr(),
              ptr(self._level_l1) if self._fixed() else None, s)
         mark("field_bw")
@@ -484,16 +491,20 @@ class TrainStep:
     def _grid_bw(self, mb, q, fuse_adam=False):
         """Part q's hash-table gradient scatter (the dominant kernel, alone so it can be timed);
         fuse_adam: with the partitioned tables' Adam step (then _finish_update(partial=True));
-        fuse_adam="all": with the whole optimizer step (then only _pack())."""
+        fuse_adam="all": with the whole optimizer step (then only _pack()); "all-slab": the same after
+        a chain with a deferred weight-gradient fold (_chain(defer_fold=True))."""
         t, m = self.parts[q], mb.part[q]
-        if self._binned() and fuse_adam == "all":
+        if self._binned() and fuse_adam in ("all", "all-slab"):
             self._fused_args = self._adam_fused_args()  # kept alive: graphs capture the call
             amp = self._amp_ptr()
             # the last pass also repacks the MLP weights (no _pack() launch after it)
-            call("mfnerf_grid_encode_bw_binned_adam_all", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min,
-                 self.x_range, self.desc, ptr(t.dfeat), ptr(self.grads), self.n_alloc, ptr(t.grid_ws),
-                 self._bin_slots(), ptr(self._level_l1), ctypes.byref(self._fused_args), ptr(self.step_dev),
-                 amp, ptr(self.packed), self.cfg.rgb_width, stream())
+            args = (ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min, self.x_range, self.desc, ptr(t.dfeat),
+                    ptr(self.grads), self.n_alloc, ptr(t.grid_ws), self._bin_slots(), ptr(self._level_l1),
+                    ctypes.byref(self._fused_args), ptr(self.step_dev), amp, ptr(self.packed), self.cfg.rgb_width)
+            if fuse_adam == "all-slab":
+                call("mfnerf_grid_encode_bw_binned_adam_all_slab", *args, ptr(t.field_ws), stream())
+            else:
+                call("mfnerf_grid_encode_bw_binned_adam_all", *args, stream())
             return
         if self._binned() and fuse_adam:
             self._fused_args = self._adam_fused_args()  # kept alive: graphs capture the call
@@ -513,12 +524,23 @@ class TrainStep:
              self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws),
              ptr(self._level_l1) if self._fixed() else None, stream())
 
-    def _fused_tail(self, j):
+    def _slab_tail(self):
+        """The one-graph step folds the MLP weight gradients after the scatter, not right after
+        field_bw (mfnerf_grid_encode_bw_binned_adam_all_slab): there the fold ran beside the next
+        step's march, 39 us instead of ~12 (r4f timeline).  MFNERF_SLAB_TAIL=0: the fold in the
+        chain."""
+        return (os.environ.get("MFNERF_SLAB_TAIL", "1") == "1" and os.environ.get("MFNERF_FUSED_ADAM_ALL", "1") == "1"
+                and self.n_parts == 1)
+
+    def _fused_tail(self, j, slab=False):
         """The replayed collective-free tail: scatter + every Adam update, then the MLP repack.  By
         default the MLPs' and dense levels' update rides the accumulate's launch
         (mfnerf_grid_encode_bw_binned_adam_all); MFNERF_FUSED_ADAM_ALL=0 keeps it a pass of its own
-        after the scatter (mfnerf_adam_step_fixed_partial).  Same bits either way."""
-        if os.environ.get("MFNERF_FUSED_ADAM_ALL", "1") == "1":
+        after the scatter (mfnerf_adam_step_fixed_partial).  slab: the chain deferred the MLP weight
+        gradients' fold (the MLPs' update then runs in the slab tail).  Same bits every way."""
+        if slab:
+            self._grid_bw(self.mbuf[j], 0, fuse_adam="all-slab")
+        elif os.environ.get("MFNERF_FUSED_ADAM_ALL", "1") == "1":
             self._grid_bw(self.mbuf[j], 0, fuse_adam="all")  # + the repack
         else:
             self._grid_bw(self.mbuf[j], 0, fuse_adam=True)
@@ -807,10 +829,12 @@ class TrainStep:
             if gated:
                 # the whole step as ONE graph: the chain signals the device gate where the host used
                 # to record the event that starts the next march
+                slab = fuse and self._slab_tail()
+
                 def step(j):
-                    self._chain(self._static[j], self.mbuf[j], 0, signal_at)
+                    self._chain(self._static[j], self.mbuf[j], 0, signal_at, defer_fold=slab)
                     if fuse:
-                        self._fused_tail(j)
+                        self._fused_tail(j, slab=slab)
                     else:
                         self._grid_bw(self.mbuf[j], 0)
                         tail()
@@ -827,6 +851,10 @@ class TrainStep:
         # the extra streams share hardware queues) -- the data-parallel step would pay it on every rank
         hi = os.environ.get("MFNERF_SIDE_HIGH_PRIORITY", "0") == "1"
         self._side = torch.cuda.Stream(device=self.dev, priority=torch.cuda.Stream.priority_range()[1] if hi else 0)
+        # gated marches wait as a stream operation (mfnerf_gate_wait_stream) on the count of signals
+        # the host has enqueued; MFNERF_GATE_STREAM=0: the captured one-thread polling kernel
+        self._gate_stream = gated and os.environ.get("MFNERF_GATE_STREAM", "1") == "1"
+        self._gate_target = 0
         self._part_streams = [None] + [torch.cuda.Stream(device=self.dev) for _ in range(P - 1)]
         self._ev_march = [torch.cuda.Event(), torch.cuda.Event()]
         self._ev_start = torch.cuda.Event()
@@ -842,7 +870,7 @@ class TrainStep:
         MFNERF_GATE_AT (default "composite": the next draw + march start beside field_bw, whose one
         wave per SIMD leaves room and issue cycles for the march's waves -- 0.687 -> 0.672 ms/step
         against opening after the whole chain ("field_bw"); "field_fw" 0.677); counts its signals."""
-        self._gate = torch.zeros(2, dtype=torch.int32, device=self.dev)
+        self._gate = torch.zeros(4, dtype=torch.int32, device=self.dev)  # {signals, waits, ticket, -}
         gp = ptr(self._gate)
         gate_at = os.environ.get("MFNERF_GATE_AT", "composite")
         if gate_at not in ("grid_fw", "field_fw", "composite", "field_bw"):
@@ -851,11 +879,25 @@ class TrainStep:
         # second ("composite_bw"), the same place as after the fused kernel
         name_ = "composite_bw" if gate_at == "composite" and self.cfg.lambda_distortion > 0 else gate_at
 
+        ridden = set()
+
         def signal_at(name):
             if name == name_:
-                call("mfnerf_gate_signal", gp, stream())
+                if name in ridden:  # the stage's own kernel opened it (ride)
+                    ridden.discard(name)
+                else:
+                    call("mfnerf_gate_signal", gp, stream())
                 signal_at.count += 1
+
+        def ride(name):
+            """The gate pointer if stage `name`'s kernel should open the gate itself (its last
+            workgroup: no one-thread signal kernel on the critical path; MFNERF_GATE_RIDE=0: off)."""
+            if name == name_ and os.environ.get("MFNERF_GATE_RIDE", "1") == "1":
+                ridden.add(name)
+                return gp
+            return None
         signal_at.count = 0
+        signal_at.ride = ride
         return signal_at
 
     def _stage_batch(self, j, batch):
@@ -879,7 +921,14 @@ class TrainStep:
                 if noise is None:
                     raise ValueError("captured with host_noise: pass noise= / next_noise= to replay()")
                 self._static_noise[j].copy_(noise)
-            self.graphs["march_gated" if gated else "march"][j].replay()
+            if gated and self._gate_stream:
+                # the queue itself holds until the step graph just enqueued has signalled (its
+                # composite's last workgroup): no polling wave beside the chain
+                self._gate_target += 1
+                call("mfnerf_gate_wait_stream", ptr(self._gate), self._gate_target, self._side.cuda_stream)
+                self.graphs["march"][j].replay()
+            else:
+                self.graphs["march_gated" if gated else "march"][j].replay()
             self._ev_march[j].record(self._side)
 
     def replay(self, batch: Batch = None, exchange=None, grid_bw_events=None, next_batch=None, prefetch=None,

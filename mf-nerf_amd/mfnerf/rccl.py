@@ -79,6 +79,11 @@ class Comm:
         self.comm = ctypes.c_void_p()
         torch.cuda.synchronize()
         _check(lib.ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, self.rank), "ncclCommInitRank")
+        # the mean's reduction op: at one rank the mean IS the sum, and RCCL runs an in-place one-rank
+        # SUM as no work at all, where AVG launches its premultiply kernel over the whole buffer (66 us
+        # for the Lego gradient, r4e timeline) -- the one-rank rehearsal then times the data-parallel
+        # step's own kernels, not a copy no real run makes
+        self._mean_op = NCCL_SUM if self.world == 1 else NCCL_AVG
 
     @staticmethod
     def _stream():
@@ -88,7 +93,7 @@ class Comm:
         """shard <- this rank's slice of the mean over ranks of flat (shard may be that slice of flat)."""
         assert flat.numel() == shard.numel() * self.world and flat.dtype == shard.dtype
         _check(_lib().ncclReduceScatter(ctypes.c_void_p(flat.data_ptr()), ctypes.c_void_p(shard.data_ptr()),
-                                        shard.numel(), _dtype(shard), NCCL_AVG, self.comm, self._stream()),
+                                        shard.numel(), _dtype(shard), self._mean_op, self.comm, self._stream()),
                "ncclReduceScatter")
         return shard
 
@@ -102,7 +107,7 @@ class Comm:
 
     def all_reduce_avg_(self, flat):
         _check(_lib().ncclAllReduce(ctypes.c_void_p(flat.data_ptr()), ctypes.c_void_p(flat.data_ptr()), flat.numel(),
-                                    _dtype(flat), NCCL_AVG, self.comm, self._stream()), "ncclAllReduce")
+                                    _dtype(flat), self._mean_op, self.comm, self._stream()), "ncclAllReduce")
         return flat
 
     def close(self):
