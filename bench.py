@@ -63,9 +63,11 @@ def parse():
     ap.add_argument("--log2-T", type=int, default=None, help="override the preset's log2 table size")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--roofline-every", type=int, default=8,
+    ap.add_argument("--roofline-every", type=int, default=25,
                     help="time grid_bw with events on every k-th timed step (those steps replay the scatter "
-                         "as its own graph; the others replay scatter + Adam as one graph)")
+                         "as its own graph, ~45 us more per such step than the one-graph step (r4h: 0.5645 "
+                         "ms/step at k = 8 vs 0.5588 at k = 1000); the others replay the whole step as one "
+                         "graph); 25: 8 timed launches in the default 200 steps")
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of the HIP graphs")
     ap.add_argument("--parts", type=int, default=1, help="ray-range parts per step (chain/scatter overlap)")
     ap.add_argument("--dp", choices=("shard", "allreduce"), default="shard",

@@ -285,12 +285,15 @@ int mfnerf_grid_encode_bw_binned_adam(const float* x, int64_t n, const int32_t* 
  * mfnerf_grid_encode_bw_binned + mfnerf_adam_step_fixed).  packed (optional, else NULL): the last pass
  * also repacks the MLP weights from adam->p16 into the field head's fragment blob for rgb width
  * rgb_width (= mfnerf_field_pack_weights_f16(p16, p16 + 3072, rgb_width, packed), one launch less).
+ * gate (optional, gate.hip's int32 {signals, waits, ticket}; NULL: none): a signal added as the
+ * dense-level launch starts (round 4: the side stream's next march starts beside the scatter
+ * without a signal kernel of its own).
  * Replaces tcnn's hash-grid backward + apex FusedAdam's step over the whole model (train.py:136). */
 int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                                           const mfnerf_grid_desc* desc, const float* dL_dout, float* grads,
                                           int64_t n_params, void* workspace, int64_t n_slots, float* level_l1,
                                           const mfnerf_adam_fused* adam, int32_t* step_dev, mfnerf_amp_state* amp,
-                                          void* packed, int rgb_width, mfnerf_stream_t stream);
+                                          void* packed, int rgb_width, int32_t* gate, mfnerf_stream_t stream);
 /* mfnerf_grid_encode_bw_binned_adam_all after a field_bw whose weight-gradient fold was DEFERRED
  * (mfnerf_field_bw with grad_xyz = grad_rgb = NULL; field_workspace = its workspace): the MLPs'
  * values [0, N_DW) are left out of the accumulate launch's leading workgroups, and a launch after it
@@ -299,13 +302,13 @@ int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32
  * stays zero).  Same bits as mfnerf_field_bw_reduce + mfnerf_grid_encode_bw_binned_adam_all: the fold
  * moves from beside the next step's march (field_bw's tail) to after the scatter.  Requires the
  * non-finite flag to be final when field_bw returns, which field_bw guarantees by checking its slab
- * rows (every row finite bounds the sum far inside f32). */
+ * rows (every row finite bounds the sum far inside f32).  gate: as for _adam_all. */
 int mfnerf_grid_encode_bw_binned_adam_all_slab(const float* x, int64_t n, const int32_t* n_dev, float x_min,
                                                float x_range, const mfnerf_grid_desc* desc, const float* dL_dout,
                                                float* grads, int64_t n_params, void* workspace, int64_t n_slots,
                                                float* level_l1, const mfnerf_adam_fused* adam, int32_t* step_dev,
                                                mfnerf_amp_state* amp, void* packed, int rgb_width,
-                                               const void* field_workspace, mfnerf_stream_t stream);
+                                               const void* field_workspace, int32_t* gate, mfnerf_stream_t stream);
 
 /* out[l] += sum over rows i < n (or *n_dev) of |dL_dout[i][2l]| + |dL_dout[i][2l+1]| (f32). */
 int mfnerf_grid_level_l1(const float* dL_dout, int64_t n, const int32_t* n_dev, int n_levels, float* out,

@@ -405,8 +405,14 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_dense_kernel(const float* _
                                                                   const float* __restrict__ dy,
                                                                   float* __restrict__ priv, int64_t dense_entries,
                                                                   const float* __restrict__ level_l1, int l_hi,
-                                                                  int32_t* __restrict__ zero_flag) {
+                                                                  int32_t* __restrict__ zero_flag,
+                                                                  int32_t* __restrict__ gate) {
     if (zero_flag && blockIdx.x == 0 && threadIdx.x == 0) *zero_flag = 0;
+    // gate (gate.hip's {signals, waits, ticket}): opened as the table-gradient launches begin, so the
+    // side stream's next march starts beside them with no one-thread signal kernel of its own on
+    // the step's critical path (MFNERF_GATE_AT=grid_bw)
+    if (gate && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_fetch_add(gate, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     __shared__ float fs_s[MFN_MAX_LEVELS];
     // per wave, one entry per run: the 4 rows' (x0, x1) keys and the inclusive prefix at the run's
     // tail of the 16 values as 4 int4 (row r: x0f0, x0f1, x1f0, x1f1).  The runs tile the chunk's
@@ -1447,6 +1453,7 @@ struct AdamRest {
     int n_blocks;        // 0: none
     int first;           // 1: the grid's first n_blocks workgroups (dispatched early), 0: its last
     int64_t lo4;         // first float4 group (0; the MLPs' count when their update rides the slab tail)
+    int32_t* gate;       // opened as the dense-level launch starts (NULL: none)
 };
 
 __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, int64_t n,
@@ -2043,7 +2050,7 @@ int adam_all_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, 
                   const mfnerf_grid_desc* desc, const float* dL_dout, float* grads, int64_t n_params,
                   void* workspace, int64_t n_slots, float* level_l1, const mfnerf_adam_fused* adam,
                   int32_t* step_dev, mfnerf_amp_state* amp, void* packed, int rgb_width, const float* slab,
-                  int slab_rows, mfnerf_stream_t stream) {
+                  int slab_rows, int32_t* gate, mfnerf_stream_t stream) {
     if (slab && ((rgb_width != 64 && rgb_width != 128) || slab_rows <= 0 || !adam || !adam->params)) {
         mfn_set_error("grid_encode_bw_binned_adam_all_slab: bad slab (rgb_width 64 or 128, rows > 0)");
         return MFN_ERR_INVALID;
@@ -2086,7 +2093,7 @@ int adam_all_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, 
         mfn_set_error("grid_encode_bw_binned_adam_all_slab: the MLP weights must precede the table");
         return MFN_ERR_INVALID;
     }
-    AdamRest X{grads, (int*)workspace, 2 * dense_entries_of(desc), total, fused_from / 4, 0, 1, n_dw / 4};
+    AdamRest X{grads, (int*)workspace, 2 * dense_entries_of(desc), total, fused_from / 4, 0, 1, n_dw / 4, gate};
     // <= 256 workgroups, the grid's first (256 vs 64 of them 0.655 vs 0.657 ms/step; first vs last
     // in the grid within noise)
     const int64_t want = div_up<int64_t>((fused_from - n_dw) / 4, ACC_THREADS);
@@ -2121,9 +2128,9 @@ int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32
                                           const mfnerf_grid_desc* desc, const float* dL_dout, float* grads,
                                           int64_t n_params, void* workspace, int64_t n_slots, float* level_l1,
                                           const mfnerf_adam_fused* adam, int32_t* step_dev, mfnerf_amp_state* amp,
-                                          void* packed, int rgb_width, mfnerf_stream_t stream) {
+                                          void* packed, int rgb_width, int32_t* gate, mfnerf_stream_t stream) {
     return adam_all_impl(x, n, n_dev, x_min, x_range, desc, dL_dout, grads, n_params, workspace, n_slots, level_l1,
-                         adam, step_dev, amp, packed, rgb_width, nullptr, 0, stream);
+                         adam, step_dev, amp, packed, rgb_width, nullptr, 0, gate, stream);
 }
 
 int mfnerf_grid_encode_bw_binned_adam_all_slab(const float* x, int64_t n, const int32_t* n_dev, float x_min,
@@ -2131,14 +2138,14 @@ int mfnerf_grid_encode_bw_binned_adam_all_slab(const float* x, int64_t n, const 
                                                float* grads, int64_t n_params, void* workspace, int64_t n_slots,
                                                float* level_l1, const mfnerf_adam_fused* adam, int32_t* step_dev,
                                                mfnerf_amp_state* amp, void* packed, int rgb_width,
-                                               const void* field_workspace, mfnerf_stream_t stream) {
+                                               const void* field_workspace, int32_t* gate, mfnerf_stream_t stream) {
     if (!field_workspace) {
         mfn_set_error("grid_encode_bw_binned_adam_all_slab: null field workspace");
         return MFN_ERR_INVALID;
     }
     return adam_all_impl(x, n, n_dev, x_min, x_range, desc, dL_dout, grads, n_params, workspace, n_slots, level_l1,
                          adam, step_dev, amp, packed, rgb_width, (const float*)field_workspace,
-                         mfnerf_field_bw_slab_rows(rgb_width), stream);
+                         mfnerf_field_bw_slab_rows(rgb_width), gate, stream);
 }
 
 int64_t mfnerf_grid_binned_first_value(const mfnerf_grid_desc* desc) {
@@ -2204,13 +2211,16 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
         auto dk = l_first <= 8 ? grid_bw_dense_kernel<4> : l_first <= 16 ? grid_bw_dense_kernel<8> : grid_bw_dense_kernel<16>;
         hipLaunchKernelGGL(dk, dim3((unsigned)(wb < cap ? wb : cap)), dim3(ENC_BLOCK), 0, stream,
                            x, n, n_dev, x_min, x_range, *desc, dL_dout, W.priv, dense_entries_of(desc), level_l1,
-                           l_first, (parts & 2) ? W.ovf : (int32_t*)nullptr);
+                           l_first, (parts & 2) ? W.ovf : (int32_t*)nullptr, rest ? rest->gate : (int32_t*)nullptr);
     } else if ((parts & 1) && l_first > 0) {  // dense levels [0, l_first): request-shaped atomics, private copies
         auto kern = big ? grid_bw_kernel<MFN_MAX_LEVELS, true> : grid_bw_kernel<16, true>;
         hipLaunchKernelGGL(kern, dim3((unsigned)atomic_blocks), dim3(ENC_BLOCK), 0, stream, x, n, n_dev, x_min,
                            x_range, *desc, dL_dout, grad_table, W.priv, dense_entries_of(desc), level_l1, l_first,
                            (parts & 2) ? W.ovf : (int32_t*)nullptr);
     }
+    // the gate opens here whichever dense path ran (only grid_bw_dense_kernel opens it itself)
+    if (rest && rest->gate && !((parts & 1) && l_first > 0 && l_first <= n_dense_levels))
+        mfnerf_gate_signal(rest->gate, stream);  // (after the request-shaped atomics, or first)
     if ((parts & 2) && P.n_bins > 0) {
         if (!((parts & 1) && l_first > 0)) mfn_zero_async(W.ovf, sizeof(int32_t), stream);
         // the staged dL/dy rows sized for the binned levels (10 at the Lego layout; MixedFeature's

@@ -82,10 +82,10 @@ SIGNATURES = {
     "mfnerf_grid_encode_bw_binned_adam": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _I64,
                                               _P, ctypes.POINTER(AdamFused), _P]),
     "mfnerf_grid_encode_bw_binned_adam_all": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _I64, _P,
-                                                  _I64, _P, ctypes.POINTER(AdamFused), _P, _P, _P, _I, _P]),
+                                                  _I64, _P, ctypes.POINTER(AdamFused), _P, _P, _P, _I, _P, _P]),
     "mfnerf_grid_encode_bw_binned_adam_all_slab": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _I64,
                                                        _P, _I64, _P, ctypes.POINTER(AdamFused), _P, _P, _P, _I, _P,
-                                                       _P]),
+                                                       _P, _P]),
     "mfnerf_grid_binned_first_value": (_I64, [ctypes.POINTER(GridDesc)]),
     "mfnerf_grid_encode_bw_binned_flag_offset": (_I64, [ctypes.POINTER(GridDesc), _I64]),
     "mfnerf_grid_level_l1": (_I, [_P, _I64, _P, _I, _P, _P]),

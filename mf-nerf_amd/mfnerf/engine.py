@@ -488,11 +488,12 @@ class TrainStep:
                          beta2=0.999, eps=float(c.eps), step_dev=self.step_dev.data_ptr(),
                          lr_dev=self.lr_dev.data_ptr(), amp=amp.value if amp is not None else None)
 
-    def _grid_bw(self, mb, q, fuse_adam=False):
+    def _grid_bw(self, mb, q, fuse_adam=False, gate=None):
         """Part q's hash-table gradient scatter (the dominant kernel, alone so it can be timed);
         fuse_adam: with the partitioned tables' Adam step (then _finish_update(partial=True));
         fuse_adam="all": with the whole optimizer step (then only _pack()); "all-slab": the same after
-        a chain with a deferred weight-gradient fold (_chain(defer_fold=True))."""
+        a chain with a deferred weight-gradient fold (_chain(defer_fold=True)); gate (its pointer):
+        opened as the dense-level launch starts."""
         t, m = self.parts[q], mb.part[q]
         if self._binned() and fuse_adam in ("all", "all-slab"):
             self._fused_args = self._adam_fused_args()  # kept alive: graphs capture the call
@@ -502,9 +503,9 @@ class TrainStep:
                     ptr(self.grads), self.n_alloc, ptr(t.grid_ws), self._bin_slots(), ptr(self._level_l1),
                     ctypes.byref(self._fused_args), ptr(self.step_dev), amp, ptr(self.packed), self.cfg.rgb_width)
             if fuse_adam == "all-slab":
-                call("mfnerf_grid_encode_bw_binned_adam_all_slab", *args, ptr(t.field_ws), stream())
+                call("mfnerf_grid_encode_bw_binned_adam_all_slab", *args, ptr(t.field_ws), gate, stream())
             else:
-                call("mfnerf_grid_encode_bw_binned_adam_all", *args, stream())
+                call("mfnerf_grid_encode_bw_binned_adam_all", *args, gate, stream())
             return
         if self._binned() and fuse_adam:
             self._fused_args = self._adam_fused_args()  # kept alive: graphs capture the call
@@ -525,23 +526,29 @@ class TrainStep:
              ptr(self._level_l1) if self._fixed() else None, stream())
 
     def _slab_tail(self):
-        """The one-graph step folds the MLP weight gradients after the scatter, not right after
-        field_bw (mfnerf_grid_encode_bw_binned_adam_all_slab): there the fold ran beside the next
-        step's march, 39 us instead of ~12 (r4f timeline).  MFNERF_SLAB_TAIL=0: the fold in the
-        chain."""
-        return (os.environ.get("MFNERF_SLAB_TAIL", "1") == "1" and os.environ.get("MFNERF_FUSED_ADAM_ALL", "1") == "1"
+        """MFNERF_SLAB_TAIL=1: the one-graph step folds the MLP weight gradients after the scatter
+        (mfnerf_grid_encode_bw_binned_adam_all_slab) instead of right after field_bw.  Off by
+        default: with the gate after field_bw the in-chain fold runs before the march starts (~12 us),
+        and moving it out put the march beside the dense-level scatter instead -- 0.5499-0.5547 vs
+        0.5431-0.5504 ms/step (r4i, r4k2)."""
+        return (os.environ.get("MFNERF_SLAB_TAIL", "0") == "1" and os.environ.get("MFNERF_FUSED_ADAM_ALL", "1") == "1"
                 and self.n_parts == 1)
 
-    def _fused_tail(self, j, slab=False):
+    def _fused_tail(self, j, slab=False, mark=None):
         """The replayed collective-free tail: scatter + every Adam update, then the MLP repack.  By
         default the MLPs' and dense levels' update rides the accumulate's launch
         (mfnerf_grid_encode_bw_binned_adam_all); MFNERF_FUSED_ADAM_ALL=0 keeps it a pass of its own
         after the scatter (mfnerf_adam_step_fixed_partial).  slab: the chain deferred the MLP weight
         gradients' fold (the MLPs' update then runs in the slab tail).  Same bits every way."""
+        mark = mark or (lambda _n: None)
         if slab:
-            self._grid_bw(self.mbuf[j], 0, fuse_adam="all-slab")
+            gate = getattr(mark, "ride", lambda _n: None)("grid_bw")
+            self._grid_bw(self.mbuf[j], 0, fuse_adam="all-slab", gate=gate)
+            mark("grid_bw")
         elif os.environ.get("MFNERF_FUSED_ADAM_ALL", "1") == "1":
-            self._grid_bw(self.mbuf[j], 0, fuse_adam="all")  # + the repack
+            gate = getattr(mark, "ride", lambda _n: None)("grid_bw")
+            self._grid_bw(self.mbuf[j], 0, fuse_adam="all", gate=gate)  # + the repack
+            mark("grid_bw")
         else:
             self._grid_bw(self.mbuf[j], 0, fuse_adam=True)
             self._finish_update(partial=True)
@@ -787,6 +794,7 @@ class TrainStep:
                 self._pack()  # the previous step's all-gathered / updated fp16 weights
                 self._chain(self._static[j], self.mbuf[j], 0, mark)
                 self._grid_bw_float(self.mbuf[j])
+                mark("grid_bw")  # (MFNERF_GATE_AT=grid_bw: here, after the whole scatter)
                 if amp:  # the non-finite flag rides the collective: NaN into every shard's first value
                     call("mfnerf_flag_to_shards", ptr(self.grads), n_sh, w, ptr(self.finite_status), stream())
 
@@ -834,7 +842,7 @@ class TrainStep:
                 def step(j):
                     self._chain(self._static[j], self.mbuf[j], 0, signal_at, defer_fold=slab)
                     if fuse:
-                        self._fused_tail(j, slab=slab)
+                        self._fused_tail(j, slab=slab, mark=signal_at)
                     else:
                         self._grid_bw(self.mbuf[j], 0)
                         tail()
@@ -849,8 +857,12 @@ class TrainStep:
         # (0.601 vs 0.601 ms/step) but, once an RCCL communicator exists in the process, it ran every
         # step at 1.10 ms (kernels on the main queue 2-7x slower; GPU_MAX_HW_QUEUES=8 also cured it:
         # the extra streams share hardware queues) -- the data-parallel step would pay it on every rank
+        # MFNERF_SIDE_PRIORITY=low: the least priority the runtime offers (A/B: does a low-priority
+        # queue keep the march's 8192 waves from taking the scatter's wave slots?)
         hi = os.environ.get("MFNERF_SIDE_HIGH_PRIORITY", "0") == "1"
-        self._side = torch.cuda.Stream(device=self.dev, priority=torch.cuda.Stream.priority_range()[1] if hi else 0)
+        lo = os.environ.get("MFNERF_SIDE_PRIORITY", "normal") == "low"
+        least, greatest = torch.cuda.Stream.priority_range()
+        self._side = torch.cuda.Stream(device=self.dev, priority=greatest if hi else least if lo else 0)
         # gated marches wait as a stream operation (mfnerf_gate_wait_stream) on the count of signals
         # the host has enqueued; MFNERF_GATE_STREAM=0: the captured one-thread polling kernel
         self._gate_stream = gated and os.environ.get("MFNERF_GATE_STREAM", "1") == "1"
@@ -867,14 +879,17 @@ class TrainStep:
 
     def _gate_signaller(self):
         """mark() for the gated graphs: signals the device gate after the chain stage named by
-        MFNERF_GATE_AT (default "composite": the next draw + march start beside field_bw, whose one
-        wave per SIMD leaves room and issue cycles for the march's waves -- 0.687 -> 0.672 ms/step
-        against opening after the whole chain ("field_bw"); "field_fw" 0.677); counts its signals."""
+        MFNERF_GATE_AT (default "grid_bw", since round 4: the next draw + march start as the
+        table-gradient launches begin -- opened by the dense-level launch's first workgroup, no
+        signal kernel of its own -- after field_bw and its weight-gradient fold: 0.5469-0.5485 ms/step
+        vs 0.5475-0.5496 for "field_bw" (a signal kernel after the fold) and 0.5526-0.5581 for
+        "composite", which round 2 preferred when field_bw ran one wave per SIMD and left room beside
+        it; at the END of the dense-level launch 0.576; r4i, r4k2, r4l); counts its signals."""
         self._gate = torch.zeros(4, dtype=torch.int32, device=self.dev)  # {signals, waits, ticket, -}
         gp = ptr(self._gate)
-        gate_at = os.environ.get("MFNERF_GATE_AT", "composite")
-        if gate_at not in ("grid_fw", "field_fw", "composite", "field_bw"):
-            raise ValueError(f"MFNERF_GATE_AT={gate_at!r}: one of grid_fw, field_fw, composite, field_bw")
+        gate_at = os.environ.get("MFNERF_GATE_AT", "grid_bw")
+        if gate_at not in ("grid_fw", "field_fw", "composite", "field_bw", "grid_bw"):
+            raise ValueError(f"MFNERF_GATE_AT={gate_at!r}: one of grid_fw, field_fw, composite, field_bw, grid_bw")
         # with the distortion loss the chain composites in two stages: the gate opens after the
         # second ("composite_bw"), the same place as after the fused kernel
         name_ = "composite_bw" if gate_at == "composite" and self.cfg.lambda_distortion > 0 else gate_at

@@ -319,6 +319,30 @@ def test_gated_replay_with_distortion_loss_keeps_the_gate_in_step(gpu):
     assert torch.equal(a.params, b.params) and torch.equal(a.p16, b.p16)
 
 
+@pytest.mark.parametrize("gate_at,ride,stream_wait", [("composite", "1", "1"), ("composite", "0", "0"),
+                                                      ("field_bw", "1", "1"), ("grid_bw", "1", "1"),
+                                                      ("grid_bw", "1", "0"), ("grid_bw", "0", "1")])
+def test_gate_positions_replay_like_eager(gpu, monkeypatch, gate_at, ride, stream_wait):
+    """Every gate position (the signal riding the compositing / dense-level launch or a kernel of its
+    own; the march waiting as a stream operation or by the polling kernel): the gated replays open and
+    consume the gate once per step and stay bit-identical to eager steps."""
+    monkeypatch.setenv("MFNERF_GATE_AT", gate_at)
+    monkeypatch.setenv("MFNERF_GATE_RIDE", ride)
+    monkeypatch.setenv("MFNERF_GATE_STREAM", stream_wait)
+    K = 5
+    a, b = _make(gpu, 1), _make(gpu, 1)
+    batches = a.make_batches(K + 1, seed=13)
+    for k in range(K):
+        b.run(batches[k])
+    a.run(batches[0])
+    a.capture()
+    for k in range(1, K):
+        a.replay(batches[k], next_batch=batches[k + 1] if k + 1 < K else None)
+    torch.cuda.synchronize()
+    assert _gate_state(a) == (K - 2, K - 2)
+    assert torch.equal(a.params, b.params) and torch.equal(a.p16, b.p16) and torch.equal(a.m, b.m)
+
+
 def test_gate_position_is_validated(gpu, monkeypatch):
     st = _make(gpu, 1)
     st.run(st.make_batches(1, seed=1)[0])

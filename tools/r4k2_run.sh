@@ -1,0 +1,16 @@
+set -o pipefail
+D=gpurun_out/r4k2
+mkdir -p $D
+export TMPDIR=/tmp
+ok() { rc=$?; [ $rc -le 1 ] || exit $rc; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_engine.py -v --timeout 300 --timeout-method thread -p no:cacheprovider > $D/tests.log 2>&1; ok
+B="timeout -k 10 200 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --roofline-every 1000"
+for rep in 1 2; do
+for V in "grid_bw_dense 1 1" "field_bw 0 1" "field_bw 1 1" "composite 1 1"; do
+  set -- $V
+  MFNERF_GATE_AT=$1 MFNERF_SLAB_TAIL=$2 MFNERF_GATE_RIDE=$3 $B > $D/ab.json 2> $D/ab.err || exit $?
+  python -c "import json;d=json.load(open('$D/ab.json'));print('gate=$1 slab=$2 ride=$3',d['ms_per_step'],d['grid_bw_ms'])" >> $D/ab.txt
+done
+done
+cd /tmp && MFNERF_GATE_AT=grid_bw_dense timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$D/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 40 --warmup 10 --no-cpu-baseline --roofline-every 1000 > $GRAFT_REPO_ROOT/$D/prof.log 2>&1 && cd $GRAFT_REPO_ROOT && \
+python tools/step_timeline.py $D/prof > $D/timeline.txt
