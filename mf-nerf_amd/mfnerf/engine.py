@@ -793,8 +793,8 @@ class TrainStep:
             def dp_pre(j, mark):
                 self._pack()  # the previous step's all-gathered / updated fp16 weights
                 self._chain(self._static[j], self.mbuf[j], 0, mark)
+                mark("grid_bw")  # (MFNERF_GATE_AT=grid_bw: a signal kernel as the scatter begins)
                 self._grid_bw_float(self.mbuf[j])
-                mark("grid_bw")  # (MFNERF_GATE_AT=grid_bw: here, after the whole scatter)
                 if amp:  # the non-finite flag rides the collective: NaN into every shard's first value
                     call("mfnerf_flag_to_shards", ptr(self.grads), n_sh, w, ptr(self.finite_status), stream())
 
@@ -857,15 +857,17 @@ class TrainStep:
         # (0.601 vs 0.601 ms/step) but, once an RCCL communicator exists in the process, it ran every
         # step at 1.10 ms (kernels on the main queue 2-7x slower; GPU_MAX_HW_QUEUES=8 also cured it:
         # the extra streams share hardware queues) -- the data-parallel step would pay it on every rank
-        # MFNERF_SIDE_PRIORITY=low: the least priority the runtime offers (A/B: does a low-priority
-        # queue keep the march's 8192 waves from taking the scatter's wave slots?)
+        # (no priority below normal exists here: torch.cuda.Stream.priority_range() is (0, -1) on this
+        # ROCm, r4m -- a "least" priority side stream measured the same as normal)
         hi = os.environ.get("MFNERF_SIDE_HIGH_PRIORITY", "0") == "1"
-        lo = os.environ.get("MFNERF_SIDE_PRIORITY", "normal") == "low"
-        least, greatest = torch.cuda.Stream.priority_range()
-        self._side = torch.cuda.Stream(device=self.dev, priority=greatest if hi else least if lo else 0)
-        # gated marches wait as a stream operation (mfnerf_gate_wait_stream) on the count of signals
-        # the host has enqueued; MFNERF_GATE_STREAM=0: the captured one-thread polling kernel
-        self._gate_stream = gated and os.environ.get("MFNERF_GATE_STREAM", "1") == "1"
+        self._side = torch.cuda.Stream(device=self.dev, priority=torch.cuda.Stream.priority_range()[1] if hi else 0)
+        # MFNERF_GATE_STREAM=1: gated marches wait as a stream operation (mfnerf_gate_wait_stream) on
+        # the count of signals the host has enqueued -- 5 us/step faster (r4h), but it has no timeout:
+        # under rocprofv3 --pmc (dispatches serialised) it deadlocked the step (r4z2), and a side
+        # stream sharing a hardware queue with the main one (more streams than GPU_MAX_HW_QUEUES = 4,
+        # e.g. beside RCCL's) would block the very kernel that releases it.  Default: the captured
+        # polling kernel, which gives up after GATE_TIMEOUT_US.
+        self._gate_stream = gated and os.environ.get("MFNERF_GATE_STREAM", "0") == "1"
         self._gate_target = 0
         self._part_streams = [None] + [torch.cuda.Stream(device=self.dev) for _ in range(P - 1)]
         self._ev_march = [torch.cuda.Event(), torch.cuda.Event()]
