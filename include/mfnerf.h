@@ -341,6 +341,14 @@ int mfnerf_field_pack_weights_f16(const void* params_xyz_f16, const void* params
  * dirs (n,3) f32 (ignored when density_only) -> sigma (n) f32, rgb (n,3) f32. */
 int mfnerf_field_fw(const void* feat_f16, int64_t feat_plane_stride, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
                     int rgb_width, int density_only, float* sigma, float* rgb, mfnerf_stream_t stream);
+/* The occupancy refresh's density query (networks.py:252-259, `density_grid_tmp[c, indices] =
+ * self.density(xyzs)`): mfnerf_field_fw density_only over min(n, *n_dev) points, each sigma also
+ * written to tmp[cell_idx[i]] (skipped for cell_idx < 0) -- the update's scatter in the same launch
+ * (then call mfnerf_occupancy_update_dev with n_points = 0).  Duplicate cells: unordered, like
+ * the reference's index_put; the engine's probes are distinct (mfnerf_occupancy_cells_unique). */
+int mfnerf_field_fw_density_scatter(const void* feat_f16, int64_t feat_plane_stride, int64_t n, const int32_t* n_dev,
+                                    const void* packed, int rgb_width, float* sigma, const int32_t* cell_idx,
+                                    float* tmp, mfnerf_stream_t stream);
 
 /* Backward of mfnerf_field_fw (recomputes the forward; same feat layouts).  dL_dsigma (n), dL_drgb (n,3) f32 ->
  * dL_dfeat (n,32) f32, and ADDS the weight grads into grad_xyz / grad_rgb (tcnn layout f32).
@@ -431,7 +439,8 @@ int mfnerf_occupancy_update(float* density_grid, const float* sigmas, const int3
  * mfnerf_occupancy_points_unique(...)).  The set of probed cells is exactly the set the plain call
  * with the same seed and call index draws.  Deterministic.  The workspace must be zero-filled before
  * its first use (the call leaves its byte map zeroed); cascades*G^3 must be a multiple of 16.
- * mfnerf_occupancy_update_dev: mfnerf_occupancy_update over the first min(n_points, *n_dev) points. */
+ * mfnerf_occupancy_update_dev: mfnerf_occupancy_update over the first min(n_points, *n_dev) points;
+ * tmp_zero = 1 promises tmp is all-zero on entry and leaves it zero (no fill launch). */
 int64_t mfnerf_occupancy_points_unique(int cascades, int grid_size, int64_t n_uniform, int warmup);
 int mfnerf_occupancy_cells_unique(const float* density_grid, int cascades, int grid_size, float scale,
                                   int64_t n_uniform, int warmup, float density_threshold, uint64_t seed,
@@ -443,8 +452,8 @@ int mfnerf_occupancy_cells_unique_dev(const float* density_grid, int cascades, i
                                       void* workspace, mfnerf_stream_t stream);
 int mfnerf_occupancy_update_dev(float* density_grid, const float* sigmas, const int32_t* cell_idx, int64_t n_points,
                                 const int32_t* n_dev, int cascades, int grid_size, float decay, const float* count_grid,
-                                float density_threshold, float* tmp, uint8_t* bitfield, void* workspace,
-                                mfnerf_stream_t stream);
+                                float density_threshold, float* tmp, int tmp_zero, uint8_t* bitfield,
+                                void* workspace, mfnerf_stream_t stream);
 
 /* ---------------------------------------------------------------- training batch */
 

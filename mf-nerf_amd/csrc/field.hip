@@ -345,7 +345,9 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_fw_kernel(const _Float16* _
                                                                 const float* __restrict__ dirs, int64_t n,
                                                                 const int32_t* __restrict__ n_dev,
                                                                 const _Float16* __restrict__ packed,
-                                                                float* __restrict__ sigma, float* __restrict__ rgb) {
+                                                                float* __restrict__ sigma, float* __restrict__ rgb,
+                                                                const int32_t* __restrict__ cell,
+                                                                float* __restrict__ cell_out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     _Float16* lds = reinterpret_cast<_Float16*>(smem);
     load_frags(lds, packed, DENSITY_ONLY ? 8 : Geo<W>::N_FW);
@@ -373,7 +375,12 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_fw_kernel(const _Float16* _
         for (int q = 0; q < P; ++q) {
             const int64_t s = (tile + q * stride) * 32 + r;
             if (valid[q] && h == 0) {
-                sigma[s] = __expf(T[q].h0);  // TruncExp forward (custom_functions.py:166)
+                const float sg = __expf(T[q].h0);  // TruncExp forward (custom_functions.py:166)
+                sigma[s] = sg;
+                if (DENSITY_ONLY && cell_out) {  // the occupancy refresh's density_grid_tmp[cell] = sigma
+                    const int32_t k = cell[s];
+                    if (k >= 0) cell_out[k] = sg;
+                }
                 if (!DENSITY_ONLY) {
                     // tcnn returns fp16 rgb; the reference casts it to fp32 for compositing
                     rgb[3 * s] = (float)(_Float16)T[q].rgb[0];
@@ -1350,17 +1357,19 @@ void launch_pack(const TP* px, const TP* pr, void* packed, mfnerf_stream_t strea
 
 template <int W>
 void launch_fw(const void* feat, int64_t ps, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
-               int density_only, float* sigma, float* rgb, mfnerf_stream_t stream) {
+               int density_only, float* sigma, float* rgb, mfnerf_stream_t stream, const int32_t* cell = nullptr,
+               float* cell_out = nullptr) {
     const int64_t tiles = div_up<int64_t>(n, 32);
     const int64_t want = div_up<int64_t>(tiles, 4);
     const unsigned blocks = (unsigned)(want < 2048 ? want : 2048);
     if (density_only)
         hipLaunchKernelGGL((field_fw_kernel<W, true>), dim3(blocks), dim3(FIELD_BLOCK), 8 * FRAG_HALFS * 2, stream,
-                           (const _Float16*)feat, ps, dirs, n, n_dev, (const _Float16*)packed, sigma, rgb);
+                           (const _Float16*)feat, ps, dirs, n, n_dev, (const _Float16*)packed, sigma, rgb, cell,
+                           cell_out);
     else
         hipLaunchKernelGGL((field_fw_kernel<W, false>), dim3(blocks), dim3(FIELD_BLOCK),
                            (size_t)Geo<W>::N_FW * FRAG_HALFS * 2, stream, (const _Float16*)feat, ps, dirs, n, n_dev,
-                           (const _Float16*)packed, sigma, rgb);
+                           (const _Float16*)packed, sigma, rgb, nullptr, nullptr);
 }
 
 template <int W, int NW>
@@ -1477,6 +1486,24 @@ int mfnerf_field_fw(const void* feat_f16, int64_t feat_plane_stride, const float
     if (rgb_width == 64) launch_fw<64>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, density_only, sigma, rgb, stream);
     else launch_fw<128>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, density_only, sigma, rgb, stream);
     return mfn_check_launch("field_fw");
+}
+
+int mfnerf_field_fw_density_scatter(const void* feat_f16, int64_t feat_plane_stride, int64_t n, const int32_t* n_dev,
+                                    const void* packed, int rgb_width, float* sigma, const int32_t* cell_idx,
+                                    float* tmp, mfnerf_stream_t stream) {
+    if (!width_ok(rgb_width)) return bad_width(rgb_width);
+    if (n < 0 || (feat_plane_stride != 0 && feat_plane_stride < n)) {
+        mfn_set_error("field_fw_density_scatter: bad size");
+        return MFN_ERR_INVALID;
+    }
+    if (n == 0) return MFN_OK;
+    if (!feat_f16 || !packed || !sigma || !cell_idx || !tmp) {
+        mfn_set_error("field_fw_density_scatter: null pointer");
+        return MFN_ERR_INVALID;
+    }
+    if (rgb_width == 64) launch_fw<64>(feat_f16, feat_plane_stride, nullptr, n, n_dev, packed, 1, sigma, nullptr, stream, cell_idx, tmp);
+    else launch_fw<128>(feat_f16, feat_plane_stride, nullptr, n, n_dev, packed, 1, sigma, nullptr, stream, cell_idx, tmp);
+    return mfn_check_launch("field_fw_density_scatter");
 }
 
 int mfnerf_field_bw_slab_rows(int rgb_width) {

@@ -122,6 +122,8 @@ struct PointsArgs {
     uint64_t key;
     uint64_t seed;
     const uint64_t* call_dev;  // non-null: key from the device-resident call index (graph replays)
+    uint64_t call_lag;         // the index was already advanced by this much (the probe kernel reads it
+                               // after the marked-cell compaction advanced it)
 };
 
 // draw p's cell: cascade c, morton m; ok = false for an occupied draw from an empty set
@@ -166,7 +168,7 @@ __global__ __launch_bounds__(OCC_BLOCK) void occ_points_kernel(PointsArgs a, con
                                                                const int32_t* __restrict__ counts,
                                                                float* __restrict__ xyzs, int32_t* __restrict__ cell) {
     const int64_t n = (int64_t)a.cascades * a.per_cascade;
-    if (a.call_dev) a.key = splitmix64_host(splitmix64_host(a.seed ^ OCC_SEED_MIX) ^ *a.call_dev);
+    if (a.call_dev) a.key = splitmix64_host(splitmix64_host(a.seed ^ OCC_SEED_MIX) ^ (*a.call_dev - a.call_lag));
     for (int64_t p = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; p < n; p += (int64_t)gridDim.x * OCC_BLOCK) {
         int c;
         uint32_t m;
@@ -189,7 +191,7 @@ __global__ __launch_bounds__(OCC_BLOCK) void occ_mark_kernel(PointsArgs a, const
                                                              const int32_t* __restrict__ counts,
                                                              uint8_t* __restrict__ mark) {
     const int64_t n = (int64_t)a.cascades * a.per_cascade;
-    if (a.call_dev) a.key = splitmix64_host(splitmix64_host(a.seed ^ OCC_SEED_MIX) ^ *a.call_dev);
+    if (a.call_dev) a.key = splitmix64_host(splitmix64_host(a.seed ^ OCC_SEED_MIX) ^ (*a.call_dev - a.call_lag));
     for (int64_t p = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; p < n; p += (int64_t)gridDim.x * OCC_BLOCK) {
         int c;
         uint32_t m;
@@ -217,7 +219,12 @@ __global__ __launch_bounds__(OCC_BLOCK) void occ_mark_count_kernel(const uint8_t
 __global__ __launch_bounds__(OCC_BLOCK) void occ_mark_compact_kernel(uint8_t* __restrict__ mark, int64_t total,
                                                                      const int32_t* __restrict__ block_counts,
                                                                      int32_t* __restrict__ list,
-                                                                     int32_t* __restrict__ count) {
+                                                                     int32_t* __restrict__ count,
+                                                                     uint64_t* __restrict__ call_dev) {
+    // the draws' device call index advanced here: every read of it for these draws (the mark
+    // kernel) is done, and the probe kernel after this reads it with call_lag 1 -- no launch of its own
+    if (call_dev && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_fetch_add(call_dev, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __shared__ int lds[OCC_BLOCK / 64];
     __shared__ int wave_tot[OCC_BLOCK / 64];
     const int b = blockIdx.x, nblk = gridDim.x;
@@ -261,7 +268,7 @@ __global__ __launch_bounds__(OCC_BLOCK) void occ_unique_points_kernel(PointsArgs
                                                                       const int32_t* __restrict__ count,
                                                                       float* __restrict__ xyzs,
                                                                       int32_t* __restrict__ cell) {
-    if (a.call_dev) a.key = splitmix64_host(splitmix64_host(a.seed ^ OCC_SEED_MIX) ^ *a.call_dev);
+    if (a.call_dev) a.key = splitmix64_host(splitmix64_host(a.seed ^ OCC_SEED_MIX) ^ (*a.call_dev - a.call_lag));
     const uint64_t jkey = splitmix64_host(a.key ^ OCC_JITTER_MIX);
     const int64_t n = *count;
     for (int64_t i = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * OCC_BLOCK) {
@@ -302,18 +309,19 @@ __device__ __forceinline__ float decay_cell(float v, float t, const float* __res
 }
 
 // four cells per thread per step (float4), every load of a thread's slice issued before the math
-__global__ __launch_bounds__(OCC_BLOCK) void occ_decay_kernel(float* __restrict__ grid, const float* __restrict__ tmp,
+__global__ __launch_bounds__(OCC_BLOCK) void occ_decay_kernel(float* __restrict__ grid, float* __restrict__ tmp,
                                                               const float* __restrict__ count_grid, int64_t n,
-                                                              float decay, OccStats* __restrict__ st) {
+                                                              float decay, OccStats* __restrict__ st, int zero_tmp) {
     __shared__ double lds_d[OCC_BLOCK / 64];
     __shared__ unsigned long long lds_u[OCC_BLOCK / 64];
     double s = 0.0;
     unsigned long long k = 0;
     float4* g4 = reinterpret_cast<float4*>(grid);
-    const float4* t4 = reinterpret_cast<const float4*>(tmp);
+    float4* t4 = reinterpret_cast<float4*>(tmp);
     for (int64_t i = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; i < n / 4; i += (int64_t)gridDim.x * OCC_BLOCK) {
         float4 v = g4[i];
         const float4 t = t4[i];
+        if (zero_tmp) t4[i] = make_float4(0.f, 0.f, 0.f, 0.f);  // left zero for the next refresh
         v.x = decay_cell(v.x, t.x, count_grid, 4 * i, decay);
         v.y = decay_cell(v.y, t.y, count_grid, 4 * i + 1, decay);
         v.z = decay_cell(v.z, t.z, count_grid, 4 * i + 2, decay);
@@ -337,6 +345,40 @@ __global__ __launch_bounds__(OCC_BLOCK) void occ_decay_kernel(float* __restrict_
 
 // thr = min(mean, threshold) with Python's min(): NaN mean (no positive cell) stays NaN.  One wave:
 // the partials of nb <= DECAY_BLOCKS workgroups summed in a fixed lane / tree order.
+// occ_thr_pack_kernel: thr + packbits in one launch (the refresh's form): every workgroup's first
+// wave derives thr from the partials in that order, workgroup 0 also stores it, then the workgroup
+// packs its bytes (the partials are 16 KB, L2-resident; <= 256 workgroups re-read them).
+__global__ __launch_bounds__(256) void occ_thr_pack_kernel(OccStats* st, int nb, float threshold,
+                                                           const float* __restrict__ grid, int64_t n_bytes,
+                                                           uint8_t* __restrict__ bits) {
+    __shared__ float thr_s;
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        double s = 0.0;
+        unsigned long long k = 0;
+        for (int b = lane; b < nb; b += 64) { s += st->sum[b]; k += st->count[b]; }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            s += __shfl_xor(s, off, 64);
+            k += __shfl_xor(k, off, 64);
+        }
+        if (lane == 0) {
+            const float mean = k ? (float)(s / (double)k) : __builtin_nanf("");
+            thr_s = (threshold < mean) ? threshold : mean;
+            if (blockIdx.x == 0) st->thr = thr_s;
+        }
+    }
+    __syncthreads();
+    const float t = thr_s;
+    for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < n_bytes; m += (int64_t)gridDim.x * blockDim.x) {
+        const float4 a = reinterpret_cast<const float4*>(grid)[2 * m];
+        const float4 b = reinterpret_cast<const float4*>(grid)[2 * m + 1];
+        const uint32_t v = (a.x > t) | ((a.y > t) << 1) | ((a.z > t) << 2) | ((a.w > t) << 3) |
+                           ((b.x > t) << 4) | ((b.y > t) << 5) | ((b.z > t) << 6) | ((b.w > t) << 7);
+        bits[m] = (uint8_t)v;
+    }
+}
+
 __global__ void occ_thr_kernel(OccStats* st, int nb, float threshold) {
     const int lane = threadIdx.x;
     double s = 0.0;
@@ -451,7 +493,8 @@ int mfnerf_occupancy_cells_unique_dev(const float* density_grid, int cascades, i
     const int st = occupancy_cells_impl(density_grid, cascades, grid_size, scale, n_uniform, warmup, density_threshold,
                                         seed, 0, call_index_dev, xyzs, cell_idx, workspace, stream, count_dev);
     if (st) return st;
-    hipLaunchKernelGGL(occ_call_bump_kernel, dim3(1), dim3(64), 0, stream, call_index_dev);
+    if (warmup)  // (otherwise the marked-cell compaction advanced it)
+        hipLaunchKernelGGL(occ_call_bump_kernel, dim3(1), dim3(64), 0, stream, call_index_dev);
     return mfn_check_launch("occupancy_cells_unique_dev");
 }
 
@@ -498,6 +541,7 @@ int occupancy_cells_impl(const float* density_grid, int cascades, int grid_size,
     a.key = splitmix64_host(splitmix64_host(seed ^ OCC_SEED_MIX) ^ call_index);
     a.seed = seed;
     a.call_dev = call_dev;
+    a.call_lag = 0;
     const int64_t n = (int64_t)cascades * a.per_cascade;
     if (unique_count && !warmup) {
         if (((int64_t)cascades * cells) % 16) {
@@ -509,7 +553,8 @@ int occupancy_cells_impl(const float* density_grid, int cascades, int grid_size,
         hipLaunchKernelGGL(occ_mark_kernel, dim3(blocks_for(n)), dim3(OCC_BLOCK), 0, stream, a, w.list, w.counts, w.mark);
         hipLaunchKernelGGL(occ_mark_count_kernel, dim3(ub), dim3(OCC_BLOCK), 0, stream, w.mark, total, w.ublock);
         hipLaunchKernelGGL(occ_mark_compact_kernel, dim3(ub), dim3(OCC_BLOCK), 0, stream, w.mark, total, w.ublock, w.ulist,
-                           unique_count);
+                           unique_count, call_dev);
+        if (call_dev) a.call_lag = 1;
         const int64_t cap = n < total ? n : total;
         hipLaunchKernelGGL(occ_unique_points_kernel, dim3(blocks_for(cap)), dim3(OCC_BLOCK), 0, stream, a, w.ulist,
                            unique_count, xyzs, cell_idx);
@@ -529,12 +574,12 @@ int mfnerf_occupancy_update(float* density_grid, const float* sigmas, const int3
                             int cascades, int grid_size, float decay, const float* count_grid, float density_threshold,
                             float* tmp, uint8_t* bitfield, void* workspace, mfnerf_stream_t stream) {
     return mfnerf_occupancy_update_dev(density_grid, sigmas, cell_idx, n_points, nullptr, cascades, grid_size, decay,
-                                       count_grid, density_threshold, tmp, bitfield, workspace, stream);
+                                       count_grid, density_threshold, tmp, 0, bitfield, workspace, stream);
 }
 
 int mfnerf_occupancy_update_dev(float* density_grid, const float* sigmas, const int32_t* cell_idx, int64_t n_points,
                                 const int32_t* n_dev, int cascades, int grid_size, float decay, const float* count_grid,
-                                float density_threshold, float* tmp, uint8_t* bitfield, void* workspace,
+                                float density_threshold, float* tmp, int tmp_zero, uint8_t* bitfield, void* workspace,
                                 mfnerf_stream_t stream) {
     if (bad_grid(cascades, grid_size)) { mfn_set_error("occupancy_update: bad cascades/grid_size"); return MFN_ERR_INVALID; }
     if (n_points < 0) { mfn_set_error("occupancy_update: bad n_points"); return MFN_ERR_INVALID; }
@@ -545,17 +590,21 @@ int mfnerf_occupancy_update_dev(float* density_grid, const float* sigmas, const 
     Ws w;
     ws_layout(cascades, grid_size, (char*)workspace, &w);
     const int64_t n = (int64_t)cascades * grid_size * grid_size * grid_size;
-    mfn_zero_async(tmp, n * sizeof(float), stream);
+    if (((uintptr_t)density_grid) & 15) {
+        mfn_set_error("occupancy_update: density grid must be 16-byte aligned");
+        return MFN_ERR_INVALID;
+    }
+    if (!tmp_zero) mfn_zero_async(tmp, n * sizeof(float), stream);  // (tmp_zero: zero on entry already)
     if (n_points)
         hipLaunchKernelGGL(occ_scatter_kernel, dim3(blocks_for(n_points)), dim3(OCC_BLOCK), 0, stream, sigmas, cell_idx,
                            n_points, n_dev, tmp);
     const int nb = (int)blocks_for(n, DECAY_BLOCKS);  // every partial written (grid-stride beyond)
     hipLaunchKernelGGL(occ_decay_kernel, dim3(nb), dim3(OCC_BLOCK), 0, stream, density_grid, tmp, count_grid, n,
-                       decay, w.stats);
-    hipLaunchKernelGGL(occ_thr_kernel, dim3(1), dim3(64), 0, stream, w.stats, nb, density_threshold);
-    int st = mfn_check_launch("occupancy_update");
-    if (st) return st;
-    return mfnerf_packbits(density_grid, n / 8, 0.0f, &w.stats->thr, bitfield, stream);
+                       decay, w.stats, tmp_zero);
+    const int64_t nbytes = n / 8, pb = blocks_for(nbytes, 256);
+    hipLaunchKernelGGL(occ_thr_pack_kernel, dim3((unsigned)pb), dim3(256), 0, stream, w.stats, nb, density_threshold,
+                       density_grid, nbytes, bitfield);
+    return mfn_check_launch("occupancy_update");
 }
 
 }  // extern "C"

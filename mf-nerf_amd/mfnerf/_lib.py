@@ -94,6 +94,7 @@ SIGNATURES = {
     "mfnerf_sh4_fw": (_I, [_P, _I64, _P, _P]),
     "mfnerf_field_pack_weights": (_I, [_P, _P, _I, _P, _P]),
     "mfnerf_field_fw": (_I, [_P, _I64, _P, _I64, _P, _P, _I, _I, _P, _P, _P]),
+    "mfnerf_field_fw_density_scatter": (_I, [_P, _I64, _I64, _P, _P, _I, _P, _P, _P, _P]),
     "mfnerf_field_bw_workspace": (_I64, [_I64, _I]),
     "mfnerf_field_bw_slab_rows": (_I, [_I]),
     "mfnerf_field_bw": (_I, [_P, _I64, _P, _I64, _P, _P, _I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P]),
@@ -106,7 +107,7 @@ SIGNATURES = {
     "mfnerf_occupancy_cells_unique": (_I, [_P, _I, _I, _F, _I64, _I, _F, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P,
                                            _P, _P]),
     "mfnerf_occupancy_cells_unique_dev": (_I, [_P, _I, _I, _F, _I64, _I, _F, ctypes.c_uint64, _P, _P, _P, _P, _P, _P]),
-    "mfnerf_occupancy_update_dev": (_I, [_P, _P, _P, _I64, _P, _I, _I, _F, _P, _F, _P, _P, _P, _P]),
+    "mfnerf_occupancy_update_dev": (_I, [_P, _P, _P, _I64, _P, _I, _I, _F, _P, _F, _P, _I, _P, _P, _P]),
     "mfnerf_sample_rays": (_I, [_P, _P, _P, _I64, _I64, _I64, _I, ctypes.c_uint64, _P, _P, _P, _P, _P]),
     "mfnerf_sample_rays_prep": (_I, [_P, _P, _P, _I64, _I64, _I64, _I, ctypes.c_uint64, _P, _P, _P, _P, _F, _P, _P,
                                      _P]),

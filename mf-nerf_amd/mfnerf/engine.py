@@ -1070,7 +1070,7 @@ class TrainStep:
             o.cell = torch.empty(n, dtype=torch.int32, device=self.dev)
             o.feat = torch.empty(c.L, n, c.F, dtype=torch.float16, device=self.dev)  # level planes
             o.sigma = torch.empty(n, dtype=torch.float32, device=self.dev)
-            o.tmp = torch.empty(C * G ** 3, dtype=torch.float32, device=self.dev)
+            o.tmp = torch.zeros(C * G ** 3, dtype=torch.float32, device=self.dev)  # kept zero by the decay
             o.ws = torch.zeros(lib.mfnerf_occupancy_workspace(C, G), dtype=torch.uint8, device=self.dev)
             o.count = torch.zeros(1, dtype=torch.int32, device=self.dev)  # probed (distinct) cells
             o.calls = torch.zeros(1, dtype=torch.int64, device=self.dev)  # the draws' call index (device)
@@ -1080,8 +1080,8 @@ class TrainStep:
 
     @torch.no_grad()
     def update_density_grid(self, warmup=False, decay=0.95, count_grid=None, seed=0):
-        """NGP.update_density_grid(0.01*MAX_SAMPLES/sqrt(3), warmup, erode) as five device launches
-        (cells -> grid_encode_fw -> field_fw density-only -> scatter/decay/mean -> packbits); no
+        """NGP.update_density_grid(0.01*MAX_SAMPLES/sqrt(3), warmup, erode) as device launches only
+        (cells -> grid_encode_fw -> field_fw density-only + scatter -> decay/mean -> thr + packbits); no
         host synchronisation.  Without erosion (count_grid) the launches are captured once per
         (warmup, decay, seed) and replayed as one HIP graph (the draws' call index lives on the
         device, so every replay draws new cells): 0.45 ms of mostly launch overhead eagerly
@@ -1113,8 +1113,8 @@ class TrainStep:
              seed, ptr(o.calls), ptr(o.xyz), ptr(o.cell), ptr(o.count), ptr(o.ws), s)
         call("mfnerf_grid_encode_fw_planar", ptr(o.xyz), n, ptr(o.count), self.x_min, self.x_range, self.desc,
              ptr(self.p16[self.off_table:]), ptr(o.feat), o.n_max, s)
-        call("mfnerf_field_fw", ptr(o.feat), o.n_max, None, n, ptr(o.count), ptr(self.packed), c.rgb_width, 1,
-             ptr(o.sigma), None, s)
-        call("mfnerf_occupancy_update_dev", ptr(self.density_grid), ptr(o.sigma), ptr(o.cell), n, ptr(o.count), C, G,
-             float(decay), ptr(count_grid) if count_grid is not None else None, thr, ptr(o.tmp), ptr(self.bitfield),
-             ptr(o.ws), s)
+        # sigma + density_grid_tmp[cell] = sigma in one launch; the update then starts at the decay
+        call("mfnerf_field_fw_density_scatter", ptr(o.feat), o.n_max, n, ptr(o.count), ptr(self.packed), c.rgb_width,
+             ptr(o.sigma), ptr(o.cell), ptr(o.tmp), s)
+        call("mfnerf_occupancy_update_dev", ptr(self.density_grid), None, None, 0, None, C, G, float(decay),
+             ptr(count_grid) if count_grid is not None else None, thr, ptr(o.tmp), 1, ptr(self.bitfield), ptr(o.ws), s)

@@ -506,6 +506,24 @@ def test_planar_encode_and_field_match_row_major(gpu, name, args):
     call("mfnerf_field_fw", ptr(planes), cap, ptr(dg), N, None, ptr(packed), 64, 0, ptr(s2), ptr(c2), st)
     torch.cuda.synchronize()
     assert torch.equal(s1, s2) and torch.equal(c1, c2)
+    # the occupancy refresh's form: density only, each sigma also scattered to tmp[cell] (cell -1:
+    # skipped), over the device count's first points only
+    M = 3 * N
+    cell = torch.randperm(M, generator=g)[:N].int()
+    cell[::97] = -1
+    cg = cell.to(gpu)
+    s3 = torch.full((N,), -1.0, device=gpu)
+    tmp = torch.zeros(M, device=gpu)
+    n_part = torch.tensor([N - 77], dtype=torch.int32, device=gpu)
+    call("mfnerf_field_fw_density_scatter", ptr(planes), cap, N, ptr(n_part), ptr(packed), 64, ptr(s3), ptr(cg),
+         ptr(tmp), st)
+    torch.cuda.synchronize()
+    k = N - 77
+    assert torch.equal(s3[:k], s1[:k]) and bool((s3[k:] == -1.0).all())
+    ref_tmp = torch.zeros(M)
+    keep = cell[:k] >= 0
+    ref_tmp[cell[:k][keep].long()] = s1[:k].cpu()[keep]
+    assert torch.equal(tmp.cpu(), ref_tmp)
     dsig = (torch.randn(N, generator=g) * 1e-6).to(gpu)
     drgb = (torch.randn(N, 3, generator=g) * 1e-5).to(gpu)
     outs = []

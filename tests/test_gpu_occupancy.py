@@ -148,12 +148,17 @@ def test_engine_refresh_end_to_end(gpu):
     from mfnerf import engine, synthetic
     st = engine.TrainStep(engine.StepConfig(n_rays=512, log2_T=16), device=gpu, seed=0)
     st.set_occupancy(synthetic.ball_density_grid())
-    for warm in (True, False, False):
+    for i, warm in enumerate((True, False, False, False)):
         before = st.density_grid.clone().cpu()
         st.update_density_grid(warmup=warm)
         torch.cuda.synchronize()
         o = st._occ
         n = int(o.count)
+        # the draws' device call index advanced once per refresh (by a kernel of its own after the
+        # warm-up draws, by the marked-cell compaction after the steady-state ones)
+        assert int(o.calls) == i + 1
+        # the update's scratch is handed back zero (the refresh runs no fill launch for it)
+        assert int(torch.count_nonzero(o.tmp)) == 0
         cap = load().mfnerf_occupancy_points_unique(st.cascades, st.G, st.G ** 3 // 4, int(warm))
         assert 0 < n <= cap
         cell = o.cell[:n].cpu().long()
@@ -173,6 +178,7 @@ def test_engine_refresh_end_to_end(gpu):
                     for b in bad]
             raise AssertionError(f"warm={warm} n={n}: {int((got != ref_g).sum())} cells differ; "
                                  f"(cell, got, ref, before, tmp, list index, sigma): {info}")
+        assert torch.equal(st.bitfield.cpu().flatten(), ref_bf.flatten())  # thr + packbits in one launch
         assert OO.cell_points_ok(o.xyz[:n].cpu(), cell, st.cascades, st.G, st.cfg.scale)
 
 

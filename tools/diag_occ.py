@@ -23,7 +23,6 @@ for warm in (True, False, False):
         o.xyz.fill_(float("nan"))
         o.cell.fill_(12345)
         o.feat.fill_(float("nan"))
-        o.tmp.fill_(7.0)
     st.update_density_grid(warmup=warm)
     torch.cuda.synchronize()
     o = st._occ
