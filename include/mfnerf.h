@@ -263,10 +263,11 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
  * pass covers only the values before them.  Same floats as the two-call form.  grad_table must be
  * zero before the partitioned tables' first value (mfnerf_grid_binned_first_value); the rest is
  * overwritten.  Replaces tcnn's hash-grid backward (networks.py:36-49) feeding DDP's all-reduce
- * (train.py:284). */
+ * (train.py:284).  gate (optional, mfnerf_gate_wait): signalled once as the dense-level launch
+ * starts (by its first workgroup; a signal launch when no dense-level launch runs). */
 int mfnerf_grid_encode_bw_binned_float(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                                        const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
-                                       void* workspace, int64_t n_slots, const float* level_l1,
+                                       void* workspace, int64_t n_slots, const float* level_l1, int32_t* gate,
                                        mfnerf_stream_t stream);
 /* mfnerf_grid_encode_bw_binned (parts = 3) with the partitioned tables' Adam step fused into the
  * accumulate (adam: see mfnerf_adam_step_fixed_partial). */
@@ -500,6 +501,15 @@ int mfnerf_sample_rays_prep(const float* images, const float* poses, const float
 int mfnerf_adam_step(float* params, float* grads, float* m, float* v, void* p_f16, int64_t n, float lr,
                      float beta1, float beta2, float eps, float grad_scale, int step, int32_t* step_dev,
                      const float* lr_dev, mfnerf_amp_state* amp, int zero_grads, mfnerf_stream_t stream);
+/* The sharded update after the reduce-scatter (data parallel, train.py:277-287 DDP + apex
+ * FusedAdam): mfnerf_flag_from_shard + mfnerf_adam_step(zero_grads = 0) in one launch.  The
+ * non-finite flag is read from g_shard[0] (mfnerf_flag_to_shards put NaN there on any rank that
+ * raised it; the reduction carries it to every shard); the last workgroup stores it in
+ * amp->nonfinite for the bookkeeping, then zeroes zero[0, nz) (a per-step accumulator, e.g. the
+ * grid's level L1 bounds).  amp and step_dev are required; g_shard is not modified. */
+int mfnerf_adam_step_shard(float* params, const float* g_shard, float* m, float* v, void* p_f16, int64_t n, float lr,
+                           float beta1, float beta2, float eps, float grad_scale, int32_t* step_dev, const float* lr_dev,
+                           mfnerf_amp_state* amp, float* zero, int nz, mfnerf_stream_t stream);
 
 /* mfnerf_grid_encode_bw_finish + mfnerf_adam_step (zero_grads on) in one pass, for a step with no
  * gradient exchange between them: grads[0, table_offset) are float gradients, grads[table_offset, ...)

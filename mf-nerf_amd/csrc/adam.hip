@@ -10,13 +10,17 @@ namespace {
 __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, __half* __restrict__ p16, int64_t n, float lr, float b1, float b2,
                             float eps, float gscale, int step, int32_t* __restrict__ step_dev,
-                            const float* __restrict__ lr_dev, mfnerf_amp_state* __restrict__ amp, int zero_grads) {
+                            const float* __restrict__ lr_dev, mfnerf_amp_state* __restrict__ amp, int zero_grads,
+                            const float* __restrict__ flag_src, float* __restrict__ zero, int nz) {
     const int64_t n4 = n / 4;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     // step_dev counts completed steps; this update is number *step_dev + 1 (the last workgroup
     // advances it after every workgroup has read it)
-    const bool skipped = amp && amp->nonfinite;  // GradScaler: no update on a non-finite gradient
+    // GradScaler: no update on a non-finite gradient.  flag_src: the exchanged shard's first value
+    // carries every rank's flag (mfnerf_flag_to_shards) -- read here instead of a flag_from_shard launch
+    const bool flag_bad = flag_src && !isfinite(flag_src[0]);
+    const bool skipped = amp && (flag_src ? flag_bad : amp->nonfinite != 0);
     const int st = step_dev ? *step_dev + 1 : step;
     if (lr_dev) lr = *lr_dev;
     if (skipped) {
@@ -53,7 +57,22 @@ __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ g, float*
             if (p16) p16[i] = __float2half_rn(p[i]);
         }
     }
-    if (amp) mfn::amp_step_end_last_block(step_dev, amp, nullptr, 0);
+    if (amp) {
+        if (flag_src) {  // the bookkeeping's workgroup (the last) sets the flag it reads from the shard
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const unsigned total = gridDim.x;
+                const int prev = __hip_atomic_fetch_add(&amp->ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((unsigned)prev == total - 1) {
+                    amp->nonfinite = flag_bad ? 1 : 0;
+                    mfn::amp_step_end(step_dev, amp, zero, nz);
+                    __hip_atomic_store(&amp->ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        } else {
+            mfn::amp_step_end_last_block(step_dev, amp, zero, nz);
+        }
+    }
 }
 
 }  // namespace
@@ -124,12 +143,34 @@ extern "C" int mfnerf_adam_step(float* params, float* grads, float* m, float* v,
     // atomic on one address), grid-stride does the rest at the same bandwidth (grid.hip adam_fixed)
     const unsigned blocks = (unsigned)(want < 1024 ? (want < 1 ? 1 : want) : 1024);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(threads), 0, stream, params, grads, m, v, (__half*)p_f16, n, lr,
-                       beta1, beta2, eps, grad_scale, step, step_dev, lr_dev, amp, zero_grads);
+                       beta1, beta2, eps, grad_scale, step, step_dev, lr_dev, amp, zero_grads, (const float*)nullptr,
+                       (float*)nullptr, 0);
     // with amp the last workgroup did the bookkeeping; without it only the step count remains
     if (step_dev && !amp)
         hipLaunchKernelGGL(mfn_bump_step_kernel, dim3(1), dim3(1), 0, stream, step_dev, (mfnerf_amp_state*)nullptr,
                            (float*)nullptr, 0);
     return mfn_check_launch("adam_step");
+}
+
+extern "C" int mfnerf_adam_step_shard(float* params, const float* g_shard, float* m, float* v, void* p_f16, int64_t n,
+                                      float lr, float beta1, float beta2, float eps, float grad_scale,
+                                      int32_t* step_dev, const float* lr_dev, mfnerf_amp_state* amp, float* zero, int nz,
+                                      mfnerf_stream_t stream) {
+    if (n < 1 || nz < 0 || nz > 64) { mfn_set_error("adam_step_shard: bad size"); return MFN_ERR_INVALID; }
+    if (!params || !g_shard || !m || !v || !step_dev || !amp || (nz && !zero)) {
+        mfn_set_error("adam_step_shard: null pointer"); return MFN_ERR_INVALID;
+    }
+    if ((((uintptr_t)params) | ((uintptr_t)g_shard) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) {
+        mfn_set_error("adam_step_shard: buffers must be 16-byte aligned"); return MFN_ERR_INVALID;
+    }
+    if (p_f16 && (((uintptr_t)p_f16) & 7)) { mfn_set_error("adam_step_shard: fp16 copy must be 8-byte aligned"); return MFN_ERR_INVALID; }
+    const int threads = 256;
+    const int64_t want = mfn::div_up<int64_t>(mfn::div_up<int64_t>(n, 4), threads);
+    const unsigned blocks = (unsigned)(want < 1024 ? want : 1024);
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(threads), 0, stream, params, const_cast<float*>(g_shard), m, v,
+                       (__half*)p_f16, n, lr, beta1, beta2, eps, grad_scale, 0, step_dev, lr_dev, amp, 0, g_shard,
+                       zero, nz);
+    return mfn_check_launch("adam_step_shard");
 }
 
 extern "C" int mfnerf_check_finite(const float* x, int64_t n, int32_t* status, mfnerf_stream_t stream) {

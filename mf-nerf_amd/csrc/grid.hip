@@ -2009,15 +2009,17 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
 
 int mfnerf_grid_encode_bw_binned_float(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                                        const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
-                                       void* workspace, int64_t n_slots, const float* level_l1,
+                                       void* workspace, int64_t n_slots, const float* level_l1, int32_t* gate,
                                        mfnerf_stream_t stream) {
     BinPlan P;
     if (check_desc(desc, "grid_encode_bw_binned_float") || bin_plan(desc, &P) <= 0) {
         mfn_set_error("grid_encode_bw_binned_float: bad desc or nothing partitioned");
         return MFN_ERR_INVALID;
     }
+    AdamRest X{};  // no optimizer blocks; only the gate (opened as the dense-level launch starts)
+    X.gate = gate;
     int st = binned_impl(x, n, n_dev, x_min, x_range, desc, dL_dout, grad_table, workspace, n_slots, level_l1, 7,
-                         nullptr, stream);
+                         nullptr, stream, gate ? &X : nullptr);
     if (st || n == 0) return st;
     // the values before the partitioned tables: the dense levels' copies folded, any other level's
     // int32 sums converted (the accumulate wrote the partitioned tables' floats)

@@ -78,7 +78,7 @@ SIGNATURES = {
     "mfnerf_grid_encode_bw_binned": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _I64, _P, _I,
                                           _P]),
     "mfnerf_grid_encode_bw_binned_float": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _I64,
-                                               _P, _P]),
+                                               _P, _P, _P]),
     "mfnerf_grid_encode_bw_binned_adam": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _I64,
                                               _P, ctypes.POINTER(AdamFused), _P]),
     "mfnerf_grid_encode_bw_binned_adam_all": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _I64, _P,
@@ -112,6 +112,7 @@ SIGNATURES = {
     "mfnerf_sample_rays_prep": (_I, [_P, _P, _P, _I64, _I64, _I64, _I, ctypes.c_uint64, _P, _P, _P, _P, _F, _P, _P,
                                      _P]),
     "mfnerf_adam_step": (_I, [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _I, _P]),
+    "mfnerf_adam_step_shard": (_I, [_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _P, _P, _P, _P, _I, _P]),
     "mfnerf_adam_step_fixed": (_I, [_P, _P, _P, _P, _P, _I64, _I64, ctypes.POINTER(GridDesc), _P, _P, _F, _F, _F, _F, _P, _P, _P, _P]),
     "mfnerf_adam_step_fixed_partial": (_I, [_P, _P, _P, _P, _P, _I64, _I64, ctypes.POINTER(GridDesc), _P, _P, _F, _F, _F,
                                             _F, _P, _P, _P, _I64, _P, _P]),

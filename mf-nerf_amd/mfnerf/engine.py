@@ -561,19 +561,24 @@ class TrainStep:
             return self.off_table + load().mfnerf_grid_binned_first_value(self.desc)
         return self.n_alloc
 
-    def _grid_bw_float(self, mb):
+    def _grid_bw_float(self, mb, zero_l1=True, gate=None):
         """Data parallel, one part: the table gradient scattered and finished to floats for the
         exchange (binned: the accumulate writes the partitioned tables' floats and one finish pass
-        covers the rest, mfnerf_grid_encode_bw_binned_float), level_l1 zeroed after use."""
+        covers the rest, mfnerf_grid_encode_bw_binned_float), level_l1 zeroed after use (zero_l1
+        False: the sharded Adam's last workgroup zeroes it, _adam_shard); gate: the side stream's
+        gate pointer, opened as the dense-level launch starts (no signal launch of its own)."""
         if not self._binned():
+            if gate is not None:
+                call("mfnerf_gate_signal", gate, stream())
             self._grid_bw(mb, 0)
             self._grid_finish(0)
             return
         t, m = self.parts[0], mb.part[0]
         call("mfnerf_grid_encode_bw_binned_float", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min,
              self.x_range, self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws),
-             self._bin_slots(), ptr(self._level_l1), stream())
-        self._level_l1.zero_()
+             self._bin_slots(), ptr(self._level_l1), gate, stream())
+        if zero_l1:
+            self._level_l1.zero_()
 
     def _grid_finish(self, q):
         """Fold part q's private copies of the coarse levels / convert the fixed-point sums."""
@@ -594,6 +599,15 @@ class TrainStep:
         call("mfnerf_adam_step", ptr(self.params[lo:hi]), ptr(grads), ptr(self.m), ptr(self.v), ptr(self.p16[lo:hi]),
              hi - lo, float(c.lr), 0.9, 0.999, c.eps, 1.0, 0, ptr(self.step_dev), ptr(self.lr_dev),
              self._amp_ptr(), int(zero_grads), stream())
+
+    def _adam_shard(self):
+        """The sharded update after the reduce-scatter with the exchanged non-finite flag read from
+        the shard itself and level_l1 zeroed by its last workgroup (mfnerf_adam_step_shard: the
+        flag_from_shard launch and the level_l1 fill folded in)."""
+        c, (_, lo, hi) = self.cfg, self.shard
+        call("mfnerf_adam_step_shard", ptr(self.params[lo:hi]), ptr(self.g_shard), ptr(self.m), ptr(self.v),
+             ptr(self.p16[lo:hi]), hi - lo, float(c.lr), 0.9, 0.999, c.eps, 1.0, ptr(self.step_dev), ptr(self.lr_dev),
+             self._amp_ptr(), ptr(self._level_l1), self._level_l1.numel(), stream())
 
     def _finish_update(self, partial=False):
         """Unsharded, no exchange, fixed-point table gradient: the finish (convert) and Adam in one
@@ -790,16 +804,24 @@ class TrainStep:
             w = self.shard[2] - self.shard[1] if self.shard is not None else self.n_alloc
             n_sh = self.n_alloc // w
 
+            # sharded with amp: one launch reads the exchanged flag, updates and zeroes level_l1
+            fused_shard = (amp and self.shard is not None
+                           and os.environ.get("MFNERF_DP_SHARD_ADAM", "1") == "1")
+
             def dp_pre(j, mark):
                 self._pack()  # the previous step's all-gathered / updated fp16 weights
                 self._chain(self._static[j], self.mbuf[j], 0, mark)
-                mark("grid_bw")  # (MFNERF_GATE_AT=grid_bw: a signal kernel as the scatter begins)
-                self._grid_bw_float(self.mbuf[j])
+                # MFNERF_GATE_AT=grid_bw: opened by the dense-level launch's first workgroup
+                gate = getattr(mark, "ride", lambda _n: None)("grid_bw")
+                self._grid_bw_float(self.mbuf[j], zero_l1=not fused_shard, gate=gate)
+                mark("grid_bw")
                 if amp:  # the non-finite flag rides the collective: NaN into every shard's first value
                     call("mfnerf_flag_to_shards", ptr(self.grads), n_sh, w, ptr(self.finite_status), stream())
 
             def dp_post():
-                if self.shard is not None:
+                if fused_shard:
+                    self._adam_shard()
+                elif self.shard is not None:
                     if amp:
                         call("mfnerf_flag_from_shard", ptr(self.g_shard), ptr(self.finite_status), stream())
                     self._adam(self.g_shard, self.shard[1], self.shard[2], False)

@@ -60,6 +60,50 @@ def test_nonfinite_on_one_rank_skips_on_every_rank(mode):
         assert torch.equal(p16, out[(mode, 0)][1])
 
 
+def _replay_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mfnerf import dp, engine, synthetic
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    st = engine.TrainStep(engine.StepConfig(n_rays=512, log2_T=14), device=dev, seed=0)
+    st.set_occupancy(synthetic.ball_density_grid())
+    st.shard_optimizer(rank, world)
+    good = st.make_batches(3, seed=dp.rank_seed(100, rank))
+    bad = st.make_batches(1, seed=dp.rank_seed(200, rank))[0]
+    if rank == 1:
+        bad.rgb.fill_(float("nan"))
+    g = torch.Generator().manual_seed(rank + 5)
+    noise = [torch.rand(512, generator=g).to(dev) for _ in range(4)]
+    st.run(good[0], noise=noise[0])
+    st.capture(host_noise=True)
+    st.replay(good[1], noise=noise[1], next_batch=bad, next_noise=noise[2])
+    torch.cuda.synchronize()
+    p1, s1, l1 = st.p16.clone(), int(st.step_dev), st._level_l1.clone()
+    st.replay(bad, noise=noise[2], next_batch=good[2], next_noise=noise[3])
+    torch.cuda.synchronize()
+    skipped = (torch.equal(st.p16, p1), int(st.step_dev) == s1, st.skipped_steps(),
+               int(torch.count_nonzero(st._level_l1)), int(torch.count_nonzero(l1)))
+    st.replay(good[2], noise=noise[3])
+    torch.cuda.synchronize()
+    out[rank] = (skipped, st.p16.cpu(), bool(torch.isfinite(st.p16).all()), int(st.step_dev))
+    dist.destroy_process_group()
+
+
+def test_nonfinite_on_one_rank_skips_replayed_sharded_step():
+    """The same through the captured sharded step (dp_pre / reduce-scatter / dp_post graphs): the
+    update reads the exchanged flag from its shard in the Adam launch itself
+    (mfnerf_adam_step_shard), skips on every rank, and leaves the level L1 bounds zeroed either way."""
+    world = 2
+    out = mp.Manager().dict()
+    mp.spawn(_replay_worker, args=(world, _port(), out), nprocs=world, join=True)
+    for r in range(world):
+        skipped, p16, finite, steps = out[r]
+        assert skipped == (True, True, 1, 0, 0), (r, skipped)
+        assert finite and steps == 3
+        assert torch.equal(p16, out[0][1])
+
+
 def _union_worker(rank, world, port, mode, out):
     """Rank r trains on its half of a 2N-ray batch; the exchange must make every rank's step equal
     to ONE process stepping on the union (the reference's DDP semantics: mean of the ranks' mean

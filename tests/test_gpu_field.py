@@ -347,7 +347,7 @@ def test_grid_encode_bw_binned_float_matches_scatter_and_finish(gpu, div):
         l1 = torch.zeros(lay.L, device=gpu)
         call("mfnerf_grid_level_l1", ptr(dy), N, None, lay.L, ptr(l1), stream())
         call("mfnerf_grid_encode_bw_binned_float", ptr(x), N, None, 0.0, 1.0, desc, ptr(dy), ptr(out), ptr(ws), ns,
-             ptr(l1), stream())
+             ptr(l1), None, stream())
         torch.cuda.synchronize()
         assert torch.equal(out, ref), f"call {rep}: {int((out != ref).sum())} values differ"
 
