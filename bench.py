@@ -208,9 +208,6 @@ def main():
                                              world_size=world, rank=rank)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if os.environ.get("MFNERF_MAIN_HIGH_PRIORITY", "0") == "1":
-        # A/B knob: the step's own stream at high queue priority (the side stream's march at normal)
-        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1]))
 
     from mfnerf import dp, engine, synthetic
     if args.dp_rehearse:

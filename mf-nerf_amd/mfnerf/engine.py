@@ -880,7 +880,8 @@ class TrainStep:
         # step at 1.10 ms (kernels on the main queue 2-7x slower; GPU_MAX_HW_QUEUES=8 also cured it:
         # the extra streams share hardware queues) -- the data-parallel step would pay it on every rank
         # (no priority below normal exists here: torch.cuda.Stream.priority_range() is (0, -1) on this
-        # ROCm, r4m -- a "least" priority side stream measured the same as normal)
+        # ROCm, r4m -- a "least" priority side stream measured the same as normal; the step's own
+        # stream at high priority instead: 0.5567-0.5582 vs 0.5541-0.5542 ms, r04_v16)
         hi = os.environ.get("MFNERF_SIDE_HIGH_PRIORITY", "0") == "1"
         self._side = torch.cuda.Stream(device=self.dev, priority=torch.cuda.Stream.priority_range()[1] if hi else 0)
         # MFNERF_GATE_STREAM=1: gated marches wait as a stream operation (mfnerf_gate_wait_stream) on
