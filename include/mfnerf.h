@@ -379,6 +379,11 @@ int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float
  * needs only dL_dfeat.  Part of the tcnn backward (networks.py:96-126) split for scheduling. */
 int mfnerf_field_bw_reduce(int rgb_width, const void* workspace, float* grad_xyz, float* grad_rgb,
                            int32_t* nonfinite, mfnerf_stream_t stream);
+/* mfnerf_field_bw_reduce STORING the folded sums (grad = fold, same order and bits) instead of adding
+ * them: a gradient that holds only this step's weight gradient needs no zeroing first (the
+ * data-parallel step, where nothing else adds into the MLPs' gradient). */
+int mfnerf_field_bw_reduce_store(int rgb_width, const void* workspace, float* grad_xyz, float* grad_rgb,
+                                 int32_t* nonfinite, mfnerf_stream_t stream);
 
 /* ---------------------------------------------------------------- standalone FullyFusedMLP (MFMA)
  * tinycudann.Network / NetworkWithInputEncoding's network as MF-NeRF configures them one module at a
@@ -539,6 +544,11 @@ int mfnerf_adam_step_fixed_partial(float* params, float* grads, float* m, float*
                                    const int32_t* fused_ovf, mfnerf_stream_t stream);
 /* value index (within the table) where the partitioned tables start, or -1 (nothing partitioned) */
 int64_t mfnerf_grid_binned_first_value(const mfnerf_grid_desc* desc);
+/* Values of the dense prefix (the leading own-table dense levels whose backward adds into private
+ * copies and whose finish overwrites the gradient).  When it equals
+ * mfnerf_grid_binned_first_value, mfnerf_grid_encode_bw_binned_float overwrites every table value
+ * (no zeroing before it). */
+int64_t mfnerf_grid_dense_values(const mfnerf_grid_desc* desc);
 /* byte offset of the slot-overflow word inside the binned workspace sized for n_slots */
 int64_t mfnerf_grid_encode_bw_binned_flag_offset(const mfnerf_grid_desc* desc, int64_t n_slots);
 

@@ -1275,7 +1275,7 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_bw_wr2_kernel(
 template <int W>
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int rows,
                                                           float* __restrict__ gx, float* __restrict__ gr,
-                                                          int32_t* __restrict__ nonfinite) {
+                                                          int32_t* __restrict__ nonfinite, int store = 0) {
     // 64 parameters per block as 16 float4 columns x 16 row groups; each thread sums its rows
     // (rows/16, all loads in flight) and the 16 partials are added in a fixed tree order
     constexpr int N_DW = Geo<W>::N_DW;
@@ -1320,8 +1320,8 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int q = p + k;
-            if (q < N_XYZ_PARAMS) gx[q] += v[k];
-            else gr[q - N_XYZ_PARAMS] += v[k];
+            float* dst = q < N_XYZ_PARAMS ? gx + q : gr + (q - N_XYZ_PARAMS);
+            *dst = store ? v[k] : *dst + v[k];
             bad |= !isfinite(v[k]);
         }
         if (nonfinite && bad) atomicOr(nonfinite, 1);
@@ -1397,7 +1397,7 @@ int launch_bw(const void* feat, int64_t ps, const float* dirs, int64_t n, const 
                                (float*)workspace, nonfinite, level_l1);
             if (grad_xyz)
                 hipLaunchKernelGGL(slab_reduce_kernel<W>, dim3((Geo<W>::N_DW + 63) / 64), dim3(256), 0, stream,
-                                   (const float*)workspace, COOP_BLOCKS, grad_xyz, grad_rgb, nonfinite);
+                                   (const float*)workspace, COOP_BLOCKS, grad_xyz, grad_rgb, nonfinite, 0);
             return MFN_OK;
         }
     }
@@ -1432,7 +1432,7 @@ int launch_bw(const void* feat, int64_t ps, const float* dirs, int64_t n, const 
                            (const _Float16*)packed, dL_drgb, grad_scale, scale_dev, (float*)workspace, nonfinite);
     if (grad_xyz)  // else deferred: mfnerf_field_bw_reduce folds the slab later
         hipLaunchKernelGGL(slab_reduce_kernel<W>, dim3((Geo<W>::N_DW + 63) / 64), dim3(256), 0, stream,
-                           (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
+                           (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite, 0);
     return MFN_OK;
 }
 
@@ -1544,17 +1544,27 @@ int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float
     return mfn_check_launch("field_bw");
 }
 
-int mfnerf_field_bw_reduce(int rgb_width, const void* workspace, float* grad_xyz, float* grad_rgb,
-                           int32_t* nonfinite, mfnerf_stream_t stream) {
+static int field_bw_fold(int rgb_width, const void* workspace, float* grad_xyz, float* grad_rgb, int32_t* nonfinite,
+                         int store, mfnerf_stream_t stream) {
     if (!width_ok(rgb_width)) return bad_width(rgb_width);
     if (!workspace || !grad_xyz || !grad_rgb) { mfn_set_error("field_bw_reduce: null pointer"); return MFN_ERR_INVALID; }
     if (rgb_width == 64)
         hipLaunchKernelGGL(slab_reduce_kernel<64>, dim3((Geo<64>::N_DW + 63) / 64), dim3(256), 0, stream,
-                           (const float*)workspace, bw_rows(64), grad_xyz, grad_rgb, nonfinite);
+                           (const float*)workspace, bw_rows(64), grad_xyz, grad_rgb, nonfinite, store);
     else
         hipLaunchKernelGGL(slab_reduce_kernel<128>, dim3((Geo<128>::N_DW + 63) / 64), dim3(256), 0, stream,
-                           (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite);
+                           (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite, store);
     return mfn_check_launch("field_bw_reduce");
+}
+
+int mfnerf_field_bw_reduce(int rgb_width, const void* workspace, float* grad_xyz, float* grad_rgb,
+                           int32_t* nonfinite, mfnerf_stream_t stream) {
+    return field_bw_fold(rgb_width, workspace, grad_xyz, grad_rgb, nonfinite, 0, stream);
+}
+
+int mfnerf_field_bw_reduce_store(int rgb_width, const void* workspace, float* grad_xyz, float* grad_rgb,
+                                 int32_t* nonfinite, mfnerf_stream_t stream) {
+    return field_bw_fold(rgb_width, workspace, grad_xyz, grad_rgb, nonfinite, 1, stream);
 }
 
 

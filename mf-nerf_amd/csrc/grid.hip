@@ -2157,6 +2157,11 @@ int64_t mfnerf_grid_binned_first_value(const mfnerf_grid_desc* desc) {
     return 2 * (int64_t)P.t_offset[0];
 }
 
+int64_t mfnerf_grid_dense_values(const mfnerf_grid_desc* desc) {
+    if (check_desc(desc, "grid_dense_values")) return -1;
+    return 2 * dense_entries_of(desc);
+}
+
 int64_t mfnerf_grid_encode_bw_binned_flag_offset(const mfnerf_grid_desc* desc, int64_t n_slots) {
     if (check_desc(desc, "grid_encode_bw_binned_flag_offset") || n_slots <= 0) return -1;
     BinWorkspace W;

@@ -87,6 +87,7 @@ SIGNATURES = {
                                                        _P, _I64, _P, ctypes.POINTER(AdamFused), _P, _P, _P, _I, _P,
                                                        _P, _P]),
     "mfnerf_grid_binned_first_value": (_I64, [ctypes.POINTER(GridDesc)]),
+    "mfnerf_grid_dense_values": (_I64, [ctypes.POINTER(GridDesc)]),
     "mfnerf_grid_encode_bw_binned_flag_offset": (_I64, [ctypes.POINTER(GridDesc), _I64]),
     "mfnerf_grid_level_l1": (_I, [_P, _I64, _P, _I, _P, _P]),
     "mfnerf_field_packed_bytes": (_I64, [_I]),
@@ -117,6 +118,7 @@ SIGNATURES = {
     "mfnerf_adam_step_fixed_partial": (_I, [_P, _P, _P, _P, _P, _I64, _I64, ctypes.POINTER(GridDesc), _P, _P, _F, _F, _F,
                                             _F, _P, _P, _P, _I64, _P, _P]),
     "mfnerf_field_bw_reduce": (_I, [_I, _P, _P, _P, _P, _P]),
+    "mfnerf_field_bw_reduce_store": (_I, [_I, _P, _P, _P, _P, _P]),
     "mfnerf_mlp_n_params": (_I64, [_I, _I, _I, _I]),
     "mfnerf_mlp_packed_bytes": (_I64, [_I, _I, _I, _I]),
     "mfnerf_mlp_pack": (_I, [_P, _I, _I, _I, _I, _P, _P]),

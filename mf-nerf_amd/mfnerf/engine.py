@@ -357,6 +357,7 @@ class TrainStep:
         # this rank's slice of the gradient, reduced in place (RCCL in-place reduce-scatter: no
         # second gradient-sized buffer, and a one-rank group's "reduction" is no copy)
         self.g_shard = self.grads[lo:hi]
+        self._store_fold_v = None  # (re-derived for the sharded step)
         self.graphs = None  # re-capture with the sharded update
 
     # ---------------------------------------------------------------- the step
@@ -400,8 +401,9 @@ class TrainStep:
         c, s = self.cfg, stream()
         t, m = self.parts[q], mb.part[q]
         Np, cap = self.Np, self.cap_p
+        store_fold = q == 0 and self._store_fold()
         if q == 0:
-            if self.shard is not None:
+            if self.shard is not None and not store_fold:
                 # unsharded: the previous Adam pass left it zero; sharded, the binned scatter
                 # overwrites the partitioned tables, so only the values before them are zeroed
                 self.grads[:self._grad_zero_end()].zero_()
@@ -447,10 +449,14 @@ class TrainStep:
             mark("composite_bw")
         call("mfnerf_field_bw", ptr(t.feat), cap, ptr(m.dirs), cap, ptr(m.counter), ptr(self.packed), c.rgb_width,
              ptr(t.dsig), ptr(t.drgb_s), 0.0 if c.dynamic_loss_scale else self.grad_scale, ptr(t.dfeat),
-             None if defer_fold else ptr(t.mlp_grad), None if defer_fold else ptr(t.mlp_grad[self.off_rgb:]),
+             None if defer_fold or store_fold else ptr(t.mlp_grad),
+             None if defer_fold or store_fold else ptr(t.mlp_grad[self.off_rgb:]),
              ptr(t.field_ws),
              self._amp_ptr(),
              ptr(self._level_l1) if self._fixed() else None, s)
+        if store_fold:  # the fold writes the MLPs' gradient outright (nothing zeroed it)
+            call("mfnerf_field_bw_reduce_store", c.rgb_width, ptr(t.field_ws), ptr(t.mlp_grad),
+                 ptr(t.mlp_grad[self.off_rgb:]), self._amp_ptr(), s)
         mark("field_bw")
 
     def _fixed(self):
@@ -552,6 +558,23 @@ class TrainStep:
         else:
             self._grid_bw(self.mbuf[j], 0, fuse_adam=True)
             self._finish_update(partial=True)
+
+    def _store_fold(self):
+        """Sharded, one part, partitioned scatter whose float finish overwrites every table value
+        before the partitioned tables (they are all dense-prefix values): the weight-gradient fold
+        stores instead of adding and the step zeroes no gradient prefix (one fill launch less;
+        MFNERF_DP_STORE_FOLD=0: off)."""
+        v = getattr(self, "_store_fold_v", None)
+        if v is None:
+            lib = load()
+            n_dw = lib.mfnerf_field_bw_workspace(0, self.cfg.rgb_width) // (4 * lib.mfnerf_field_bw_slab_rows(
+                self.cfg.rgb_width))
+            v = (self.shard is not None and self.n_parts == 1 and self._binned() and self._fixed()
+                 and self.off_table == n_dw
+                 and lib.mfnerf_grid_binned_first_value(self.desc) == lib.mfnerf_grid_dense_values(self.desc)
+                 and os.environ.get("MFNERF_DP_STORE_FOLD", "1") == "1")
+            self._store_fold_v = v
+        return v
 
     def _grad_zero_end(self):
         """Gradient values a step must find zero: all of them, or with the binned scatter only those

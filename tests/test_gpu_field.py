@@ -434,6 +434,16 @@ def test_field_bw(gpu, wscale, sig_on, width):
         # vs pure fp32 autograd: the fp16 quantisation tcnn's backward has too (~1% rms)
         cos = float(torch.nn.functional.cosine_similarity(got.flatten(), r32.flatten(), dim=0))
         assert cos > 0.9995, cos
+    # the deferred fold: adding into zeros and storing over garbage give the undeferred call's bits
+    FLD.field_bw(feat.to(gpu), dirs.to(gpu), N, packed, dsig.to(gpu), drgb.to(gpu), S, dfeat, None, None, ws, width)
+    st = stream()
+    ax, ar = torch.zeros_like(gx), torch.zeros_like(gr)
+    call("mfnerf_field_bw_reduce", width, ptr(ws), ptr(ax), ptr(ar), None, st)
+    sx, sr = torch.full_like(gx, float("nan")), torch.full_like(gr, 7.0)
+    call("mfnerf_field_bw_reduce_store", width, ptr(ws), ptr(sx), ptr(sr), None, st)
+    torch.cuda.synchronize()
+    assert torch.equal(ax, gx) and torch.equal(ar, gr)
+    assert torch.equal(sx, gx) and torch.equal(sr, gr)
 
 
 @pytest.mark.parametrize("width", [64, 128])
