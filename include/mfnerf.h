@@ -264,11 +264,15 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
  * zero before the partitioned tables' first value (mfnerf_grid_binned_first_value); the rest is
  * overwritten.  Replaces tcnn's hash-grid backward (networks.py:36-49) feeding DDP's all-reduce
  * (train.py:284).  gate (optional, mfnerf_gate_wait): signalled once as the dense-level launch
- * starts (by its first workgroup; a signal launch when no dense-level launch runs). */
+ * starts (by its first workgroup; a signal launch when no dense-level launch runs).
+ * flag (optional): mfnerf_flag_to_shards(grads, flag_world, flag_shard_len, flag) folded into the
+ * finish pass, grad_table being grads + table_offset (the flat gradient's every value must be final
+ * when this is enqueued; needs a non-empty table prefix before the partitioned tables). */
 int mfnerf_grid_encode_bw_binned_float(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                                        const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
                                        void* workspace, int64_t n_slots, const float* level_l1, int32_t* gate,
-                                       mfnerf_stream_t stream);
+                                       const int32_t* flag, int64_t flag_world, int64_t flag_shard_len,
+                                       int64_t table_offset, mfnerf_stream_t stream);
 /* mfnerf_grid_encode_bw_binned (parts = 3) with the partitioned tables' Adam step fused into the
  * accumulate (adam: see mfnerf_adam_step_fixed_partial). */
 int mfnerf_grid_encode_bw_binned_adam(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,

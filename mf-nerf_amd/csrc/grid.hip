@@ -657,10 +657,19 @@ __device__ __forceinline__ int4 fold_packed_copies(int* __restrict__ priv, int64
     return make_int4(a0, (int)(a >> 32) + (a0 < 0), b0, (int)(b >> 32) + (b0 < 0));
 }
 
+// ShardFlag (the data-parallel step): the step's non-finite flag into the first value of every
+// exchange shard (NaN; mfnerf_flag_to_shards's job, without its launch) -- values this pass writes
+// get it as they are written, the others (written by earlier launches) from workgroup 0.
+struct ShardFlag {
+    const int32_t* flag;  // NULL: none
+    int64_t world, shard_len, table_off;  // grad[i] is flat value table_off + i
+};
+
 __global__ __launch_bounds__(256) void fold_convert_kernel(float* __restrict__ grad, int* __restrict__ priv,
                                                            int64_t dense_vals, int64_t total_vals,
                                                            const mfnerf_grid_desc D,
-                                                           const float* __restrict__ level_l1) {
+                                                           const float* __restrict__ level_l1,
+                                                           const ShardFlag SF = ShardFlag{}) {
     // table regions in address order -- a level's own table, or a shared MixedFeature table counted
     // once (the levels sharing it have its offset) -- each with its table's scale
     __shared__ TableRegions R;
@@ -669,6 +678,11 @@ __global__ __launch_bounds__(256) void fold_convert_kernel(float* __restrict__ g
     const int64_t* lo_v = R.lo_v;
     const int n_reg = R.n_reg;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const bool raise = SF.flag && *SF.flag;
+    if (raise && blockIdx.x == 0 && (int64_t)threadIdx.x < SF.world) {
+        const int64_t f = (int64_t)threadIdx.x * SF.shard_len - SF.table_off;  // relative to grad
+        if (f < 0 || f >= total_vals) grad[f] = __int_as_float(0x7fc00000);
+    }
     int l = 0;  // region of value i (i increases per thread: walk forward)
     for (int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; 4 * i4 < total_vals; i4 += stride) {
         const int64_t i = 4 * i4;  // region boundaries are multiples of 16 values
@@ -681,8 +695,15 @@ __global__ __launch_bounds__(256) void fold_convert_kernel(float* __restrict__ g
         } else {
             acc = *reinterpret_cast<const int4*>(grad + i);
         }
-        *reinterpret_cast<float4*>(grad + i) =
-            make_float4((float)acc.x * is, (float)acc.y * is, (float)acc.z * is, (float)acc.w * is);
+        float4 o = make_float4((float)acc.x * is, (float)acc.y * is, (float)acc.z * is, (float)acc.w * is);
+        if (raise) {
+            float* oc = &o.x;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if ((SF.table_off + i + c) % SF.shard_len == 0 && (SF.table_off + i + c) / SF.shard_len < SF.world)
+                    oc[c] = __int_as_float(0x7fc00000);
+        }
+        *reinterpret_cast<float4*>(grad + i) = o;
     }
 }
 
@@ -2010,7 +2031,12 @@ int mfnerf_grid_encode_bw_binned(const float* x, int64_t n, const int32_t* n_dev
 int mfnerf_grid_encode_bw_binned_float(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                                        const mfnerf_grid_desc* desc, const float* dL_dout, float* grad_table,
                                        void* workspace, int64_t n_slots, const float* level_l1, int32_t* gate,
-                                       mfnerf_stream_t stream) {
+                                       const int32_t* flag, int64_t flag_world, int64_t flag_shard_len,
+                                       int64_t table_offset, mfnerf_stream_t stream) {
+    if (flag && (flag_world < 1 || flag_world > 256 || flag_shard_len < 1 || table_offset < 0)) {
+        mfn_set_error("grid_encode_bw_binned_float: bad shard-flag arguments");
+        return MFN_ERR_INVALID;
+    }
     BinPlan P;
     if (check_desc(desc, "grid_encode_bw_binned_float") || bin_plan(desc, &P) <= 0) {
         mfn_set_error("grid_encode_bw_binned_float: bad desc or nothing partitioned");
@@ -2024,10 +2050,14 @@ int mfnerf_grid_encode_bw_binned_float(const float* x, int64_t n, const int32_t*
     // the values before the partitioned tables: the dense levels' copies folded, any other level's
     // int32 sums converted (the accumulate wrote the partitioned tables' floats)
     const int64_t head = 2 * (int64_t)P.t_offset[0];
+    const ShardFlag SF{flag, flag_world, flag_shard_len, table_offset};
     if (head > 0) {
         const int64_t fb = div_up<int64_t>(head / 4, 256);
         hipLaunchKernelGGL(fold_convert_kernel, dim3((unsigned)(fb < 4096 ? fb : 4096)), dim3(256), 0, stream,
-                           grad_table, (int*)workspace, 2 * dense_entries_of(desc), head, *desc, level_l1);
+                           grad_table, (int*)workspace, 2 * dense_entries_of(desc), head, *desc, level_l1, SF);
+    } else if (flag) {
+        mfn_set_error("grid_encode_bw_binned_float: a shard flag needs a table prefix to ride");
+        return MFN_ERR_INVALID;
     }
     return mfn_check_launch("grid_encode_bw_binned_float");
 }

@@ -78,7 +78,7 @@ SIGNATURES = {
     "mfnerf_grid_encode_bw_binned": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _I64, _P, _I,
                                           _P]),
     "mfnerf_grid_encode_bw_binned_float": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _I64,
-                                               _P, _P, _P]),
+                                               _P, _P, _P, _I64, _I64, _I64, _P]),
     "mfnerf_grid_encode_bw_binned_adam": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _P, _I64,
                                               _P, ctypes.POINTER(AdamFused), _P]),
     "mfnerf_grid_encode_bw_binned_adam_all": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _I64, _P,

@@ -584,24 +584,30 @@ class TrainStep:
             return self.off_table + load().mfnerf_grid_binned_first_value(self.desc)
         return self.n_alloc
 
-    def _grid_bw_float(self, mb, zero_l1=True, gate=None):
+    def _grid_bw_float(self, mb, zero_l1=True, gate=None, shard_flag=None):
         """Data parallel, one part: the table gradient scattered and finished to floats for the
         exchange (binned: the accumulate writes the partitioned tables' floats and one finish pass
         covers the rest, mfnerf_grid_encode_bw_binned_float), level_l1 zeroed after use (zero_l1
         False: the sharded Adam's last workgroup zeroes it, _adam_shard); gate: the side stream's
-        gate pointer, opened as the dense-level launch starts (no signal launch of its own)."""
+        gate pointer, opened as the dense-level launch starts (no signal launch of its own);
+        shard_flag (flag pointer, shards, shard length): mfnerf_flag_to_shards folded into the
+        float finish when it has a table prefix to ride -- returns True when it was."""
         if not self._binned():
             if gate is not None:
                 call("mfnerf_gate_signal", gate, stream())
             self._grid_bw(mb, 0)
             self._grid_finish(0)
-            return
+            return False
         t, m = self.parts[0], mb.part[0]
+        fold_flag = (shard_flag is not None and load().mfnerf_grid_binned_first_value(self.desc) > 0
+                     and os.environ.get("MFNERF_DP_FLAG_FOLD", "1") == "1")
+        fl, fw, fs = shard_flag if fold_flag else (None, 0, 0)
         call("mfnerf_grid_encode_bw_binned_float", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min,
              self.x_range, self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws),
-             self._bin_slots(), ptr(self._level_l1), gate, stream())
+             self._bin_slots(), ptr(self._level_l1), gate, fl, fw, fs, self.off_table, stream())
         if zero_l1:
             self._level_l1.zero_()
+        return fold_flag
 
     def _grid_finish(self, q):
         """Fold part q's private copies of the coarse levels / convert the fixed-point sums."""
@@ -836,9 +842,12 @@ class TrainStep:
                 self._chain(self._static[j], self.mbuf[j], 0, mark)
                 # MFNERF_GATE_AT=grid_bw: opened by the dense-level launch's first workgroup
                 gate = getattr(mark, "ride", lambda _n: None)("grid_bw")
-                self._grid_bw_float(self.mbuf[j], zero_l1=not fused_shard, gate=gate)
+                # the non-finite flag rides the collective: NaN into every shard's first value (by
+                # the float finish when it can, else a launch of its own)
+                sf = (ptr(self.finite_status), n_sh, w) if amp else None
+                folded = self._grid_bw_float(self.mbuf[j], zero_l1=not fused_shard, gate=gate, shard_flag=sf)
                 mark("grid_bw")
-                if amp:  # the non-finite flag rides the collective: NaN into every shard's first value
+                if amp and not folded:
                     call("mfnerf_flag_to_shards", ptr(self.grads), n_sh, w, ptr(self.finite_status), stream())
 
             def dp_post():

@@ -347,9 +347,30 @@ def test_grid_encode_bw_binned_float_matches_scatter_and_finish(gpu, div):
         l1 = torch.zeros(lay.L, device=gpu)
         call("mfnerf_grid_level_l1", ptr(dy), N, None, lay.L, ptr(l1), stream())
         call("mfnerf_grid_encode_bw_binned_float", ptr(x), N, None, 0.0, 1.0, desc, ptr(dy), ptr(out), ptr(ws), ns,
-             ptr(l1), None, stream())
+             ptr(l1), None, None, 0, 0, 0, stream())
         torch.cuda.synchronize()
         assert torch.equal(out, ref), f"call {rep}: {int((out != ref).sum())} values differ"
+    # the shard flag folded into the finish: a flat gradient [64 MLP values | table] cut into 3
+    # shards whose first values fall in the MLP part, the finish's prefix and the partitioned part
+    T0 = 64
+    flat_n = T0 + lay.n_params
+    for raised in (0, 1):
+        for shard_len, world in ((T0 + first // 2, 2), (flat_n // 3 // 4 * 4, 3), (T0 + 4, 5)):
+            flat = torch.zeros(flat_n, device=gpu)
+            flat[:T0] = 1.0
+            flag = torch.tensor([raised], dtype=torch.int32, device=gpu)
+            l1 = torch.zeros(lay.L, device=gpu)
+            call("mfnerf_grid_level_l1", ptr(dy), N, None, lay.L, ptr(l1), stream())
+            call("mfnerf_grid_encode_bw_binned_float", ptr(x), N, None, 0.0, 1.0, desc, ptr(dy), ptr(flat[T0:]),
+                 ptr(ws), ns, ptr(l1), None, ptr(flag), world, shard_len, T0, stream())
+            torch.cuda.synchronize()
+            want = torch.cat([torch.ones(T0, device=gpu), ref])
+            heads = [k * shard_len for k in range(world) if k * shard_len < flat_n]
+            if raised:
+                want[heads] = float("nan")
+            assert torch.equal(torch.isnan(flat), torch.isnan(want)), (raised, world, shard_len)
+            keep = ~torch.isnan(want)
+            assert torch.equal(flat[keep], want[keep]), (raised, world, shard_len)
 
 
 def test_grid_encode_world_coords_normalisation(gpu):
