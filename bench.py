@@ -97,19 +97,32 @@ def run_step(step, batch, world, ev=None, allreduce=None):
     step.run(batch, mark=mark, exchange=dp.allreduce_mean_ if allreduce else None)
 
 
-def pmc_traffic(kernel_prefix, preset="lego"):
+def pmc_suffix(preset, log2_T, n_rays):
+    """The PMC summary's file suffix for a workload: "" for the lego preset as configured, "_<preset>"
+    for another preset, "_T<k>" / "_n<rays>" where the table size / batch differ from the preset's
+    (tools/gpu_pmc.sh names its outputs the same way)."""
+    pre = PRESETS[preset]
+    suffix = "" if preset == "lego" else "_" + preset
+    if log2_T is not None and log2_T != pre["log2_T"]:
+        suffix += f"_T{log2_T}"
+    if n_rays is not None and n_rays != pre["n_rays"]:
+        suffix += f"_n{n_rays}"
+    return suffix
+
+
+def pmc_traffic(kernel_prefix, preset="lego", log2_T=None, n_rays=None):
     """(HBM-side bytes, memory-side atomic requests, source) per launch, summed over the kernels whose
     names start with one of `kernel_prefix` (one step's launches of them), from the newest
-    committed PMC summary (profiles/rNN_*pmc_traffic.json, made by tools/pmc_traffic.py from separate
-    FETCH_SIZE / WRITE_SIZE / TCC_EA0_ATOMIC rocprofv3 passes with the guide's gfx950 corrections);
-    Nones if absent."""
+    committed PMC summary of this workload (profiles/rNN_*pmc_traffic<pmc_suffix>.json, made by
+    tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE / TCC_EA0_ATOMIC rocprofv3 passes with
+    the guide's gfx950 corrections); Nones if there is none for this exact workload."""
     import glob
     import re
 
     def order(f):  # profiles/rNN_vMM_pmc_traffic.json: newest round, then newest version
         m = re.match(r"r(\d+)(?:_v(\d+))?_", os.path.basename(f))
         return (int(m.group(1)), int(m.group(2) or 0)) if m else (-1, -1)
-    suffix = "" if preset == "lego" else "_" + preset  # tools/gpu_pmc.sh PRESET=...
+    suffix = pmc_suffix(preset, log2_T, n_rays)  # tools/gpu_pmc.sh PRESET=... LOG2T=...
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*pmc_traffic{suffix}.json")), key=order)
     if not files:
         return None, None, None
@@ -213,9 +226,11 @@ def main():
     if args.dp_rehearse:
         dp.rehearse(True)  # the one-rank group's collectives through RCCL (skipped otherwise)
     # the exchange through a direct RCCL communicator on the step's stream, so the whole data-parallel
-    # step (collectives included) replays as one HIP graph (mfnerf/rccl.py); MFNERF_DIRECT_RCCL=0 keeps
-    # torch.distributed's collectives between two graphs per step
-    direct = dp_on and os.environ.get("MFNERF_DIRECT_RCCL", "1") == "1" and dp.use_direct_rccl()
+    # step (collectives included) replays as one HIP graph (mfnerf/rccl.py).  Default: on for the
+    # one-rank rehearsal, off at N > 1 (torch.distributed's collectives between two graphs per step)
+    # until a multi-GPU run has pinned the direct path against them; MFNERF_DIRECT_RCCL=1 / 0 forces it
+    want_direct = os.environ.get("MFNERF_DIRECT_RCCL", "1" if world == 1 else "0") == "1"
+    direct = dp_on and want_direct and dp.use_direct_rccl()
 
     pre = dict(PRESETS[args.preset])
     if args.n_rays is not None:
@@ -312,7 +327,7 @@ def main():
     # roofline: grid_bw (the dominant kernel), timed by events around it inside the timed region
     dom = "grid_bw"
     # the newest committed PMC summary of this preset's workload
-    traffic, atomic_req, traffic_src = pmc_traffic(GRID_BW_KERNEL, args.preset)
+    traffic, atomic_req, traffic_src = pmc_traffic(GRID_BW_KERNEL, args.preset, args.log2_T, args.n_rays)
     dom_bytes = BYTES_PER_SAMPLE[dom] * mean_samples
     achieved = dom_bytes / (grid_bw_ms * 1e-3) / 1e9
     # the bound the scatter actually meets: memory-side atomic requests per second
@@ -364,6 +379,8 @@ def main():
         with os.fdopen(out_fd, "w") as f:
             f.write(json.dumps(out) + "\n")
     if dp_on:
+        torch.cuda.synchronize()
+        dp.use_direct_rccl(False)  # the direct communicator (ncclCommDestroy) before torch's own
         torch.distributed.destroy_process_group()
 
 

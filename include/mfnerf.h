@@ -129,14 +129,6 @@ int mfnerf_composite_train_fused(const float* sigmas, const float* rgbs, const f
                                  float bg_b, int64_t* total_samples, float* opacity, float* depth, float* rgb,
                                  float* ws, float* dL_drgb, float* dL_dopacity, float* dL_dsigmas, float* dL_drgbs,
                                  float* loss_partials, mfnerf_stream_t stream);
-/* mfnerf_composite_train_fused that also opens a gate (gate.hip's int32 {signals, waits, ticket};
- * NULL: none) when its last workgroup finishes -- mfnerf_gate_signal riding the launch. */
-int mfnerf_composite_train_fused_gated(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
-                                       const int64_t* rays_a, int64_t n_rays, int64_t n_samples, float T_threshold,
-                                       const float* target, int64_t n_mean, float lambda_opacity, float bg_r,
-                                       float bg_g, float bg_b, int64_t* total_samples, float* opacity, float* depth,
-                                       float* rgb, float* ws, float* dL_drgb, float* dL_dopacity, float* dL_dsigmas,
-                                       float* dL_drgbs, float* loss_partials, int32_t* gate, mfnerf_stream_t stream);
 
 /* vren.composite_test_fw (binding.cpp:176-201, volumerendering.cu:205-285).  sigmas (n_alive,N_samples),
  * rgbs (n_alive,N_samples,3), deltas, ts (n_alive,N_samples); in place on alive_indices, opacity,
@@ -299,21 +291,6 @@ int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32
                                           int64_t n_params, void* workspace, int64_t n_slots, float* level_l1,
                                           const mfnerf_adam_fused* adam, int32_t* step_dev, mfnerf_amp_state* amp,
                                           void* packed, int rgb_width, int32_t* gate, mfnerf_stream_t stream);
-/* mfnerf_grid_encode_bw_binned_adam_all after a field_bw whose weight-gradient fold was DEFERRED
- * (mfnerf_field_bw with grad_xyz = grad_rgb = NULL; field_workspace = its workspace): the MLPs'
- * values [0, N_DW) are left out of the accumulate launch's leading workgroups, and a launch after it
- * reduces field_bw's slab rows in mfnerf_field_bw_reduce's order and applies Adam to the MLP weights
- * as it goes, before the last pass repacks them and does the bookkeeping.  grads[0, N_DW) must be zero on entry (it
- * stays zero).  Same bits as mfnerf_field_bw_reduce + mfnerf_grid_encode_bw_binned_adam_all: the fold
- * moves from beside the next step's march (field_bw's tail) to after the scatter.  Requires the
- * non-finite flag to be final when field_bw returns, which field_bw guarantees by checking its slab
- * rows (every row finite bounds the sum far inside f32).  gate: as for _adam_all. */
-int mfnerf_grid_encode_bw_binned_adam_all_slab(const float* x, int64_t n, const int32_t* n_dev, float x_min,
-                                               float x_range, const mfnerf_grid_desc* desc, const float* dL_dout,
-                                               float* grads, int64_t n_params, void* workspace, int64_t n_slots,
-                                               float* level_l1, const mfnerf_adam_fused* adam, int32_t* step_dev,
-                                               mfnerf_amp_state* amp, void* packed, int rgb_width,
-                                               const void* field_workspace, int32_t* gate, mfnerf_stream_t stream);
 
 /* out[l] += sum over rows i < n (or *n_dev) of |dL_dout[i][2l]| + |dL_dout[i][2l+1]| (f32). */
 int mfnerf_grid_level_l1(const float* dL_dout, int64_t n, const int32_t* n_dev, int n_levels, float* out,
@@ -574,10 +551,6 @@ int mfnerf_flag_from_shard(const float* g_shard, int32_t* flag, mfnerf_stream_t 
  * waited for.  Ordering only: data hazards must still be covered by stream events. */
 int mfnerf_gate_signal(int32_t* gate, mfnerf_stream_t stream);
 int mfnerf_gate_wait(int32_t* gate, int64_t timeout_us, mfnerf_stream_t stream);
-/* The wait as a stream operation (hipStreamWaitValue32, GTE): the stream's queue holds until
- * gate[0] >= target -- no resident wave, no timeout; the caller counts the signals it enqueued
- * (the gated march's host path, round 4: mfnerf_gate_wait's one thread polled for ~130 us per step). */
-int mfnerf_gate_wait_stream(const int32_t* gate, int32_t target, mfnerf_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1330,16 +1330,9 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 
 constexpr int BW_BLOCKS = 256;  // one workgroup per CU (persistent)
 
-// W = 64 through field_bw_coop_kernel (two waves per SIMD) unless MFNERF_FIELD_BW_COOP=0; read once
-// per process (the workspace's slab rows and the deferred fold must agree with the kernel that ran)
-bool coop64() {
-    static const bool on = [] {
-        const char* e = getenv("MFNERF_FIELD_BW_COOP");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-int bw_rows(int w) { return (w == 64 && coop64()) ? COOP_BLOCKS : BW_BLOCKS; }
+// W = 64 through field_bw_coop_kernel (two waves per SIMD, COOP_BLOCKS slab rows)
+bool coop64() { return true; }
+int bw_rows(int w) { return w == 64 ? COOP_BLOCKS : BW_BLOCKS; }
 
 bool width_ok(int w) { return w == 64 || w == 128; }
 

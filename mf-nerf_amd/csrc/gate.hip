@@ -43,19 +43,6 @@ int mfnerf_gate_signal(int32_t* gate, mfnerf_stream_t stream) {
     return mfn_check_launch("gate_signal");
 }
 
-int mfnerf_gate_wait_stream(const int32_t* gate, int32_t target, mfnerf_stream_t stream) {
-    if (!gate) { mfn_set_error("gate_wait_stream: null pointer"); return MFN_ERR_INVALID; }
-    // the stream's queue holds at a wait packet until gate[0] >= target: no wave resident, no
-    // timeout (the caller pairs every wait with a signal it has already enqueued)
-    const hipError_t e = hipStreamWaitValue32(stream, const_cast<int32_t*>(gate), (uint32_t)target,
-                                              hipStreamWaitValueGte, 0xFFFFFFFFu);
-    if (e != hipSuccess) {
-        mfn_set_error("gate_wait_stream: hipStreamWaitValue32: %s", hipGetErrorString(e));
-        return MFN_ERR_LAUNCH;
-    }
-    return MFN_OK;
-}
-
 int mfnerf_gate_wait(int32_t* gate, int64_t timeout_us, mfnerf_stream_t stream) {
     if (!gate || timeout_us < 0) { mfn_set_error("gate_wait: bad arguments"); return MFN_ERR_INVALID; }
     hipLaunchKernelGGL(gate_wait_kernel, dim3(1), dim3(64), 0, stream, gate, timeout_us * 100, 0);

@@ -874,9 +874,6 @@ struct BinPlan {
     uint32_t t_offset[MFN_MAX_LEVELS], t_size[MFN_MAX_LEVELS];
     int t_bin0[MFN_MAX_LEVELS + 1];  // first bin of each table; t_bin0[n_tables] = n_bins
     int t_level[MFN_MAX_LEVELS];     // a level of each table (its fixed-point scale)
-    int scan_waves;                  // waves scanning a level's bin chunks (MFNERF_SCAN_WAVES; A/B)
-    int lane_map;                    // 1: the accumulate's slots rotated over its lanes' registers; 0: not
-                                     // (MFNERF_BIN_LANEMAP; A/B)
 };
 
 __device__ __forceinline__ int bin_table(const BinPlan& P, int b) {
@@ -1174,12 +1171,114 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
     // the coarse levels' rows) spread over many units, so every slot fills close to the mean
     const int64_t n_chunks = (nn + 15) / 16;
     const int64_t m = n_chunks > u ? ((n_chunks - 1 - u) / UNITS + 1) * 16 : 0;  // this unit's sample slots
-    // the store of the staged level (prev_b0: its table's first bin; parity: its gdst buffer)
-    int prev_b0 = -1, par = 0;
-    auto store_prev = [&]() {
-        if (prev_b0 < 0) return;
-        const int total = s_total[par ^ 1];
-        const int2* gd = gdst[par ^ 1];
+    // Round 5: two barriers per level instead of three.  Phase A places level j's ranked records into
+    // the stage and then counts level j + 1 (the next tile's first level after the last); phase B
+    // stores level j's stage into the slots and scans level j + 1's bin counts.  Each LDS buffer is
+    // written and read in different phases: the stage (A: place, B: store), toff (B: scan, A: place),
+    // hist2 / gdst / s_total by level parity (count and scan of j + 1 beside place and store of j).
+    int par = 0;  // parity of the level whose records R holds (its hist2 / gdst / s_total buffers)
+    BinRec R[8];
+    StagedSample<MAXB> S[SPT];
+    bool live[SPT];
+    auto stage_tile = [&](int64_t base) {
+#pragma unroll
+        for (int q = 0; q < SPT; ++q) {
+            const int64_t k = base + (int64_t)q * TH + threadIdx.x;
+            const int64_t i = ((k >> 4) * UNITS + u) * 16 + (k & 15);  // chunk k/16 of the unit
+            live[q] = k < m && i < nn;
+            if (live[q]) stage_sample(D, P, X, x_min, x_range, dy, i, S[q]);
+        }
+    };
+    // count: level j's records computed once each, ranked in their bin by the LDS counter of parity cp;
+    // G(q) = sample q's dL/dy pair at level j
+    auto count = [&](int j, int cp, auto G) __attribute__((always_inline)) {
+        const int b0 = P.t_bin0[P.table_of[P.level[j]]];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) R[k].meta = ~0u;
+#pragma unroll
+        for (int q = 0; q < SPT; ++q) {
+            const SampleLevel Q = G(q);
+            if (!(live[q] && Q.live)) continue;
+            // the record's |a|, |b| maxima as two packed u16 (fp16 bits order like the values)
+            auto rank = [&](int k, int lb, uint2 r) {
+                R[k].r = r;
+                R[k].meta = (uint32_t)lb | ((uint32_t)atomicAdd(&hist2[cp][lb], 1) << 16);
+                rmax2 = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(
+                    __builtin_bit_cast(ushort2v, rmax2), __builtin_bit_cast(ushort2v, r.y & 0x7fff7fffu)));
+            };
+            if constexpr (PAIR) {
+                const int l = P.level[j];
+                const float fs = fs_s[l] * REC_DOWN;
+                pair_level_records(D, P, l, S[q].x, S[q].y, S[q].z, Q.g0 * fs, Q.g1 * fs,
+                                   [&](int yz, int lb, uint2 r) { rank(4 * q + yz, lb, r); });
+            } else {
+                level_records(D, P, j, S[q].x, S[q].y, S[q].z, Q.g0, Q.g1, fs_s[P.level[j]],
+                              [&](int sl, int bin, uint2 r) {
+                                  if (bin >= 0) rank(sl, bin - b0, r);
+                              });
+            }
+        }
+    };
+    // scan: level j's bins -> sorted tile offsets (toff) and slot places (gdst[cp]); a run's k-th
+    // record goes to slot position gdst + k.  Chunk q of 64 bins (consecutive lanes on consecutive LDS
+    // words: no bank conflicts) is scanned by wave q % 16 with an integer DPP wave scan; its carry (the
+    // bins of the chunks before it) is each lane's column sum over those chunks
+    auto scan = [&](int j, int cp) {
+        static_assert(MAX_TBINS == 1024, "hist2 indexing");
+        const int t = P.table_of[P.level[j]];
+        const int b0 = P.t_bin0[t], tb = P.t_bin0[t + 1] - b0;
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        const int per = (tb + 63) >> 6;
+        const int* hs = hist2[cp];
+        constexpr int nw = SC_THREADS / 64;
+        for (int q = wv; q < per; q += nw) {
+            int col = 0;  // chunks before q are whole (q < per - 1 ... < tb)
+            for (int q2 = 0; q2 < q; ++q2) col += hs[q2 * 64 + lane];
+            col += dppz_i<0x111, 0xF>(col); col += dppz_i<0x112, 0xF>(col);
+            col += dppz_i<0x114, 0xF>(col); col += dppz_i<0x118, 0xF>(col);
+            col += dppz_i<0x142, 0xA>(col); col += dppz_i<0x143, 0xC>(col);
+            const int carry = __builtin_amdgcn_readlane(col, 63);
+            const int lb = q * 64 + lane;
+            const int c = lb < tb ? hs[lb] : 0;
+            int x = c;
+            x += dppz_i<0x111, 0xF>(x); x += dppz_i<0x112, 0xF>(x);
+            x += dppz_i<0x114, 0xF>(x); x += dppz_i<0x118, 0xF>(x);
+            x += dppz_i<0x142, 0xA>(x); x += dppz_i<0x143, 0xC>(x);
+            const int run = carry + x - c;
+            if (lb < tb) {
+                toff[lb] = run;
+                const int gb = b0 + lb, cl = gb;
+                int32_t* gc = scnt + (int64_t)gb * UNITS + u;  // (bins past LCUR)
+                const int cu = cl < LCUR ? cursor[cl] : *gc;
+                // record k of the sorted stage is position cu - run + k of the slot
+                gdst[cp][lb] = make_int2((int)((uint32_t)(b0 + lb) * UNITS + u) * (int)slot + cu - run,
+                                         run + (int)slot - cu);
+                if (cl < LCUR) cursor[cl] = cu + c;
+                else *gc = cu + c;
+            }
+            if (q == per - 1 && lane == 63) s_total[cp] = carry + x;
+        }
+    };
+    // place: level j's records (R, parity par) sorted by bin into the stage; its counts cleared for the
+    // level after next, which counts into the same buffer
+    auto place = [&](int j) {
+        const int t = P.table_of[P.level[j]];
+        const int tb = P.t_bin0[t + 1] - P.t_bin0[t];
+        for (int b = threadIdx.x; b < tb; b += TH) hist2[par][b] = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (R[k].meta == ~0u) continue;
+            const int lb = R[k].meta & 0xffff;
+            const int p = toff[lb] + (int)(R[k].meta >> 16);
+            stage[p] = R[k].r;
+            sbin[p] = (uint16_t)lb;
+        }
+    };
+    // store: level j's sorted stage as one contiguous run per bin into the unit's slot of the bin
+    auto store = [&](int j) {
+        const int b0 = P.t_bin0[P.table_of[P.level[j]]];
+        const int total = s_total[par];
+        const int2* gd = gdst[par];
         for (int k = threadIdx.x; k < total; k += TH) {
             const int lb = sbin[k];
             const int2 g = gd[lb];
@@ -1190,133 +1289,61 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                 __builtin_nontemporal_store((unsigned long long)r.x | ((unsigned long long)r.y << 32),
                                             reinterpret_cast<unsigned long long*>(dst));
             } else {
-                overflow_add(P, ovw, prev_b0 + lb, r);  // a full slot: into the overflow words
+                overflow_add(P, ovw, b0 + lb, r);  // a full slot: into the overflow words
             }
         }
     };
-    for (int64_t base = 0; base < m; base += (int64_t)SPT * TH) {
-        StagedSample<MAXB> S[SPT];
-        bool live[SPT];
-        // (round 4 measured lane l of wave w taking position w of chunk l + 64 q instead, so that one
-        // instruction's lanes hold 64 different rays: the counting atomics' address conflicts fell
-        // from 22 to 5.5 % of the LDS-active cycles, the bank conflicts stayed at 53 %, and the
-        // scattered staging loads made the kernel slower, 98 -> 102 us: not kept)
-#pragma unroll
-        for (int q = 0; q < SPT; ++q) {
-            const int64_t k = base + (int64_t)q * TH + threadIdx.x;
-            const int64_t i = ((k >> 4) * UNITS + u) * 16 + (k & 15);  // chunk k/16 of the unit
-            live[q] = k < m && i < nn;
-            if (live[q]) stage_sample(D, P, X, x_min, x_range, dy, i, S[q]);
+    // one level step: phase A (place j, count the next level), phase B (store j, scan the next level)
+    auto step = [&](int j, int64_t base, auto count_next) __attribute__((always_inline)) {
+        place(j);
+        int jn = j + 1;
+        bool next = true;
+        if (jn == P.n_binned) {  // the next tile's first level
+            jn = 0;
+            next = base + (int64_t)SPT * TH < m;
+            if (next) stage_tile(base + (int64_t)SPT * TH);
         }
-        // one level's pass over the tile; G(q) = sample q's dL/dy pair at level j
-        auto pass = [&](int j, auto G) __attribute__((always_inline)) {
-            const int t = P.table_of[P.level[j]];
-            const int b0 = P.t_bin0[t], tb = P.t_bin0[t + 1] - b0;
-            // count: each record computed once, ranked in its bin by the LDS counter
-            BinRec R[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) R[k].meta = ~0u;
-#pragma unroll
-            for (int q = 0; q < SPT; ++q) {
-                const SampleLevel Q = G(q);
-                if (!(live[q] && Q.live)) continue;
-                // the record's |a|, |b| maxima as two packed u16 (fp16 bits order like the values)
-                auto rank = [&](int k, int lb, uint2 r) {
-                    R[k].r = r;
-                    R[k].meta = (uint32_t)lb | ((uint32_t)atomicAdd(&hist2[par][lb], 1) << 16);
-                    rmax2 = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(
-                        __builtin_bit_cast(ushort2v, rmax2), __builtin_bit_cast(ushort2v, r.y & 0x7fff7fffu)));
-                };
-                if constexpr (PAIR) {
-                    const int l = P.level[j];
-                    const float fs = fs_s[l] * REC_DOWN;
-                    pair_level_records(D, P, l, S[q].x, S[q].y, S[q].z, Q.g0 * fs, Q.g1 * fs,
-                                       [&](int yz, int lb, uint2 r) { rank(4 * q + yz, lb, r); });
-                } else {
-                    level_records(D, P, j, S[q].x, S[q].y, S[q].z, Q.g0, Q.g1, fs_s[P.level[j]],
-                                  [&](int sl, int bin, uint2 r) {
-                                      if (bin >= 0) rank(sl, bin - b0, r);
-                                  });
-                }
-            }
-            store_prev();  // the previous level's sorted stage, beside this level's counting
-            __syncthreads();
-            // scan: bins -> sorted tile offsets; a run's k-th record goes to slot position gdst + k.
-            // Chunk q of 64 bins (consecutive lanes on consecutive LDS words: no bank conflicts) is
-            // scanned by wave q % waves with an integer DPP wave scan; its carry (the bins of the
-            // chunks before it) is each lane's column sum over those chunks, reduced once -- the
-            // chunks in parallel instead of one wave walking them in turn (round 3: 2.1 k cycles of
-            // one wave per level while the others waited)
-            {
-                static_assert(MAX_TBINS == 1024, "hist2 indexing");
-                const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-                const int per = (tb + 63) >> 6;
-                const int* hs = hist2[par];
-                const int nw = P.scan_waves;
-                for (int q = wv < nw ? wv : per; q < per; q += nw) {
-                    int col = 0;  // chunks before q are whole (q < per - 1 ... < tb)
-                    for (int q2 = 0; q2 < q; ++q2) col += hs[q2 * 64 + lane];
-                    col += dppz_i<0x111, 0xF>(col); col += dppz_i<0x112, 0xF>(col);
-                    col += dppz_i<0x114, 0xF>(col); col += dppz_i<0x118, 0xF>(col);
-                    col += dppz_i<0x142, 0xA>(col); col += dppz_i<0x143, 0xC>(col);
-                    const int carry = __builtin_amdgcn_readlane(col, 63);
-                    const int lb = q * 64 + lane;
-                    const int c = lb < tb ? hs[lb] : 0;
-                    int x = c;
-                    x += dppz_i<0x111, 0xF>(x); x += dppz_i<0x112, 0xF>(x);
-                    x += dppz_i<0x114, 0xF>(x); x += dppz_i<0x118, 0xF>(x);
-                    x += dppz_i<0x142, 0xA>(x); x += dppz_i<0x143, 0xC>(x);
-                    const int run = carry + x - c;
-                    if (lb < tb) {
-                        toff[lb] = run;
-                        const int gb = b0 + lb, cl = gb;
-                        int32_t* gc = scnt + (int64_t)gb * UNITS + u;  // (bins past LCUR)
-                        const int cu = cl < LCUR ? cursor[cl] : *gc;
-                        // record k of the sorted stage is position cu - run + k of the slot
-                        gdst[par][lb] = make_int2((int)((uint32_t)(b0 + lb) * UNITS + u) * (int)slot + cu - run,
-                                                  run + (int)slot - cu);
-                        if (cl < LCUR) cursor[cl] = cu + c;
-                        else *gc = cu + c;
-                    }
-                    if (q == per - 1 && lane == 63) s_total[par] = carry + x;
-                }
-            }
-            __syncthreads();
-            // place: the records sorted by bin into the stage (and this level's counts cleared for
-            // the level after next, which counts into the same buffer)
-            for (int b = threadIdx.x; b < tb; b += TH) hist2[par][b] = 0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                if (R[k].meta == ~0u) continue;
-                const int lb = R[k].meta & 0xffff;
-                const int p = toff[lb] + (int)(R[k].meta >> 16);
-                stage[p] = R[k].r;
-                sbin[p] = (uint16_t)lb;
-            }
-            __syncthreads();
-            prev_b0 = b0;
-            par ^= 1;
-        };
+        if (next) count_next(jn, par ^ 1);
+        __syncthreads();
+        store(j);
+        if (next) scan(jn, par ^ 1);
+        __syncthreads();
+        par ^= 1;
+    };
+    auto level_g = [&](int j) {  // runtime-level dL/dy pair (sample_level's register select)
+        return [&, j](int q) { return sample_level(D, P, S[q], j); };
+    };
+    if (m > 0) {  // the first tile's first level: count, scan
+        stage_tile(0);
+        count(0, 0, level_g(0));
+        __syncthreads();
+        scan(0, 0);
+        __syncthreads();
+    }
+    for (int64_t base = 0; base < m; base += (int64_t)SPT * TH) {
         if constexpr (PAIR && MAXB <= 10) {
             // the level loop written out: j a constant in every copy, so the staged pair is a plain
             // register (sample_level's select costs 2 MAXB v_cndmask per sample and level)
-            auto each = [&](auto jc) __attribute__((always_inline)) {
-                constexpr int j = decltype(jc)::value;
-                if (j < P.n_binned)
-                    pass(j, [&](int q) {
-                        SampleLevel r;
-                        r.g0 = S[q].g[2 * j];
-                        r.g1 = S[q].g[2 * j + 1];
-                        r.live = !(r.g0 == 0.0f && r.g1 == 0.0f);
-                        return r;
-                    });
+            auto count_c = [&](int jn, int cp) __attribute__((always_inline)) {
+                auto each = [&](auto jc) __attribute__((always_inline)) {
+                    constexpr int jj = decltype(jc)::value;
+                    if (jj == jn)
+                        count(jj, cp, [&](int q) {
+                            SampleLevel r;
+                            r.g0 = S[q].g[2 * jj];
+                            r.g1 = S[q].g[2 * jj + 1];
+                            r.live = !(r.g0 == 0.0f && r.g1 == 0.0f);
+                            return r;
+                        });
+                };
+                static_for<MAXB>(each);
             };
-            static_for<MAXB>(each);
+            for (int j = 0; j < P.n_binned; ++j) step(j, base, count_c);
         } else {
-            for (int j = 0; j < P.n_binned; ++j) pass(j, [&](int q) { return sample_level(D, P, S[q], j); });
+            for (int j = 0; j < P.n_binned; ++j)
+                step(j, base, [&](int jn, int cp) { count(jn, cp, level_g(jn)); });
         }
     }
-    store_prev();
     // the unit's largest contribution (one word per unit: the accumulate's per-partition bound is
     // sum over units of count x this max)
     {
@@ -1384,98 +1411,42 @@ __device__ __forceinline__ void accum_record(unsigned long long* img, int mask, 
 constexpr int ACC_THREADS = 512;
 static_assert(MAX_BIN_ENTRIES % ACC_THREADS == 0, "the fused Adam's per-thread entries");
 
-// The MLPs' part of the collective-free step's optimizer, run after the table's (the slab tail of
-// mfnerf_grid_encode_bw_binned_adam_all_slab): field_bw left its weight gradients as per-workgroup
-// slab rows (deferred fold), so slab_reduce_kernel's reduction runs HERE, after the scatter, instead
-// of right after field_bw, where it sat beside the next step's march (39 us there, r4f timeline).
-// Workgroup cg sums parameters [64 cg, 64 cg + 64) over the rows in slab_reduce_kernel's order and
-// applies Adam to them at once (the non-finite flag is final: field_bw checks its rows,
-// slab_row_flag).  The repack and the bookkeeping follow as adam_fixed_kernel's tail pass (a
-// last-workgroup repack here needs an agent-scope release per workgroup -- an L2 writeback each:
-// 58 us for this kernel in the r4g timeline).  Bit-identical to slab_reduce (into zeroed
-// gradients) + adam_fixed_kernel.
-template <int W>
-__global__ __launch_bounds__(256) void mlp_slab_tail_kernel(const float* __restrict__ slab, int rows,
-                                                            float* __restrict__ p, float* __restrict__ m,
-                                                            float* __restrict__ v, __half* __restrict__ p16,
-                                                            float lr,
-                                                            float b1, float b2, float eps,
-                                                            int32_t* __restrict__ step_dev,
-                                                            const float* __restrict__ lr_dev,
-                                                            const mfnerf_amp_state* __restrict__ amp) {
-    constexpr int N_DW = mfn_field::Geo<W>::N_DW;
-    static_assert(N_DW % 4 == 0, "float4 columns");
-    __shared__ float4 part[16][16];
-    const int c = threadIdx.x & 15, rg = threadIdx.x >> 4;
-    const int q0 = blockIdx.x * 64 + 4 * c;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (q0 < N_DW) {
-        const float4* src = reinterpret_cast<const float4*>(slab + q0);
-        constexpr int RS = N_DW / 4;
-        constexpr int U = 8;
-        for (int r0 = rg; r0 < rows; r0 += 16 * U) {
-            float4 x[U];
-#pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int r = r0 + 16 * k;
-                x[k] = r < rows ? src[(int64_t)r * RS] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int k = 0; k < U; ++k)
-                if (r0 + 16 * k < rows) { acc.x += x[k].x; acc.y += x[k].y; acc.z += x[k].z; acc.w += x[k].w; }
-        }
-    }
-    part[rg][c] = acc;
-    __syncthreads();
-    if (rg == 0 && q0 < N_DW) {
-        float4 t[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) t[k] = part[k][c];
-#pragma unroll
-        for (int w = 8; w > 0; w >>= 1)
-#pragma unroll
-            for (int k = 0; k < w; ++k) {
-                t[k].x += t[k + w].x; t[k].y += t[k + w].y; t[k].z += t[k + w].z; t[k].w += t[k + w].w;
-            }
-        const bool skipped = amp && amp->nonfinite;
-        if (!skipped) {
-            const int st = *step_dev + 1;
-            if (lr_dev) lr = *lr_dev;
-            const float bc1 = 1.0f - powf(b1, (float)st);
-            const float bc2 = 1.0f - powf(b2, (float)st);
-            // the gradient the unfused path's Adam reads: 0 + the sum (slab_reduce adds into zeros)
-            const float g[4] = {0.0f + t[0].x, 0.0f + t[0].y, 0.0f + t[0].z, 0.0f + t[0].w};
-            float4 pp = *reinterpret_cast<float4*>(p + q0);
-            float4 mm = *reinterpret_cast<float4*>(m + q0);
-            float4 vv = *reinterpret_cast<float4*>(v + q0);
-            mfn::adam_elem(pp.x, mm.x, vv.x, g[0], b1, b2, eps, lr, bc1, bc2);
-            mfn::adam_elem(pp.y, mm.y, vv.y, g[1], b1, b2, eps, lr, bc1, bc2);
-            mfn::adam_elem(pp.z, mm.z, vv.z, g[2], b1, b2, eps, lr, bc1, bc2);
-            mfn::adam_elem(pp.w, mm.w, vv.w, g[3], b1, b2, eps, lr, bc1, bc2);
-            *reinterpret_cast<float4*>(p + q0) = pp;
-            *reinterpret_cast<float4*>(m + q0) = mm;
-            *reinterpret_cast<float4*>(v + q0) = vv;
-            if (p16) {
-                __half2 a = __floats2half2_rn(pp.x, pp.y), b = __floats2half2_rn(pp.z, pp.w);
-                uint2 u; u.x = *reinterpret_cast<uint32_t*>(&a); u.y = *reinterpret_cast<uint32_t*>(&b);
-                *reinterpret_cast<uint2*>(p16 + q0) = u;
-            }
-        }
-    }
-}
-
-// The rest of the optimizer step carried by the accumulate's launch (mfnerf_grid_encode_bw_binned_adam_all):
-// its first n_blocks workgroups run adam_fixed_body over the float4 groups [0, end4) -- the MLPs and
-// the dense levels, whose gradients are final before the scatter -- beside the partitions' workgroups.
 struct AdamRest {
     float* g;            // the flat gradient (MLP floats, then the table's int32 sums)
     int* priv;           // the dense levels' private copies
     int64_t dense_vals, total_vals, end4;
     int n_blocks;        // 0: none
     int first;           // 1: the grid's first n_blocks workgroups (dispatched early), 0: its last
-    int64_t lo4;         // first float4 group (0; the MLPs' count when their update rides the slab tail)
     int32_t* gate;       // opened as the dense-level launch starts (NULL: none)
 };
+
+// Round 5: the partition's records are routed through an LDS stage by LDS-DMA
+// (global_load_lds_dword), so that a workgroup has ALL its record loads in flight at once.  The
+// round-4 form loaded 8 slots' first 32 records per half-wave into registers, waited, added, then
+// loaded the slots' records 32-63, then the next 8 slots: ~5 dependent memory round trips per
+// workgroup at 0.11 VMEM reads in flight per wave (PMC r04_final: waiting 50 % of the wave cycles).
+// Now: (1) the 256 slot counts (and the fused Adam's optimizer state of this thread's entries) are
+// loaded; (2) an exclusive prefix of the counts gives every slot's place in a compacted stage; (3)
+// wave w copies slots w, w + 8, ... into the stage, 32 records (64 lanes x 4 B) per DMA instruction,
+// with no register destination -- one round trip for the whole partition; (4) the adds read the
+// stage in a strided order (record 37 t mod 512 of each 512-record block for thread t) so one LDS
+// instruction's lanes hold records ~37 apart -- different slots, i.e. different rays -- instead of a
+// ray's run of consecutive samples in one cell (same-address atomics).  A partition holding more
+// records than the stage is done in chunks of ACC_RB records.  Same records, same integer adds:
+// bit-identical sums.  LDS: 16 KB image + 62 KB stage -> two workgroups per CU.
+constexpr int ACC_RB = 7936;
+struct AccumStage {
+    unsigned long long img[MAX_BIN_ENTRIES];
+    uint2 recs[ACC_RB];
+    int pre[UNITS + 1];  // exclusive prefix of the slots' record counts; pre[UNITS] = the partition's
+    float wsum[ACC_THREADS / 64];
+    int wtot[ACC_THREADS / 64];
+};
+union AccumShared {  // ONE __shared__ object (a second one beside an LDS-DMA stage can cost waits)
+    AccumStage a;
+    TableRegions tr;
+};
+static_assert(sizeof(AccumShared) <= 81920, "two accumulate workgroups per CU");
 
 __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, int64_t n,
                                                                 const int32_t* __restrict__ n_dev,
@@ -1489,10 +1460,11 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
                                                                 const float* __restrict__ level_l1,
                                                                 const mfnerf_adam_fused A, const AdamRest X,
                                                                 int float_out) {
+    __shared__ AccumShared S;
     const int rest_b = X.first ? (int)blockIdx.x : (int)blockIdx.x - P.n_bins;
     if (rest_b >= 0 && rest_b < X.n_blocks) {
         // independent of the slot-overflow flag: these values never go through the partitions
-        __shared__ TableRegions TR;
+        TableRegions& TR = S.tr;
         TR.build(D, level_l1, X.total_vals);
         const bool skipped = A.amp && A.amp->nonfinite;
         const int stp = *A.step_dev + 1;
@@ -1501,81 +1473,74 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         const float bc2 = 1.0f - powf(A.beta2, (float)stp);
         adam_fixed_body(A.params, X.g, A.m, A.v, reinterpret_cast<__half*>(A.p16), A.table_offset, X.priv,
                         X.dense_vals, X.total_vals, TR, lr, A.beta1, A.beta2, A.eps, bc1, bc2, skipped,
-                        X.lo4 + (int64_t)rest_b * blockDim.x + threadIdx.x, X.end4, (int64_t)X.n_blocks * blockDim.x);
+                        (int64_t)rest_b * blockDim.x + threadIdx.x, X.end4, (int64_t)X.n_blocks * blockDim.x);
         return;
     }
     const bool add_words = *ovf != 0;  // a slot overflowed: its records are in the gradient words
-    __shared__ unsigned long long img[MAX_BIN_ENTRIES];
+    unsigned long long* img = S.a.img;
     const int bin = (int)blockIdx.x - (X.first ? X.n_blocks : 0);
     const int n_ent = 1 << P.shift, mask = n_ent - 1;
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     const int64_t slot = slot_size(min(nn, n_slots), P);  // = bin_scatter_kernel's
-    // one unit's slot per half-wave (32 lanes; ~30 records per slot at the Lego config), QF slots
-    // in flight per half-wave: each slot's count and first 32 records are loaded together,
-    // unconditionally (a slot always holds >= 96 records, so lane hl < 32 stays inside it; records
-    // past the count are dropped below) -- one memory round trip instead of a dependent pair.
-    // Measured in round 2: 4 -> 16 -> 8 slots per round 0.709 -> 0.693 -> 0.683 ms/step; the records
-    // 32-63 loaded in the same round as well 0.711 (double the record reads); exact loads after the
-    // counts (round 3, 106 VGPRs, 2 workgroups per CU) 157 vs 108 us.
-    //
-    // Round 4: the records are loaded as above (a slot's 32 consecutive records per half-wave: a few
-    // whole lines per load), then ROTATED across the QF registers per lane -- lane hl's register q
-    // takes the record of slot (q + hl) mod QF -- so one LDS-add instruction carries records of QF
-    // different units' slots instead of 32 consecutive records of one.  A unit's slot holds a ray's
-    // consecutive samples in one cell as consecutive records (the same entry): in one instruction
-    // those were same-address LDS atomics, serialised (PMC r4e: address conflicts 59 % of the
-    // LDS-active cycles, 10.9 LDS-active cycles per LDS instruction).  Rotating the slot ASSIGNMENT
-    // instead (r4g) ended the conflicts but made each load touch 8 slots' lines: slower.  Here it
-    // is a 3-stage register barrel shift (v_cndmask) after coalesced loads.  Same records, same adds.
-    const int hw = threadIdx.x >> 5, hl = threadIdx.x & 31, n_hw = ACC_THREADS / 32;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    constexpr int NW = ACC_THREADS / 64;
     const int32_t* cnt = scnt + (int64_t)bin * UNITS;
     const uint2* base = rec + (int64_t)bin * UNITS * slot;
-    constexpr int QF = 8;
-    static_assert((QF & (QF - 1)) == 0, "slot rotation");
-    uint2 r[QF];
-    int c[QF];  // the count of slot q of the batch (uniform over the half-wave)
-    auto prefetch = [&](int u0) {
-#pragma unroll
-        for (int q = 0; q < QF; ++q) {
-            const int u = u0 + q * n_hw;
-            c[q] = u < UNITS ? min(cnt[u], (int32_t)slot) : 0;  // (records past a full slot: overflow_add)
-            // 32-bit record offsets in the partition (the scalar base + a 32-bit vector offset)
-            r[q] = base[(uint32_t)(u < UNITS ? u : 0) * (uint32_t)slot + (uint32_t)hl];
-        }
-    };
-    const int rot = P.lane_map ? (hl & (QF - 1)) : 0;
-    // r[q] <- r[(q + rot) mod QF]: log2(QF) conditional register rotations by 1, 2, 4
-    auto rotate = [&]() {
-#pragma unroll
-        for (int b = 1; b < QF; b <<= 1) {
-            const bool sh = (rot & b) != 0;
-            uint2 t[QF];
-#pragma unroll
-            for (int q = 0; q < QF; ++q) t[q] = r[q];
-#pragma unroll
-            for (int q = 0; q < QF; ++q) r[q] = sh ? t[(q + b) & (QF - 1)] : t[q];
-        }
-    };
-    prefetch(hw);  // the first round's loads overlap the image zeroing and the partition's bound
-    for (int i = threadIdx.x; i < n_ent; i += blockDim.x) img[i] = 0;
-    __syncthreads();
-    // the partition's bound (sum over units of count x max), summed in a fixed order -> its unit 2^-k
-    __shared__ float wsum[ACC_THREADS / 64];
+    const int t = bin_table(P, bin);
+    const int64_t e_lo = (int64_t)(bin - P.t_bin0[t]) << P.shift;
+    const int n_e = (int)min<int64_t>(n_ent, (int64_t)P.t_size[t] - e_lo);
+    // (1) the slot counts, each slot's largest contribution ...
+    int c = 0;
     float term = 0.0f;
     bool full = false;  // a slot of this partition overflowed (its extra records: overflow_add)
-    const uint32_t* sm = smax;
-    if ((int)threadIdx.x < UNITS) {
-        const int u = threadIdx.x;
-        term = (float)min(cnt[u], (int32_t)slot) * __uint_as_float(sm[u]);
-        full = cnt[u] > slot;
+    if (tid < UNITS) {
+        const int c0 = cnt[tid];
+        c = min(c0, (int32_t)slot);
+        full = c0 > slot;
+        term = (float)c * __uint_as_float(smax[tid]);
+    }
+    // ... and, fused, this thread's entries' optimizer state: it lands while the records travel
+    constexpr int IT = MAX_BIN_ENTRIES / ACC_THREADS;
+    float2 p[IT], m[IT], v[IT];
+    const int64_t base_v = A.table_offset + 2 * ((int64_t)P.t_offset[t] + e_lo);
+    float2* __restrict__ pp = reinterpret_cast<float2*>(A.params + base_v);
+    float2* __restrict__ mm = reinterpret_cast<float2*>(A.m + base_v);
+    float2* __restrict__ vv = reinterpret_cast<float2*>(A.v + base_v);
+    if (A.params) {
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int i = tid + k * ACC_THREADS;
+            if (i < n_e) { p[k] = pp[i]; m[k] = mm[i]; v[k] = vv[i]; }
+        }
+    }
+    for (int i = tid; i < n_ent; i += ACC_THREADS) img[i] = 0;
+    // (2) exclusive prefix of the counts (waves 0-3 hold them), and the partition's bound (sum over
+    // units of count x max, summed in a fixed order) -> its unit 2^-k
+    int x = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) term += __shfl_xor(term, off, 64);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = term;
+    if (lane == 63) S.a.wtot[wv] = x;
+    if (lane == 0) S.a.wsum[wv] = term;
     full = __syncthreads_or(full);
+    {
+        int before = 0, total = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            const int s = S.a.wtot[k];
+            before += k < wv ? s : 0;
+            total += s;
+        }
+        if (tid < UNITS) S.a.pre[tid] = before + x - c;
+        if (tid == 0) S.a.pre[UNITS] = total;
+    }
     float bound = 0.0f;
 #pragma unroll
-    for (int k = 0; k < ACC_THREADS / 64; ++k) bound += wsum[k];
+    for (int k = 0; k < NW; ++k) bound += S.a.wsum[k];
     int kbits = 0;
     // a partition with an overflowed slot sums at the table's own unit: every contribution, in the
     // image or added by overflow_add, is then rounded alike, so the sum does not depend on which of
@@ -1586,39 +1551,42 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         kbits = max(0, min(30, 30 - e));
     }
     const float k2 = ldexpf(1.0f, kbits + 15);  // the records' values are 2^-15 x table units
-    for (int u0 = hw; u0 < UNITS; u0 += QF * n_hw) {
-        if (u0 != hw) prefetch(u0);
-        // records 32..63 of the slots holding more (~35 % of them at the Lego config), loaded only by
-        // the lanes that have one, all issued before the first batch's adds (round 2 loaded them one
-        // slot at a time inside the add loop: a dependent round trip per slot)
-        uint2 r2[QF];
-        // which of this lane's records are live (bit q: record hl of slot q), rotated like r (before
-        // the second records' loads: their registers are not live across the rotation)
-        uint32_t live = 0;
-#pragma unroll
-        for (int q = 0; q < QF; ++q) live |= (uint32_t)(hl < c[q]) << q;
-        live = ((live | (live << QF)) >> rot) & ((1u << QF) - 1);
-        rotate();
-#pragma unroll
-        for (int q = 0; q < QF; ++q) {
-            const int u = u0 + q * n_hw;
-            r2[q] = hl + 32 < c[q] ? base[(uint32_t)u * (uint32_t)slot + (uint32_t)(hl + 32)] : make_uint2(0u, 0u);
+    __syncthreads();
+    const int T = S.a.pre[UNITS];
+    // lane j < 32 of wave wv: the run bounds of slot wv + NW j (read by the wave one slot at a time)
+    const int my_u = wv + NW * (lane & 31);
+    const int my_lo = my_u < UNITS ? S.a.pre[my_u] : T, my_hi = my_u < UNITS ? S.a.pre[my_u + 1] : T;
+    for (int c0 = 0; c0 < T; c0 += ACC_RB) {
+        const int c1 = min(T, c0 + ACC_RB);
+        if (c0 > 0) __syncthreads();  // the previous chunk's adds are done with the stage
+        // (3) wave wv copies the part of its slots' runs inside [c0, c1), 32 records per instruction
+        for (int j = 0; NW * j + wv < UNITS; ++j) {
+            const int lo = max(__builtin_amdgcn_readlane(my_lo, j), c0);
+            const int hi = min(__builtin_amdgcn_readlane(my_hi, j), c1);
+            const int r0 = __builtin_amdgcn_readlane(my_lo, j);  // the slot's first record's place
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(base + (uint32_t)(NW * j + wv) * (uint32_t)slot);
+            for (int q = lo; q < hi; q += 32) {
+                const int k = q + (lane >> 1);  // record k of the compacted partition, dword lane & 1
+                if (k < hi)
+                    __builtin_amdgcn_global_load_lds(src + 2 * (k - r0) + (lane & 1), &S.a.recs[q - c0], 4, 0, 0);
+            }
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // (4) the adds, in a strided order over the stage
+        const int len = c1 - c0;
+        const int perm = (tid * 37) & (ACC_THREADS - 1);
+        constexpr int UR = 4;  // stage reads in flight per thread before the first add
+        for (int i0 = 0; i0 < len; i0 += UR * ACC_THREADS) {
+            uint2 r[UR];
 #pragma unroll
-        for (int q = 0; q < QF; ++q)
-            if ((live >> q) & 1u) accum_record(img, mask, r[q], k2);
+            for (int q = 0; q < UR; ++q) r[q] = S.a.recs[min(i0 + q * ACC_THREADS + perm, ACC_RB - 1)];
 #pragma unroll
-        for (int q = 0; q < QF; ++q) {
-            const int u = u0 + q * n_hw;
-            if (hl + 32 < c[q]) accum_record(img, mask, r2[q], k2);
-            for (int k = hl + 64; k < c[q]; k += 32)
-                accum_record(img, mask, base[(uint32_t)u * (uint32_t)slot + (uint32_t)k], k2);
+            for (int q = 0; q < UR; ++q)
+                if (i0 + q * ACC_THREADS + perm < len) accum_record(img, mask, r[q], k2);
         }
     }
     __syncthreads();
-    const int t = bin_table(P, bin);
-    const int64_t e_lo = (int64_t)(bin - P.t_bin0[t]) << P.shift;
-    const int n_e = (int)min<int64_t>(n_ent, (int64_t)P.t_size[t] - e_lo);
     int* dst = grad + 2 * ((int64_t)P.t_offset[t] + e_lo);
     int2* ow = reinterpret_cast<int2*>(ovw) + ((int64_t)(P.t_offset[t] - P.t_offset[0]) + e_lo);  // overflow words
     const int rnd = kbits > 0 ? 1 << (kbits - 1) : 0;
@@ -1629,7 +1597,6 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         const float sc = table_fixed_scale(D, level_l1, P.t_level[t]);
         const float is = sc > 0.0f ? 1.0f / sc : 0.0f;
         if (add_words) {  // the overflowed records' sums join the image; the words are zeroed
-            __syncthreads();
             for (int i = threadIdx.x; i < n_e; i += blockDim.x) {
                 const int2 g = ow[i];  // overflow_add's packed word
                 const unsigned long long w = img[i];
@@ -1646,23 +1613,10 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         const float lr = A.lr_dev ? *A.lr_dev : A.lr;
         const float bc1 = 1.0f - powf(A.beta1, (float)stp);
         const float bc2 = 1.0f - powf(A.beta2, (float)stp);
-        const int64_t base_v = A.table_offset + 2 * ((int64_t)P.t_offset[t] + e_lo);
-        float2* __restrict__ pp = reinterpret_cast<float2*>(A.params + base_v);
-        float2* __restrict__ mm = reinterpret_cast<float2*>(A.m + base_v);
-        float2* __restrict__ vv = reinterpret_cast<float2*>(A.v + base_v);
         __half2* __restrict__ hh = reinterpret_cast<__half2*>(reinterpret_cast<__half*>(A.p16) + base_v);
-        // every entry's optimizer state loaded before the first update (a load after the previous
-        // entry's stores would be one HBM round trip per entry the thread owns)
-        constexpr int IT = MAX_BIN_ENTRIES / ACC_THREADS;
-        float2 p[IT], m[IT], v[IT];
 #pragma unroll
         for (int k = 0; k < IT; ++k) {
-            const int i = (int)threadIdx.x + k * ACC_THREADS;
-            if (i < n_e) { p[k] = pp[i]; m[k] = mm[i]; v[k] = vv[i]; }
-        }
-#pragma unroll
-        for (int k = 0; k < IT; ++k) {
-            const int i = (int)threadIdx.x + k * ACC_THREADS;
+            const int i = tid + k * ACC_THREADS;
             if (i >= n_e) break;
             const unsigned long long w = img[i];
             const int lo = (int)(uint32_t)w, hi = (int)(uint32_t)(w >> 32) + (lo < 0);
@@ -1739,10 +1693,6 @@ int bin_plan(const mfnerf_grid_desc* d, BinPlan* P) {
     }
     P->t_bin0[P->n_tables] = nb;
     P->n_bins = nb;
-    const char* sw = getenv("MFNERF_SCAN_WAVES");
-    P->scan_waves = sw && atoi(sw) >= 1 && atoi(sw) <= SC_THREADS / 64 ? atoi(sw) : SC_THREADS / 64;
-    const char* lm = getenv("MFNERF_BIN_LANEMAP");
-    P->lane_map = lm ? (atoi(lm) != 0) : 1;
     if (P->n_binned > MAX_BINNED) return -1;
     for (int j = 1; j < P->n_binned; ++j)  // the binned levels are contiguous (staged dL/dy rows)
         if (P->level[j] != P->level[0] + j) return -1;
@@ -2081,12 +2031,8 @@ namespace {
 int adam_all_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, float x_range,
                   const mfnerf_grid_desc* desc, const float* dL_dout, float* grads, int64_t n_params,
                   void* workspace, int64_t n_slots, float* level_l1, const mfnerf_adam_fused* adam,
-                  int32_t* step_dev, mfnerf_amp_state* amp, void* packed, int rgb_width, const float* slab,
-                  int slab_rows, int32_t* gate, mfnerf_stream_t stream) {
-    if (slab && ((rgb_width != 64 && rgb_width != 128) || slab_rows <= 0 || !adam || !adam->params)) {
-        mfn_set_error("grid_encode_bw_binned_adam_all_slab: bad slab (rgb_width 64 or 128, rows > 0)");
-        return MFN_ERR_INVALID;
-    }
+                  int32_t* step_dev, mfnerf_amp_state* amp, void* packed, int rgb_width, int32_t* gate,
+                  mfnerf_stream_t stream) {
     if (packed && ((rgb_width != 64 && rgb_width != 128) || !adam || !adam->p16)) {
         mfn_set_error("grid_encode_bw_binned_adam_all: the repack needs rgb_width 64 or 128 and adam->p16");
         return MFN_ERR_INVALID;
@@ -2119,27 +2065,16 @@ int adam_all_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, 
         return MFN_ERR_INVALID;
     }
     // [0, fused_from) by the accumulate launch's leading workgroups (one float4 per thread, <= 256 of
-    // them); with the slab tail the MLPs' values [0, N_DW) are left to it
-    const int64_t n_dw = !slab ? 0 : rgb_width == 64 ? mfn_field::Geo<64>::N_DW : mfn_field::Geo<128>::N_DW;
-    if (n_dw % 4 || n_dw > adam->table_offset) {
-        mfn_set_error("grid_encode_bw_binned_adam_all_slab: the MLP weights must precede the table");
-        return MFN_ERR_INVALID;
-    }
-    AdamRest X{grads, (int*)workspace, 2 * dense_entries_of(desc), total, fused_from / 4, 0, 1, n_dw / 4, gate};
+    // them)
+    AdamRest X{grads, (int*)workspace, 2 * dense_entries_of(desc), total, fused_from / 4, 0, 1, gate};
     // <= 256 workgroups, the grid's first (256 vs 64 of them 0.655 vs 0.657 ms/step; first vs last
     // in the grid within noise)
-    const int64_t want = div_up<int64_t>((fused_from - n_dw) / 4, ACC_THREADS);
+    const int64_t want = div_up<int64_t>(fused_from / 4, ACC_THREADS);
     X.n_blocks = (int)(want < 1 ? 1 : (want < 256 ? want : 256));
     X.first = 1;
     st = binned_impl(x, n, n_dev, x_min, x_range, desc, dL_dout, grads + adam->table_offset, workspace, n_slots,
                      level_l1, 3, adam, stream, &X);
     if (st) return st;
-    if (slab) {  // the MLPs: their slab rows reduced + Adam (the tail pass below repacks them)
-        auto tk = rgb_width == 64 ? mlp_slab_tail_kernel<64> : mlp_slab_tail_kernel<128>;
-        hipLaunchKernelGGL(tk, dim3((unsigned)div_up<int64_t>(n_dw, 64)), dim3(256), 0, stream, slab, slab_rows,
-                           adam->params, adam->m, adam->v, (__half*)adam->p16, adam->lr, adam->beta1, adam->beta2,
-                           adam->eps, step_dev, adam->lr_dev, amp);
-    }
     // the MLP repack and the step's bookkeeping (step count, loss scale, level_l1 zeroed) by the last
     // workgroup -- after every workgroup of the accumulate has read them
     hipLaunchKernelGGL(adam_fixed_kernel, dim3(64), dim3(256), 0, stream, adam->params, grads, adam->m, adam->v,
@@ -2162,22 +2097,7 @@ int mfnerf_grid_encode_bw_binned_adam_all(const float* x, int64_t n, const int32
                                           const mfnerf_adam_fused* adam, int32_t* step_dev, mfnerf_amp_state* amp,
                                           void* packed, int rgb_width, int32_t* gate, mfnerf_stream_t stream) {
     return adam_all_impl(x, n, n_dev, x_min, x_range, desc, dL_dout, grads, n_params, workspace, n_slots, level_l1,
-                         adam, step_dev, amp, packed, rgb_width, nullptr, 0, gate, stream);
-}
-
-int mfnerf_grid_encode_bw_binned_adam_all_slab(const float* x, int64_t n, const int32_t* n_dev, float x_min,
-                                               float x_range, const mfnerf_grid_desc* desc, const float* dL_dout,
-                                               float* grads, int64_t n_params, void* workspace, int64_t n_slots,
-                                               float* level_l1, const mfnerf_adam_fused* adam, int32_t* step_dev,
-                                               mfnerf_amp_state* amp, void* packed, int rgb_width,
-                                               const void* field_workspace, int32_t* gate, mfnerf_stream_t stream) {
-    if (!field_workspace) {
-        mfn_set_error("grid_encode_bw_binned_adam_all_slab: null field workspace");
-        return MFN_ERR_INVALID;
-    }
-    return adam_all_impl(x, n, n_dev, x_min, x_range, desc, dL_dout, grads, n_params, workspace, n_slots, level_l1,
-                         adam, step_dev, amp, packed, rgb_width, (const float*)field_workspace,
-                         mfnerf_field_bw_slab_rows(rgb_width), gate, stream);
+                         adam, step_dev, amp, packed, rgb_width, gate, stream);
 }
 
 int64_t mfnerf_grid_binned_first_value(const mfnerf_grid_desc* desc) {

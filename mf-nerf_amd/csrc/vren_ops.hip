@@ -233,6 +233,46 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
 }
 __device__ __forceinline__ int ffs64(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
 
+// One chunk of the chain on the lanes: its points, where the successor chain breaks, the next chunk's
+// base, and each live lane's cell with its bitfield byte requested (chunk_occ reads it later).
+struct MarchChunk {
+    float tl, x, y, z, next_base;
+    int chain_end;
+    bool live;
+    Cell c;
+    uint32_t bit;      // bit of the cell in its byte
+    uint32_t byte;     // the bitfield byte (in flight until chunk_occ)
+};
+
+__device__ __forceinline__ MarchChunk march_chunk(const MarchParams& p, float t_base, float dt, float t2, float ox,
+                                                  float oy, float oz, float dx, float dy, float dz, int lane) {
+    MarchChunk k;
+    const float delta = (t_base + dt) - t_base;
+    k.tl = fmaf((float)lane, delta, t_base);
+    const float succ = k.tl + dt;
+    const float tl_next = __shfl_down(k.tl, 1, 64);
+    const uint64_t bad = __ballot(lane < 63 && succ != tl_next);
+    k.chain_end = bad ? ffs64(bad) + 1 : 64;
+    k.next_base = readlane_f(succ, k.chain_end - 1);
+    k.live = lane < k.chain_end && k.tl < t2;
+    k.x = fmaf(k.tl, dx, ox); k.y = fmaf(k.tl, dy, oy); k.z = fmaf(k.tl, dz, oz);
+    // lookup_cell's arithmetic on every lane (branch-free: a load under a lane condition makes the
+    // compiler wait for every outstanding load where the paths join, i.e. for this prefetch), the
+    // byte load issued here and used a chunk later; a lane past the chain reads byte 0
+    const uint32_t g3 = (uint32_t)p.grid_size * p.grid_size * p.grid_size;
+    const int mip = max(mip_from_pos(k.x, k.y, k.z, p.cascades), mip_from_dt(dt, p.grid_size, p.cascades));
+    k.c.mip_bound = fminf(scalbnf(1.0f, mip - 1), p.scale);
+    const float inv = 1 / k.c.mip_bound;
+    const float gs = (float)p.grid_size, gm1 = (float)p.grid_size - 1.0f;
+    k.c.nx = (int)clampf(0.5f * fmaf(k.x, inv, 1.0f) * gs, 0.0f, gm1);
+    k.c.ny = (int)clampf(0.5f * fmaf(k.y, inv, 1.0f) * gs, 0.0f, gm1);
+    k.c.nz = (int)clampf(0.5f * fmaf(k.z, inv, 1.0f) * gs, 0.0f, gm1);
+    const uint32_t idx = (uint32_t)mip * g3 + morton3((uint32_t)k.c.nx, (uint32_t)k.c.ny, (uint32_t)k.c.nz);
+    k.bit = idx & 7;
+    k.byte = p.bitfield[k.live ? idx >> 3 : 0u];
+    return k;
+}
+
 __device__ __forceinline__ void march_wave_ray(const MarchParams& p, int64_t r, int32_t* __restrict__ counts,
                                                float* __restrict__ tbuf) {
     const int lane = threadIdx.x & 63;
@@ -250,24 +290,20 @@ __device__ __forceinline__ void march_wave_ray(const MarchParams& p, int64_t r, 
         t1 = fmaf(dt, p.noise[r], t1);
         float t_base = t1, pending = 0.0f;
         bool skip = false, done = false;
+        // round 5: the next chunk's points are pure arithmetic (the chain does not depend on the
+        // walk), so its bitfield bytes are requested before this chunk's walk -- one memory round trip
+        // hidden per chunk (the march runs beside the table-gradient scatter, where every load waits
+        // behind its traffic)
+        MarchChunk cur = march_chunk(p, t_base, dt, t2, ox, oy, oz, dx, dy, dz, lane);
         while (!done) {
             if (!(t_base < t2) || n >= limit) break;  // every later visited point fails the loop test
-            const float delta = (t_base + dt) - t_base;
-            const float tl = fmaf((float)lane, delta, t_base);
-            const float succ = tl + dt;
-            const float tl_next = __shfl_down(tl, 1, 64);
-            const uint64_t bad = __ballot(lane < 63 && succ != tl_next);
-            const int chain_end = bad ? ffs64(bad) + 1 : 64;
-            const float next_base = readlane_f(succ, chain_end - 1);
-            const bool live = lane < chain_end && tl < t2;
-            bool occ = false;
-            float tt = 0.0f, x = 0.0f, y = 0.0f, z = 0.0f;
-            if (live) {
-                x = fmaf(tl, dx, ox); y = fmaf(tl, dy, oy); z = fmaf(tl, dz, oz);
-                const Cell c = lookup_cell(x, y, z, dt, p.cascades, p.grid_size, p.scale, p.bitfield);
-                occ = c.occ;
-                if (!occ) tt = skip_target(tl, c, x, y, z, dx, dy, dz, dxi, dyi, dzi, gsi);
-            }
+            const MarchChunk nxt = march_chunk(p, cur.next_base, dt, t2, ox, oy, oz, dx, dy, dz, lane);
+            const float tl = cur.tl;
+            const int chain_end = cur.chain_end;
+            const bool live = cur.live;
+            const bool occ = live && ((cur.byte >> cur.bit) & 1u);
+            const float tt = live && !occ ? skip_target(tl, cur.c, cur.x, cur.y, cur.z, dx, dy, dz, dxi, dyi, dzi, gsi)
+                                          : 0.0f;
             const uint64_t live_m = __ballot(live), occ_m = __ballot(occ);
             const uint64_t chain_m = chain_end == 64 ? ~0ull : ((1ull << chain_end) - 1);
             uint64_t emit_m = 0;
@@ -293,14 +329,14 @@ __device__ __forceinline__ void march_wave_ray(const MarchParams& p, int64_t r, 
                 }
             }
             if ((emit_m >> lane) & 1) tr[n0 + __popcll(emit_m & ((1ull << lane) - 1))] = tl;
-            t_base = next_base;
+            t_base = cur.next_base;
+            cur = nxt;
         }
     }
     if (lane == 0) counts[r] = n;
 }
 
-// one ray per wave per trip; a wave takes rays w, w + W, ... (W = the grid's waves): with fewer waves
-// than rays the march leaves wave slots to the kernels it runs beside (MFNERF_MARCH_RPW)
+// one ray per wave per trip; a wave takes rays w, w + W, ... (W = the grid's waves)
 __global__ __launch_bounds__(256) void march_wave_kernel(MarchParams p, int64_t n_rays, int32_t* __restrict__ counts,
                                                          float* __restrict__ tbuf) {
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -550,8 +586,7 @@ __global__ __launch_bounds__(256) void composite_fused_wave_kernel(
     const float* __restrict__ target, int64_t n_mean, float lambda_o, float bg0, float bg1, float bg2,
     int64_t* __restrict__ total_samples, float* __restrict__ opacity, float* __restrict__ depth,
     float* __restrict__ rgb, float* __restrict__ ws, float* __restrict__ dL_drgb, float* __restrict__ dL_dop,
-    float* __restrict__ dL_dsigmas, float* __restrict__ dL_drgbs, float* __restrict__ loss_part,
-    int32_t* __restrict__ gate) {
+    float* __restrict__ dL_dsigmas, float* __restrict__ dL_drgbs, float* __restrict__ loss_part) {
     __shared__ float lsum[4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t n = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -653,16 +688,6 @@ __global__ __launch_bounds__(256) void composite_fused_wave_kernel(
     if (lane == 0) lsum[wid] = l;
     __syncthreads();
     if (threadIdx.x == 0 && loss_part) loss_part[blockIdx.x] = (lsum[0] + lsum[1]) + (lsum[2] + lsum[3]);
-    // gate (gate.hip's {signals, waits, ticket}): the workgroup that finishes last opens it -- the
-    // signal rides this launch instead of a one-thread kernel of its own (~6 us on the step's
-    // critical path, r4f timeline).  Scheduling only: the gated work reads nothing written here.
-    if (gate && threadIdx.x == 0) {
-        const int prev = __hip_atomic_fetch_add(gate + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == (int)gridDim.x - 1) {
-            __hip_atomic_store(gate + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(gate, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 __global__ void composite_test_kernel(const float* __restrict__ sigmas, const float* __restrict__ rgbs,
@@ -838,8 +863,7 @@ int mfnerf_raymarching_train(const float* rays_o, const float* rays_d, const flo
     float* tbuf = reinterpret_cast<float*>((char*)workspace + ((n_rays * 4 + 255) / 256) * 256);
     const unsigned nb = blocks_for(n_rays, RAY_BLOCK);
     const bool wave = exp_step_factor == 0.0f;  // constant dt: the wave-per-ray marcher applies
-    static const int rpw = [] { const char* e = getenv("MFNERF_MARCH_RPW"); return e && atoi(e) > 0 ? atoi(e) : 1; }();
-    const unsigned nbw = (unsigned)div_up<int64_t>(n_rays, 4 * (int64_t)rpw);
+    const unsigned nbw = (unsigned)div_up<int64_t>(n_rays, 4);
     if (wave)
         hipLaunchKernelGGL(march_wave_kernel, dim3(nbw), dim3(256), 0, stream, p, n_rays, counts, tbuf);
     else
@@ -914,18 +938,6 @@ int mfnerf_composite_train_fused(const float* sigmas, const float* rgbs, const f
                                  float bg_b, int64_t* total_samples, float* opacity, float* depth, float* rgb,
                                  float* ws, float* dL_drgb, float* dL_dopacity, float* dL_dsigmas, float* dL_drgbs,
                                  float* loss_partials, mfnerf_stream_t stream) {
-    return mfnerf_composite_train_fused_gated(sigmas, rgbs, deltas, ts, rays_a, n_rays, n_samples, T_threshold,
-                                              target, n_mean, lambda_opacity, bg_r, bg_g, bg_b, total_samples,
-                                              opacity, depth, rgb, ws, dL_drgb, dL_dopacity, dL_dsigmas, dL_drgbs,
-                                              loss_partials, nullptr, stream);
-}
-
-int mfnerf_composite_train_fused_gated(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
-                                       const int64_t* rays_a, int64_t n_rays, int64_t n_samples, float T_threshold,
-                                       const float* target, int64_t n_mean, float lambda_opacity, float bg_r,
-                                       float bg_g, float bg_b, int64_t* total_samples, float* opacity, float* depth,
-                                       float* rgb, float* ws, float* dL_drgb, float* dL_dopacity, float* dL_dsigmas,
-                                       float* dL_drgbs, float* loss_partials, int32_t* gate, mfnerf_stream_t stream) {
     if (n_rays < 0 || n_samples < 0 || n_mean < 0 || (n_mean > 0 && n_mean < n_rays)) {
         mfn_set_error("composite_train_fused: bad sizes"); return MFN_ERR_INVALID;
     }
@@ -938,7 +950,7 @@ int mfnerf_composite_train_fused_gated(const float* sigmas, const float* rgbs, c
     hipLaunchKernelGGL(composite_fused_wave_kernel, dim3(blocks_for(n_rays, 4)), dim3(256), 0, stream, sigmas, rgbs,
                        deltas, ts, rays_a, n_rays, T_threshold, target, n_mean, lambda_opacity, bg_r, bg_g, bg_b,
                        total_samples, opacity, depth, rgb, ws, dL_drgb, dL_dopacity, dL_dsigmas, dL_drgbs,
-                       loss_partials, gate);
+                       loss_partials);
     return mfn_check_launch("composite_train_fused");
 }
 

@@ -62,8 +62,6 @@ SIGNATURES = {
     "mfnerf_composite_train_bw": (_I, [_P] * 13 + [_I64, _I64, _F, _P, _P, _P]),
     "mfnerf_composite_train_fused": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _F, _P, _I64, _F, _F, _F, _F]
                                      + [_P] * 10 + [_P]),
-    "mfnerf_composite_train_fused_gated": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _F, _P, _I64, _F, _F, _F, _F]
-                                           + [_P] * 10 + [_P, _P]),
     "mfnerf_composite_test_fw": (_I, [_P, _P, _P, _P, _P, _I64, _I, _F, _P, _P, _P, _P, _P]),
     "mfnerf_distortion_loss_fw": (_I, [_P, _P, _P, _P, _I64, _I64, _P, _P, _P, _P]),
     "mfnerf_distortion_loss_bw": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P, _P]),
@@ -83,9 +81,6 @@ SIGNATURES = {
                                               _P, ctypes.POINTER(AdamFused), _P]),
     "mfnerf_grid_encode_bw_binned_adam_all": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _I64, _P,
                                                   _I64, _P, ctypes.POINTER(AdamFused), _P, _P, _P, _I, _P, _P]),
-    "mfnerf_grid_encode_bw_binned_adam_all_slab": (_I, [_P, _I64, _P, _F, _F, ctypes.POINTER(GridDesc), _P, _P, _I64,
-                                                       _P, _I64, _P, ctypes.POINTER(AdamFused), _P, _P, _P, _I, _P,
-                                                       _P, _P]),
     "mfnerf_grid_binned_first_value": (_I64, [ctypes.POINTER(GridDesc)]),
     "mfnerf_grid_dense_values": (_I64, [ctypes.POINTER(GridDesc)]),
     "mfnerf_grid_encode_bw_binned_flag_offset": (_I64, [ctypes.POINTER(GridDesc), _I64]),
@@ -130,7 +125,6 @@ SIGNATURES = {
     "mfnerf_flag_from_shard": (_I, [_P, _P, _P]),
     "mfnerf_gate_signal": (_I, [_P, _P]),
     "mfnerf_gate_wait": (_I, [_P, _I64, _P]),
-    "mfnerf_gate_wait_stream": (_I, [_P, _I, _P]),
 }
 
 _lib = None

@@ -58,6 +58,8 @@ def use_direct_rccl(on=True):
         from .rccl import Comm
         try:
             _COMM = Comm()
+            import atexit
+            atexit.register(use_direct_rccl, False)  # ncclCommDestroy at exit (a no-op once closed)
         except (OSError, RuntimeError) as e:  # e.g. no RCCL symbols: keep torch.distributed's collectives
             import warnings
             warnings.warn(f"direct RCCL communicator unavailable ({e}); using torch.distributed collectives")

@@ -21,7 +21,6 @@ Multi-GPU: run/replay(exchange=dp.allreduce_mean_) all-reduces `grads` between b
 """
 import ctypes
 import math
-import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -64,9 +63,9 @@ class StepConfig:
     loss_scale: float = 65536.0
     growth_interval: int = 2000
     fixed_point_grid: bool = True  # table gradient by int32 fixed-point atomics (n_parts == 1)
-    # ... of the hashed tables by partitioned LDS sums (mfnerf_grid_encode_bw_binned); MFNERF_BINNED=0
-    # selects the memory-side-atomic scatter for A/B measurements
-    binned_grid: bool = os.environ.get("MFNERF_BINNED", "1") == "1"
+    # ... of the hashed tables by partitioned LDS sums (mfnerf_grid_encode_bw_binned); False keeps the
+    # memory-side-atomic scatter (the layouts the partitions do not support take it anyway)
+    binned_grid: bool = True
     # the binned scatter's record slots are sized for this many samples per ray (the capacity is
     # max_samples = 1024 per ray; trained scenes march ~60): a step marching more than ~3x this
     # (the first steps, before the occupancy grid is pruned) overflows slots, whose extra records
@@ -394,10 +393,9 @@ class TrainStep:
         self.samples_marched.add_(mb.counters[0, 0] if self.n_parts == 1 else mb.counters[:, 0].sum())
         mark("march")
 
-    def _chain(self, batch: Batch, mb, q, mark, defer_fold=False):
+    def _chain(self, batch: Batch, mb, q, mark):
         """Part q: encode -> field -> composite -> loss -> composite bw -> field bw (no grid bw).
-        Part 0 also zeroes the gradient (every part's writes come after it).  defer_fold: field_bw
-        leaves the MLP weight gradients as its slab rows (folded by the slab tail, _fused_tail)."""
+        Part 0 also zeroes the gradient (every part's writes come after it)."""
         c, s = self.cfg, stream()
         t, m = self.parts[q], mb.part[q]
         Np, cap = self.Np, self.cap_p
@@ -425,11 +423,7 @@ class TrainStep:
                     target, c.n_rays, c.lambda_opacity, bg, bg, bg, ptr(t.total), ptr(t.opacity), ptr(t.depth),
                     ptr(t.rgb), ptr(t.ws), ptr(t.dL_drgb), ptr(t.dL_dop), ptr(t.dsig), ptr(t.drgb_s),
                     ptr(self.loss_parts[q * self._nb_part:]))
-            gate = getattr(mark, "ride", lambda _n: None)("composite")  # the gate signal riding the launch
-            if gate is not None:
-                call("mfnerf_composite_train_fused_gated", *args, gate, s)
-            else:
-                call("mfnerf_composite_train_fused", *args, s)
+            call("mfnerf_composite_train_fused", *args, s)
             mark("composite")
         else:
             call("mfnerf_composite_train_fw", ptr(t.sigma), ptr(t.rgb_s), ptr(m.deltas), ptr(m.ts), ptr(m.rays_a),
@@ -449,8 +443,8 @@ class TrainStep:
             mark("composite_bw")
         call("mfnerf_field_bw", ptr(t.feat), cap, ptr(m.dirs), cap, ptr(m.counter), ptr(self.packed), c.rgb_width,
              ptr(t.dsig), ptr(t.drgb_s), 0.0 if c.dynamic_loss_scale else self.grad_scale, ptr(t.dfeat),
-             None if defer_fold or store_fold else ptr(t.mlp_grad),
-             None if defer_fold or store_fold else ptr(t.mlp_grad[self.off_rgb:]),
+             None if store_fold else ptr(t.mlp_grad),
+             None if store_fold else ptr(t.mlp_grad[self.off_rgb:]),
              ptr(t.field_ws),
              self._amp_ptr(),
              ptr(self._level_l1) if self._fixed() else None, s)
@@ -483,8 +477,7 @@ class TrainStep:
     def _fused_adam_ok(self):
         """The collective-free replayed tail can run the partitioned tables' Adam inside the scatter's
         accumulate (mfnerf_grid_encode_bw_binned_adam + mfnerf_adam_step_fixed_partial)."""
-        return (self._binned() and self.shard is None and os.environ.get("MFNERF_FUSED_ADAM", "1") == "1"
-                and load().mfnerf_grid_binned_first_value(self.desc) >= 0)
+        return self._binned() and self.shard is None and load().mfnerf_grid_binned_first_value(self.desc) >= 0
 
     def _adam_fused_args(self):
         c = self.cfg
@@ -497,22 +490,21 @@ class TrainStep:
     def _grid_bw(self, mb, q, fuse_adam=False, gate=None):
         """Part q's hash-table gradient scatter (the dominant kernel, alone so it can be timed);
         fuse_adam: with the partitioned tables' Adam step (then _finish_update(partial=True));
-        fuse_adam="all": with the whole optimizer step (then only _pack()); "all-slab": the same after
-        a chain with a deferred weight-gradient fold (_chain(defer_fold=True)); gate (its pointer):
-        opened as the dense-level launch starts."""
+        fuse_adam="all": with the whole optimizer step and the MLP repack.  gate (the side stream's
+        gate pointer): opened as the scatter starts -- by the dense-level launch's first workgroup
+        where the launch takes a gate, else by a signal kernel of its own just before it."""
         t, m = self.parts[q], mb.part[q]
-        if self._binned() and fuse_adam in ("all", "all-slab"):
+        if gate is not None:
+            self._gate_opened += 1
+        if self._binned() and fuse_adam == "all":
             self._fused_args = self._adam_fused_args()  # kept alive: graphs capture the call
-            amp = self._amp_ptr()
-            # the last pass also repacks the MLP weights (no _pack() launch after it)
-            args = (ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min, self.x_range, self.desc, ptr(t.dfeat),
-                    ptr(self.grads), self.n_alloc, ptr(t.grid_ws), self._bin_slots(), ptr(self._level_l1),
-                    ctypes.byref(self._fused_args), ptr(self.step_dev), amp, ptr(self.packed), self.cfg.rgb_width)
-            if fuse_adam == "all-slab":
-                call("mfnerf_grid_encode_bw_binned_adam_all_slab", *args, ptr(t.field_ws), gate, stream())
-            else:
-                call("mfnerf_grid_encode_bw_binned_adam_all", *args, gate, stream())
+            call("mfnerf_grid_encode_bw_binned_adam_all", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min,
+                 self.x_range, self.desc, ptr(t.dfeat), ptr(self.grads), self.n_alloc, ptr(t.grid_ws),
+                 self._bin_slots(), ptr(self._level_l1), ctypes.byref(self._fused_args), ptr(self.step_dev),
+                 self._amp_ptr(), ptr(self.packed), self.cfg.rgb_width, gate, stream())
             return
+        if gate is not None:
+            call("mfnerf_gate_signal", gate, stream())
         if self._binned() and fuse_adam:
             self._fused_args = self._adam_fused_args()  # kept alive: graphs capture the call
             call("mfnerf_grid_encode_bw_binned_adam", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min,
@@ -531,39 +523,10 @@ class TrainStep:
              self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws),
              ptr(self._level_l1) if self._fixed() else None, stream())
 
-    def _slab_tail(self):
-        """MFNERF_SLAB_TAIL=1: the one-graph step folds the MLP weight gradients after the scatter
-        (mfnerf_grid_encode_bw_binned_adam_all_slab) instead of right after field_bw.  Off by
-        default: with the gate after field_bw the in-chain fold runs before the march starts (~12 us),
-        and moving it out put the march beside the dense-level scatter instead -- 0.5499-0.5547 vs
-        0.5431-0.5504 ms/step (r4i, r4k2)."""
-        return (os.environ.get("MFNERF_SLAB_TAIL", "0") == "1" and os.environ.get("MFNERF_FUSED_ADAM_ALL", "1") == "1"
-                and self.n_parts == 1)
-
-    def _fused_tail(self, j, slab=False, mark=None):
-        """The replayed collective-free tail: scatter + every Adam update, then the MLP repack.  By
-        default the MLPs' and dense levels' update rides the accumulate's launch
-        (mfnerf_grid_encode_bw_binned_adam_all); MFNERF_FUSED_ADAM_ALL=0 keeps it a pass of its own
-        after the scatter (mfnerf_adam_step_fixed_partial).  slab: the chain deferred the MLP weight
-        gradients' fold (the MLPs' update then runs in the slab tail).  Same bits every way."""
-        mark = mark or (lambda _n: None)
-        if slab:
-            gate = getattr(mark, "ride", lambda _n: None)("grid_bw")
-            self._grid_bw(self.mbuf[j], 0, fuse_adam="all-slab", gate=gate)
-            mark("grid_bw")
-        elif os.environ.get("MFNERF_FUSED_ADAM_ALL", "1") == "1":
-            gate = getattr(mark, "ride", lambda _n: None)("grid_bw")
-            self._grid_bw(self.mbuf[j], 0, fuse_adam="all", gate=gate)  # + the repack
-            mark("grid_bw")
-        else:
-            self._grid_bw(self.mbuf[j], 0, fuse_adam=True)
-            self._finish_update(partial=True)
-
     def _store_fold(self):
         """Sharded, one part, partitioned scatter whose float finish overwrites every table value
         before the partitioned tables (they are all dense-prefix values): the weight-gradient fold
-        stores instead of adding and the step zeroes no gradient prefix (one fill launch less;
-        MFNERF_DP_STORE_FOLD=0: off)."""
+        stores instead of adding and the step zeroes no gradient prefix (one fill launch less)."""
         v = getattr(self, "_store_fold_v", None)
         if v is None:
             lib = load()
@@ -571,8 +534,7 @@ class TrainStep:
                 self.cfg.rgb_width))
             v = (self.shard is not None and self.n_parts == 1 and self._binned() and self._fixed()
                  and self.off_table == n_dw
-                 and lib.mfnerf_grid_binned_first_value(self.desc) == lib.mfnerf_grid_dense_values(self.desc)
-                 and os.environ.get("MFNERF_DP_STORE_FOLD", "1") == "1")
+                 and lib.mfnerf_grid_binned_first_value(self.desc) == lib.mfnerf_grid_dense_values(self.desc))
             self._store_fold_v = v
         return v
 
@@ -593,14 +555,13 @@ class TrainStep:
         shard_flag (flag pointer, shards, shard length): mfnerf_flag_to_shards folded into the
         float finish when it has a table prefix to ride -- returns True when it was."""
         if not self._binned():
-            if gate is not None:
-                call("mfnerf_gate_signal", gate, stream())
-            self._grid_bw(mb, 0)
+            self._grid_bw(mb, 0, gate=gate)
             self._grid_finish(0)
             return False
         t, m = self.parts[0], mb.part[0]
-        fold_flag = (shard_flag is not None and load().mfnerf_grid_binned_first_value(self.desc) > 0
-                     and os.environ.get("MFNERF_DP_FLAG_FOLD", "1") == "1")
+        if gate is not None:
+            self._gate_opened += 1
+        fold_flag = shard_flag is not None and load().mfnerf_grid_binned_first_value(self.desc) > 0
         fl, fw, fs = shard_flag if fold_flag else (None, 0, 0)
         call("mfnerf_grid_encode_bw_binned_float", ptr(m.xyzs), self.cap_p, ptr(m.counter), self.x_min,
              self.x_range, self.desc, ptr(t.dfeat), ptr(self.grads[self.off_table:]), ptr(t.grid_ws),
@@ -770,8 +731,8 @@ class TrainStep:
 
         One part, no collective (the default N=1 step): ONE graph per step ("step": chain -> scatter
         with the whole optimizer in its launches -> repack); the next step's batch draw + march is a
-        graph of its own on a high-priority side stream, started by a device gate the step graph
-        opens after compositing (gate.hip).  Data parallel (one part): TWO graphs per step around
+        graph of its own on a side stream, started by a device gate the step graph opens as the
+        table-gradient scatter begins (gate.hip).  Data parallel (one part): TWO graphs per step around
         the collective ("dp_pre": repack -> chain -> scatter -> float gradient -> non-finite flag
         into the shards; "dp_post": flag back -> Adam on this rank's shard (sharded) or everywhere
         (all-reduce)), the collectives issued stream-ordered between them, the march gated the same
@@ -814,10 +775,13 @@ class TrainStep:
             "finish": [cap(lambda q=q: self._grid_finish(q)) for q in range(P)],
             "reduce": cap(self._reduce_parts) if P > 1 else None,
         }
-        gated = P == 1 and os.environ.get("MFNERF_GATED_MARCH", "1") == "1"
-        signal_at = self._gate_signaller() if gated else None
+        # one part: the next step's march waits on the side stream for the gate the step graph opens
+        # as its scatter begins (the dense-level launch's first workgroup, or a signal kernel)
+        gated = P == 1
+        self._gate = torch.zeros(4, dtype=torch.int32, device=self.dev)  # {signals, waits, ticket, -}
+        gp = ptr(self._gate) if gated else None
+        self._gate_opened = 0
         if gated:
-            gp = ptr(self._gate)
             self.graphs["march_gated"] = [
                 cap(lambda j=j: (call("mfnerf_gate_wait", gp, GATE_TIMEOUT_US, stream()), march(j)), rng=True)
                 for j in range(2)]
@@ -832,21 +796,16 @@ class TrainStep:
             # data parallel: the step up to the exchange, then the update after it
             w = self.shard[2] - self.shard[1] if self.shard is not None else self.n_alloc
             n_sh = self.n_alloc // w
-
             # sharded with amp: one launch reads the exchanged flag, updates and zeroes level_l1
-            fused_shard = (amp and self.shard is not None
-                           and os.environ.get("MFNERF_DP_SHARD_ADAM", "1") == "1")
+            fused_shard = amp and self.shard is not None
 
-            def dp_pre(j, mark):
+            def dp_pre(j):
                 self._pack()  # the previous step's all-gathered / updated fp16 weights
-                self._chain(self._static[j], self.mbuf[j], 0, mark)
-                # MFNERF_GATE_AT=grid_bw: opened by the dense-level launch's first workgroup
-                gate = getattr(mark, "ride", lambda _n: None)("grid_bw")
+                self._chain(self._static[j], self.mbuf[j], 0, nomark)
                 # the non-finite flag rides the collective: NaN into every shard's first value (by
                 # the float finish when it can, else a launch of its own)
                 sf = (ptr(self.finite_status), n_sh, w) if amp else None
-                folded = self._grid_bw_float(self.mbuf[j], zero_l1=not fused_shard, gate=gate, shard_flag=sf)
-                mark("grid_bw")
+                folded = self._grid_bw_float(self.mbuf[j], zero_l1=not fused_shard, gate=gp, shard_flag=sf)
                 if amp and not folded:
                     call("mfnerf_flag_to_shards", ptr(self.grads), n_sh, w, ptr(self.finite_status), stream())
 
@@ -861,7 +820,7 @@ class TrainStep:
                     if amp:
                         call("mfnerf_flag_from_shard", ptr(self.grads), ptr(self.finite_status), stream())
                     self._adam(self.grads, 0, self.n_alloc, True)
-            self.graphs["dp_pre"] = [cap(lambda j=j: dp_pre(j, signal_at or nomark)) for j in range(2)]
+            self.graphs["dp_pre"] = [cap(lambda j=j: dp_pre(j)) for j in range(2)]
             self.graphs["dp_post"] = cap(dp_post)
             from . import dp as _dp
             if _dp.direct_rccl() is not None:
@@ -869,7 +828,7 @@ class TrainStep:
                 # data-parallel step (repack, chain, scatter, exchange, Adam, all-gather) replays as
                 # ONE graph -- no host hop between the backward and the update
                 def dp_step(j):
-                    dp_pre(j, signal_at or nomark)
+                    dp_pre(j)
                     if self.shard is not None:
                         _dp.reduce_scatter_mean_(self.g_shard, self.grads)
                         dp_post()
@@ -883,47 +842,34 @@ class TrainStep:
             self.graphs["finish_update"] = cap(tail)
             fuse = self._fixed() and self._fused_adam_ok()
             # the scatter with the optimizer (one graph transition less) for untimed steps
-            if fuse:  # the tables' Adam inside the accumulate
+            if fuse:  # the whole optimizer inside the scatter's launches
                 self.graphs["grid_bw_tail"] = [cap(lambda j=j: self._fused_tail(j)) for j in range(2)]
             else:
                 self.graphs["grid_bw_tail"] = [cap(lambda j=j: (self._grid_bw(self.mbuf[j], 0), tail()))
                                                for j in range(2)]
-            if gated:
-                # the whole step as ONE graph: the chain signals the device gate where the host used
-                # to record the event that starts the next march
-                slab = fuse and self._slab_tail()
 
-                def step(j):
-                    self._chain(self._static[j], self.mbuf[j], 0, signal_at, defer_fold=slab)
-                    if fuse:
-                        self._fused_tail(j, slab=slab, mark=signal_at)
-                    else:
-                        self._grid_bw(self.mbuf[j], 0)
-                        tail()
-                self.graphs["step"] = [cap(lambda j=j: step(j)) for j in range(2)]
+            # the whole step as ONE graph: the scatter opens the device gate where the host used to
+            # record the event that starts the next march
+            def step(j):
+                self._chain(self._static[j], self.mbuf[j], 0, nomark)
+                if fuse:
+                    self._fused_tail(j, gate=gp)
+                else:
+                    self._grid_bw(self.mbuf[j], 0, gate=gp)
+                    tail()
+            self.graphs["step"] = [cap(lambda j=j: step(j)) for j in range(2)]
         n_gated = 2 * sum(1 for k in ("step", "dp_pre", "dp_step") if self.graphs.get(k) is not None)
-        if gated and signal_at.count != n_gated:
+        if gated and self._gate_opened != n_gated:
             # every gated graph must open the gate exactly once, or each gated march would spin for
             # GATE_TIMEOUT_US before starting
-            raise RuntimeError(f"gated graphs signalled {signal_at.count} times")
+            raise RuntimeError(f"gated graphs opened the gate {self._gate_opened} times, not {n_gated}")
         torch.cuda.synchronize()
         # the side stream at normal queue priority: a high-priority one measured the same alone
         # (0.601 vs 0.601 ms/step) but, once an RCCL communicator exists in the process, it ran every
-        # step at 1.10 ms (kernels on the main queue 2-7x slower; GPU_MAX_HW_QUEUES=8 also cured it:
-        # the extra streams share hardware queues) -- the data-parallel step would pay it on every rank
-        # (no priority below normal exists here: torch.cuda.Stream.priority_range() is (0, -1) on this
-        # ROCm, r4m -- a "least" priority side stream measured the same as normal; the step's own
-        # stream at high priority instead: 0.5567-0.5582 vs 0.5541-0.5542 ms, r04_v16)
-        hi = os.environ.get("MFNERF_SIDE_HIGH_PRIORITY", "0") == "1"
-        self._side = torch.cuda.Stream(device=self.dev, priority=torch.cuda.Stream.priority_range()[1] if hi else 0)
-        # MFNERF_GATE_STREAM=1: gated marches wait as a stream operation (mfnerf_gate_wait_stream) on
-        # the count of signals the host has enqueued -- 5 us/step faster (r4h), but it has no timeout:
-        # under rocprofv3 --pmc (dispatches serialised) it deadlocked the step (r4z2), and a side
-        # stream sharing a hardware queue with the main one (more streams than GPU_MAX_HW_QUEUES = 4,
-        # e.g. beside RCCL's) would block the very kernel that releases it.  Default: the captured
-        # polling kernel, which gives up after GATE_TIMEOUT_US.
-        self._gate_stream = gated and os.environ.get("MFNERF_GATE_STREAM", "0") == "1"
-        self._gate_target = 0
+        # step at 1.10 ms (kernels on the main queue 2-7x slower; the extra streams share hardware
+        # queues) -- the data-parallel step would pay it on every rank.  No priority below normal
+        # exists here (torch.cuda.Stream.priority_range() is (0, -1) on this ROCm, r4m).
+        self._side = torch.cuda.Stream(device=self.dev, priority=0)
         self._part_streams = [None] + [torch.cuda.Stream(device=self.dev) for _ in range(P - 1)]
         self._ev_march = [torch.cuda.Event(), torch.cuda.Event()]
         self._ev_start = torch.cuda.Event()
@@ -931,46 +877,12 @@ class TrainStep:
         self._ev_part = [torch.cuda.Event() for _ in range(P)]
         self._parity = 0
         self._primed = False
-        # where the next step's march starts: under this step's grid_bw (default) or at its start
-        self.march_early = os.environ.get("MFNERF_MARCH_EARLY", "0") == "1"
 
-    def _gate_signaller(self):
-        """mark() for the gated graphs: signals the device gate after the chain stage named by
-        MFNERF_GATE_AT (default "grid_bw", since round 4: the next draw + march start as the
-        table-gradient launches begin -- opened by the dense-level launch's first workgroup, no
-        signal kernel of its own -- after field_bw and its weight-gradient fold: 0.5469-0.5485 ms/step
-        vs 0.5475-0.5496 for "field_bw" (a signal kernel after the fold) and 0.5526-0.5581 for
-        "composite", which round 2 preferred when field_bw ran one wave per SIMD and left room beside
-        it; at the END of the dense-level launch 0.576; r4i, r4k2, r4l); counts its signals."""
-        self._gate = torch.zeros(4, dtype=torch.int32, device=self.dev)  # {signals, waits, ticket, -}
-        gp = ptr(self._gate)
-        gate_at = os.environ.get("MFNERF_GATE_AT", "grid_bw")
-        if gate_at not in ("grid_fw", "field_fw", "composite", "field_bw", "grid_bw"):
-            raise ValueError(f"MFNERF_GATE_AT={gate_at!r}: one of grid_fw, field_fw, composite, field_bw, grid_bw")
-        # with the distortion loss the chain composites in two stages: the gate opens after the
-        # second ("composite_bw"), the same place as after the fused kernel
-        name_ = "composite_bw" if gate_at == "composite" and self.cfg.lambda_distortion > 0 else gate_at
-
-        ridden = set()
-
-        def signal_at(name):
-            if name == name_:
-                if name in ridden:  # the stage's own kernel opened it (ride)
-                    ridden.discard(name)
-                else:
-                    call("mfnerf_gate_signal", gp, stream())
-                signal_at.count += 1
-
-        def ride(name):
-            """The gate pointer if stage `name`'s kernel should open the gate itself (its last
-            workgroup: no one-thread signal kernel on the critical path; MFNERF_GATE_RIDE=0: off)."""
-            if name == name_ and os.environ.get("MFNERF_GATE_RIDE", "1") == "1":
-                ridden.add(name)
-                return gp
-            return None
-        signal_at.count = 0
-        signal_at.ride = ride
-        return signal_at
+    def _fused_tail(self, j, gate=None):
+        """The replayed collective-free tail: the scatter with every Adam update in its launches
+        (mfnerf_grid_encode_bw_binned_adam_all: the MLPs' and dense levels' update rides the
+        accumulate's launch) and the MLP repack; gate: opened as the scatter starts."""
+        self._grid_bw(self.mbuf[j], 0, fuse_adam="all", gate=gate)
 
     def _stage_batch(self, j, batch):
         dst = self._static[j]
@@ -983,8 +895,8 @@ class TrainStep:
     def _march_on_side(self, j, batch, after, gated=False, noise=None):
         """Copy batch (and, captured with host_noise, its perturbation) into static set j and march
         it on the side stream once `after` (an event on the main stream) has passed: set j's buffers
-        were last read two steps back.  gated: the march graph first waits for the step graph's
-        gate signal (placement only)."""
+        were last read two steps back.  gated: the march graph first waits (a polling wave, at most
+        GATE_TIMEOUT_US) for the step graph's gate signal (placement only)."""
         self._side.wait_event(after)
         with torch.cuda.stream(self._side):
             if batch is not None:
@@ -993,14 +905,7 @@ class TrainStep:
                 if noise is None:
                     raise ValueError("captured with host_noise: pass noise= / next_noise= to replay()")
                 self._static_noise[j].copy_(noise)
-            if gated and self._gate_stream:
-                # the queue itself holds until the step graph just enqueued has signalled (its
-                # composite's last workgroup): no polling wave beside the chain
-                self._gate_target += 1
-                call("mfnerf_gate_wait_stream", ptr(self._gate), self._gate_target, self._side.cuda_stream)
-                self.graphs["march"][j].replay()
-            else:
-                self.graphs["march_gated" if gated else "march"][j].replay()
+            self.graphs["march_gated" if gated else "march"][j].replay()
             self._ev_march[j].record(self._side)
 
     def replay(self, batch: Batch = None, exchange=None, grid_bw_events=None, next_batch=None, prefetch=None,
@@ -1029,8 +934,7 @@ class TrainStep:
         self._ev_start.record(main)
         if not self._primed:
             self._march_on_side(j, batch, self._ev_start, noise=noise)
-        one_graph = (P == 1 and grid_bw_events is None and prefetch and not self.march_early
-                     and g.get("march_gated") is not None)
+        one_graph = P == 1 and grid_bw_events is None and prefetch and g.get("march_gated") is not None
         if one_graph and (dp_mode or g.get("step") is not None):
             # set 1-j was last read by the previous step, all of which precedes _ev_start
             main.wait_event(self._ev_march[j])
@@ -1062,9 +966,6 @@ class TrainStep:
             return
         fuse_tail = g.get("finish_update") is not None and not dp_mode
         self._flush_pack()
-        early = prefetch and self.march_early
-        if early:  # set 1-j was last read by the previous step, all of which precedes _ev_start
-            self._march_on_side(1 - j, next_batch, self._ev_start, noise=next_noise)
         main.wait_event(self._ev_march[j])
         self._use(self.mbuf[j])
         self.last_batch = self._static[j]
@@ -1075,7 +976,7 @@ class TrainStep:
             with torch.cuda.stream(sq):
                 g["chain"][j][q].replay()
                 self._ev_chain[q].record(sq)
-                if q == P - 1 and prefetch and not early:
+                if q == P - 1 and prefetch:
                     # set 1-j was last read by the previous step, which this chain follows; waiting
                     # for the last chain puts the march under the grid_bw scatters, not the chains
                     self._march_on_side(1 - j, next_batch, self._ev_chain[q], noise=next_noise)
@@ -1140,10 +1041,10 @@ class TrainStep:
         host synchronisation.  Without erosion (count_grid) the launches are captured once per
         (warmup, decay, seed) and replayed as one HIP graph (the draws' call index lives on the
         device, so every replay draws new cells): 0.45 ms of mostly launch overhead eagerly
-        (DESIGN.md 6).  MFNERF_OCC_GRAPH=0: always eager."""
+        (DESIGN.md 6)."""
         o = self._occ_buffers()
         self._flush_pack()  # the density query runs the field on `packed`
-        if count_grid is not None or os.environ.get("MFNERF_OCC_GRAPH", "1") != "1":
+        if count_grid is not None:
             self._occ_launches(warmup, decay, count_grid, seed)
             return
         key = (bool(warmup), float(decay), int(seed))
