@@ -16,6 +16,13 @@
 
 using namespace mfn;
 
+// MFN_PROBE (timing probe builds only, tools/build_variant.sh EXTRA=-DMFN_PROBE=k; results invalid):
+// bit 0 accumulate without its adds, bit 1 without its record DMA, bit 2 scatter without its record
+// stores, bit 3 scatter without its counting atomics (every rank 0)
+#ifndef MFN_PROBE
+#define MFN_PROBE 0
+#endif
+
 __global__ void mfn_bump_step_kernel(int32_t* s, mfnerf_amp_state* amp, float* zero, int nz);  // adam.hip
 
 namespace {
@@ -1202,7 +1209,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
             // the record's |a|, |b| maxima as two packed u16 (fp16 bits order like the values)
             auto rank = [&](int k, int lb, uint2 r) {
                 R[k].r = r;
-                R[k].meta = (uint32_t)lb | ((uint32_t)atomicAdd(&hist2[cp][lb], 1) << 16);
+                R[k].meta = (uint32_t)lb | ((MFN_PROBE & 8) ? 0u : ((uint32_t)atomicAdd(&hist2[cp][lb], 1) << 16));
                 rmax2 = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(
                     __builtin_bit_cast(ushort2v, rmax2), __builtin_bit_cast(ushort2v, r.y & 0x7fff7fffu)));
             };
@@ -1283,11 +1290,12 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
             const int lb = sbin[k];
             const int2 g = gd[lb];
             const uint2 r = stage[k];
-            if (k < g.y) {  // inside the unit's slot of the bin
-                uint2* dst = rec + (uint32_t)(g.x + k);
-                // nontemporal: streamed once here, read once by the accumulate
-                __builtin_nontemporal_store((unsigned long long)r.x | ((unsigned long long)r.y << 32),
-                                            reinterpret_cast<unsigned long long*>(dst));
+            if (MFN_PROBE & 4) {
+                if (r.x == 0xFFFFFFFFu) rec[0] = r;  // (keeps the stage reads)
+            } else if (k < g.y) {  // inside the unit's slot of the bin
+                // a plain store (round 5, r5c: the nontemporal store this was made the scatter 92 instead of
+                // 82.5 us and the step 3 us slower; the accumulate reads them the same either way)
+                rec[(uint32_t)(g.x + k)] = r;
             } else {
                 overflow_add(P, ovw, b0 + lb, r);  // a full slot: into the overflow words
             }
@@ -1495,7 +1503,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     bool full = false;  // a slot of this partition overflowed (its extra records: overflow_add)
     if (tid < UNITS) {
         const int c0 = cnt[tid];
-        c = min(c0, (int32_t)slot);
+        c = min(c0, (int32_t)slot);  // (slot is even: a 16-record multiple)
         full = c0 > slot;
         term = (float)c * __uint_as_float(smax[tid]);
     }
@@ -1514,9 +1522,11 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         }
     }
     for (int i = tid; i < n_ent; i += ACC_THREADS) img[i] = 0;
-    // (2) exclusive prefix of the counts (waves 0-3 hold them), and the partition's bound (sum over
-    // units of count x max, summed in a fixed order) -> its unit 2^-k
-    int x = c;
+    // (2) exclusive prefix of the counts rounded up to even (waves 0-3 hold them): every slot's run
+    // starts on a 16-B record pair in the stage; and the partition's bound (sum over units of count x
+    // max, summed in a fixed order) -> its unit 2^-k
+    const int c2 = (c + 1) & ~1;
+    int x = c2;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const int y = __shfl_up(x, off, 64);
@@ -1535,7 +1545,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
             before += k < wv ? s : 0;
             total += s;
         }
-        if (tid < UNITS) S.a.pre[tid] = before + x - c;
+        if (tid < UNITS) S.a.pre[tid] = before + x - c2;
         if (tid == 0) S.a.pre[UNITS] = total;
     }
     float bound = 0.0f;
@@ -1556,22 +1566,30 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     // lane j < 32 of wave wv: the run bounds of slot wv + NW j (read by the wave one slot at a time)
     const int my_u = wv + NW * (lane & 31);
     const int my_lo = my_u < UNITS ? S.a.pre[my_u] : T, my_hi = my_u < UNITS ? S.a.pre[my_u + 1] : T;
+    static_assert(ACC_RB % 2 == 0, "chunks of whole record pairs");
     for (int c0 = 0; c0 < T; c0 += ACC_RB) {
         const int c1 = min(T, c0 + ACC_RB);
         if (c0 > 0) __syncthreads();  // the previous chunk's adds are done with the stage
-        // (3) wave wv copies the part of its slots' runs inside [c0, c1), 32 records per instruction
+        // (3) wave wv copies the part of its slots' runs inside [c0, c1): 16 B (a record pair) per lane,
+        // 128 records per instruction (4-B lanes measured TA-bound: 48 us of the accumulate's 92)
         for (int j = 0; NW * j + wv < UNITS; ++j) {
             const int lo = max(__builtin_amdgcn_readlane(my_lo, j), c0);
             const int hi = min(__builtin_amdgcn_readlane(my_hi, j), c1);
             const int r0 = __builtin_amdgcn_readlane(my_lo, j);  // the slot's first record's place
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(base + (uint32_t)(NW * j + wv) * (uint32_t)slot);
-            for (int q = lo; q < hi; q += 32) {
-                const int k = q + (lane >> 1);  // record k of the compacted partition, dword lane & 1
-                if (k < hi)
-                    __builtin_amdgcn_global_load_lds(src + 2 * (k - r0) + (lane & 1), &S.a.recs[q - c0], 4, 0, 0);
+            const uint4* src = reinterpret_cast<const uint4*>(base + (uint32_t)(NW * j + wv) * (uint32_t)slot);
+            for (int q = lo; q < hi; q += 128) {
+                const int k = q + 2 * lane;  // records k, k + 1 of the compacted partition (k even)
+                if (!(MFN_PROBE & 2) && k < hi)
+                    __builtin_amdgcn_global_load_lds(src + ((k - r0) >> 1), &S.a.recs[q - c0], 16, 0, 0);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // an odd slot's pad record (the slot's next, stale record) becomes a zero record (no adds)
+        if (tid < UNITS && (c & 1)) {
+            const int k = S.a.pre[tid] + c;
+            if (k >= c0 && k < c1) S.a.recs[k - c0] = make_uint2(0u, 0u);
+        }
         __syncthreads();
         // (4) the adds, in a strided order over the stage
         const int len = c1 - c0;
@@ -1583,7 +1601,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
             for (int q = 0; q < UR; ++q) r[q] = S.a.recs[min(i0 + q * ACC_THREADS + perm, ACC_RB - 1)];
 #pragma unroll
             for (int q = 0; q < UR; ++q)
-                if (i0 + q * ACC_THREADS + perm < len) accum_record(img, mask, r[q], k2);
+                if (!(MFN_PROBE & 1) && i0 + q * ACC_THREADS + perm < len) accum_record(img, mask, r[q], k2);
         }
     }
     __syncthreads();
