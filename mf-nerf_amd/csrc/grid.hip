@@ -1442,7 +1442,10 @@ struct AdamRest {
 // ray's run of consecutive samples in one cell (same-address atomics).  A partition holding more
 // records than the stage is done in chunks of ACC_RB records.  Same records, same integer adds:
 // bit-identical sums.  LDS: 16 KB image + 62 KB stage -> two workgroups per CU.
-constexpr int ACC_RB = 7936;
+#ifndef MFN_ACC_RB
+#define MFN_ACC_RB 7936
+#endif
+constexpr int ACC_RB = MFN_ACC_RB;  // (A/B builds override: smaller stages, more workgroups per CU)
 struct AccumStage {
     unsigned long long img[MAX_BIN_ENTRIES];
     uint2 recs[ACC_RB];
@@ -1454,7 +1457,7 @@ union AccumShared {  // ONE __shared__ object (a second one beside an LDS-DMA st
     AccumStage a;
     TableRegions tr;
 };
-static_assert(sizeof(AccumShared) <= 81920, "two accumulate workgroups per CU");
+static_assert(sizeof(AccumShared) <= 81920, "at least two accumulate workgroups per CU");
 
 __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, int64_t n,
                                                                 const int32_t* __restrict__ n_dev,
