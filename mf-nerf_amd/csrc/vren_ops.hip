@@ -245,7 +245,8 @@ struct MarchChunk {
 };
 
 __device__ __forceinline__ MarchChunk march_chunk(const MarchParams& p, float t_base, float dt, float t2, float ox,
-                                                  float oy, float oz, float dx, float dy, float dz, int lane) {
+                                                  float oy, float oz, float dx, float dy, float dz, int lane,
+                                                  float inv_scale) {
     MarchChunk k;
     k.t_base = t_base;
     const float delta = (t_base + dt) - t_base;
@@ -263,7 +264,9 @@ __device__ __forceinline__ MarchChunk march_chunk(const MarchParams& p, float t_
     const uint32_t g3 = (uint32_t)p.grid_size * p.grid_size * p.grid_size;
     const int mip = max(mip_from_pos(k.x, k.y, k.z, p.cascades), mip_from_dt(dt, p.grid_size, p.cascades));
     k.c.mip_bound = fminf(scalbnf(1.0f, mip - 1), p.scale);
-    const float inv = 1 / k.c.mip_bound;
+    // lookup_cell's 1 / mip_bound without a per-lane IEEE division: 2^(1-mip) is exact, and 1/scale
+    // is the same correctly rounded quotient computed once (inv_scale)
+    const float inv = k.c.mip_bound == p.scale ? inv_scale : scalbnf(1.0f, 1 - mip);
     const float gs = (float)p.grid_size, gm1 = (float)p.grid_size - 1.0f;
     k.c.nx = (int)clampf(0.5f * fmaf(k.x, inv, 1.0f) * gs, 0.0f, gm1);
     k.c.ny = (int)clampf(0.5f * fmaf(k.y, inv, 1.0f) * gs, 0.0f, gm1);
@@ -295,10 +298,11 @@ __device__ __forceinline__ void march_wave_ray(const MarchParams& p, int64_t r, 
         // walk), so its bitfield bytes are requested before this chunk's walk -- one memory round trip
         // hidden per chunk (the march runs beside the table-gradient scatter, where every load waits
         // behind its traffic)
-        MarchChunk cur = march_chunk(p, t_base, dt, t2, ox, oy, oz, dx, dy, dz, lane);
+        const float inv_scale = 1 / p.scale;
+        MarchChunk cur = march_chunk(p, t_base, dt, t2, ox, oy, oz, dx, dy, dz, lane, inv_scale);
         while (!done) {
             if (!(t_base < t2) || n >= limit) break;  // every later visited point fails the loop test
-            const MarchChunk nxt = march_chunk(p, cur.next_base, dt, t2, ox, oy, oz, dx, dy, dz, lane);
+            const MarchChunk nxt = march_chunk(p, cur.next_base, dt, t2, ox, oy, oz, dx, dy, dz, lane, inv_scale);
             const float tl = cur.tl;
             const int chain_end = cur.chain_end;
             const bool live = cur.live;
@@ -319,16 +323,16 @@ __device__ __forceinline__ void march_wave_ray(const MarchParams& p, int64_t r, 
             constexpr int OUT = 64;
             int P = lane, L = -1;
             if (live && !occ) {
+                // first k in [0, chain_end) with tl_k >= tt (chain_end: none).  Inside the verified
+                // chain tl_k = t_base + k delta exactly, so k = ceil((tt - t_base) / delta); the
+                // estimate (approximate reciprocal: off by far less than a lane) is put right by one
+                // exact comparison each way
                 const float delta = (cur.t_base + dt) - cur.t_base;
-                int lo = 0, hi = chain_end;  // first k in [0, chain_end) with tl_k >= tt (chain_end: none)
-#pragma unroll
-                for (int it = 0; it < 7; ++it) {
-                    const int mid = (lo + hi) >> 1;
-                    const bool ge = lo < hi && fmaf((float)mid, delta, cur.t_base) >= tt;
-                    hi = lo < hi && ge ? mid : hi;
-                    lo = lo < hi && !ge ? mid + 1 : lo;
-                }
-                const int J = max(lo, lane + 1);
+                const float est = (tt - cur.t_base) * __builtin_amdgcn_rcpf(delta);
+                int k = tt == tt ? (int)ceilf(fminf(fmaxf(est, 0.0f), (float)chain_end)) : chain_end;
+                if (k > 0 && fmaf((float)(k - 1), delta, cur.t_base) >= tt) --k;
+                if (k < chain_end && !(fmaf((float)k, delta, cur.t_base) >= tt)) ++k;
+                const int J = max(k, lane + 1);
                 P = J < chain_end ? J : OUT;
                 L = J < chain_end ? -1 : lane;
             }
