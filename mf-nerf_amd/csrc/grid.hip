@@ -1574,7 +1574,10 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         const int c1 = min(T, c0 + ACC_RB);
         if (c0 > 0) __syncthreads();  // the previous chunk's adds are done with the stage
         // (3) wave wv copies the part of its slots' runs inside [c0, c1): 16 B (a record pair) per lane,
-        // 128 records per instruction (4-B lanes measured TA-bound: 48 us of the accumulate's 92)
+        // 128 records per instruction (4-B lanes measured TA-bound: 48 us of the accumulate's 92).
+        // (A gather -- instruction i of the chunk on wave i mod 8, each lane's pair found in its slot
+        // by a binary search of the prefix: ~4x fewer instructions, all lanes busy -- measured 96.5
+        // vs 94.3 us: the instruction count is not what bounds the copy, profiles/r05_v6_*.)
         for (int j = 0; NW * j + wv < UNITS; ++j) {
             const int lo = max(__builtin_amdgcn_readlane(my_lo, j), c0);
             const int hi = min(__builtin_amdgcn_readlane(my_hi, j), c1);
