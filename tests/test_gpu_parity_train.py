@@ -41,8 +41,13 @@ WHOLE_LOG_TOL, WHOLE_SE_K = 0.10, 2.5
 # compounding over the first steps; a systematic gradient error of a few percent shows here first.
 EARLY_STEPS, LOSS_TOL_EARLY = 100, 0.02
 # the first steps, where the two sides train the same model up to fp16 rounding: EVERY step's loss
-# within 1 +- this of the reference's (a gradient error of a few percent shows within a few steps)
-FIRST_STEPS, LOSS_TOL_FIRST = 20, 0.03
+# within 1 +- this of the reference's (a gradient error of a few percent shows within a few steps).
+# r05 (profiles/r05_parity_train.json, early_deviation_per_step): through step 70 every step of every
+# seed is within 0.27 % (0.13 % through step 20); from step ~75 the trajectories part, a few seeds at
+# a time (seed 0 at 75, seeds 3/4/7 after 80), as two chaotic runs do -- the 25 % single step (seed
+# 3, step 84, its neighbours +0.6 % / -0.8 %) is one of 256 rays predicted differently by two
+# already-parted models, not a bias (pooled early ratio 0.9999, whole-run log ratio +0.011 se 0.054)
+FIRST_STEPS, LOSS_TOL_FIRST = 60, 0.01
 # where the protocol's numbers are written (per-seed diffs, mean, sd, bound, loss ratios)
 OUT = os.environ.get("MFNERF_PARITY_OUT", os.path.join(ROOT, "gpurun_out", "parity_train.json"))
 
