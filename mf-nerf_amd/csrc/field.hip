@@ -10,7 +10,7 @@
 //   LDS round trip (cdna_hip_programming.md section 3, "An accumulator tile as the next MFMA's
 //   operand").  The weights are the A operands, pre-permuted once per optimizer step by
 //   mfnerf_field_pack_weights into 1-KiB lane-linear fragments (ds_read_b128, conflict-free).
-//   Backward: see the comment above field_bw_kernel.
+//   Backward: see the comments above field_bw_coop_kernel (W = 64) and field_bw_coop128_kernel.
 #include <cstdlib>
 
 #include "common.hpp"
@@ -28,12 +28,10 @@ namespace {
 
 constexpr int FIELD_BLOCK = 256;    // forward: 4 waves
 
-// Backward configuration (4 waves per workgroup, one workgroup per CU, one wave per SIMD):
-//   W = 64:  all 12 weight-gradient tiles accumulate in registers (192 of the 512 a lone wave per
-//            SIMD can hold);
-//   W = 128: dW1, dW2, dWr1, dWr3 (12 tiles) in registers as at W = 64; dWr2's 16 tiles do not fit
-//            beside them, so a second pass (field_bw_wr2_kernel: forward + dR2 only, 256 accumulator
-//            registers) computes dWr2.
+// Backward: 4 waves per workgroup, each the forward + data-gradient chain of its own 32-sample tile,
+// the weight-gradient tiles split over the waves (field_bw_coop_kernel, field_bw_coop128_kernel).
+// Rounds 1-4 held every tile in each wave (one wave per SIMD; at W = 128 a second pass recomputed the
+// forward for dWr2's 16 tiles: 0.46 vs 0.23 ms on the mf128 step, profiles/r05_v8_*).
 // Measured and not kept (rounds 1-2): every tile in an LDS image with two waves per SIMD (ds_add_f32
 // per sample tile; W = 128: 836 vs 171 us), dWr2 by LDS atomics beside the register tiles (3.4 ms
 // per 983k samples), Wr2^T read from global memory, two sample tiles per loop trip (~560 registers:
@@ -72,21 +70,6 @@ __device__ __forceinline__ u32x2 tr_read(const _Float16* p) {
 
 struct SOp;
 __device__ __forceinline__ SOp s_get(const _Float16* slot, int lane);
-
-template <int W, int NW>
-struct BwCfg {
-    using G = Geo<W>;
-    static_assert(NW == 4, "one wave per SIMD");
-    static constexpr bool R2_SPLIT = (W == 128);          // dWr2 by field_bw_wr2_kernel
-    static constexpr int LDS_FRAGS = G::N;
-    static constexpr size_t IMG_OFF = (size_t)LDS_FRAGS * FRAG_HALFS * 2;
-    // per wave: SLOTS transpose images of one 32x32 f16 tile (t_put / s_get), after the fragments
-    static constexpr int SLOTS_FIT = (int)((160 * 1024 - IMG_OFF) / ((size_t)NW * TILE_BYTES));
-    static constexpr int SLOTS = SLOTS_FIT < 12 ? SLOTS_FIT : 12;
-    static constexpr size_t SLOT_OFF = IMG_OFF;
-    static constexpr size_t LDS = SLOT_OFF + (size_t)NW * SLOTS * TILE_BYTES;
-    static_assert(SLOTS >= 2 && LDS <= 160 * 1024, "the backward's LDS must fit one CU");
-};
 
 // tcnn SphericalHarmonics degree 4 as a module of its own (the tinycudann route's dir_encoder,
 // networks.py:60-67): in = (d/|d| + 1)/2 (n, 3) f32 -> (n, 16) f16, the IEEE operations and their
@@ -414,12 +397,6 @@ __device__ __forceinline__ void load_frags_bw(_Float16* lds, const _Float16* __r
     __syncthreads();
 }
 
-// a backward fragment (index in the packed blob), from LDS
-template <int W, int NW>
-__device__ __forceinline__ half8 bw_frag(const _Float16* lds, const _Float16* __restrict__ packed, int f, int lane) {
-    return lds_frag(lds, f, lane);
-}
-
 // S operands (K = samples 0..15 / 16..31 of the tile) of one 32-channel tile given as two T chunks
 struct SOp { half8 k[2]; };
 
@@ -486,410 +463,8 @@ __device__ __forceinline__ void dw_add32(float* img, const f32x16& a, int ot, in
 // one dW tile += dY x X into its register accumulator
 __device__ __forceinline__ void acc_tile(f32x16& reg, const SOp& dy, const SOp& x) { dw_acc_agpr(reg, dy, x); }
 
-// Transpose-slot plans of field_bw (slot ids < N_SLOTS; every slot is read before it is written
-// again in program order).  W = 64, 12 slots: the forward's operands are written right after the
-// forward, so their LDS traffic overlaps the backward chain.  W = 128, 6 slots (the fragments take
-// 106 KB): every operand is written just before its products.
-template <int W>
-struct TPlan;
-template <>
-struct TPlan<64> {
-    static constexpr bool EARLY = true;
-    static constexpr int N_SLOTS = 12, SHH = 4, X = 7, DO = 8, DH = 1;
-    static constexpr int r2(int t) { return t; }
-    static constexpr int r1(int t) { return 2 + t; }
-    static constexpr int y1(int t) { return 5 + t; }
-    static constexpr int dr2(int t) { return 9 + t; }
-    static constexpr int dr1(int t) { return t ? 0 : 11; }
-    static constexpr int dy1(int t) { return 2 + t; }
-};
-template <>
-struct TPlan<128> {
-    static constexpr bool EARLY = false;
-    static constexpr int N_SLOTS = 6, SHH = 5, X = 5, DO = 0, DH = 4;
-    static constexpr int r2(int t) { return 1 + t; }
-    static constexpr int r1(int) { return 0; }   // (dWr2: field_bw_wr2_kernel)
-    static constexpr int dr2(int) { return 0; }
-    static constexpr int y1(int t) { return 2 + t; }
-    static constexpr int dr1(int t) { return t; }
-    static constexpr int dy1(int t) { return t; }
-};
-
-template <int W, int NW, bool PLANAR>
-__global__ __launch_bounds__(64 * NW) void field_bw_kernel(
-    const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n,
-    const int32_t* __restrict__ n_dev, const _Float16* __restrict__ packed, const float* __restrict__ dL_dsigma,
-    const float* __restrict__ dL_drgb, float grad_scale, const float* __restrict__ scale_dev,
-    float* __restrict__ dL_dfeat, float* __restrict__ slab, int32_t* __restrict__ nonfinite, float* __restrict__ level_l1) {
-    using G = Geo<W>;
-    using C = BwCfg<W, NW>;
-    constexpr int MT = G::MT;
-    constexpr int oR1 = N_XYZ_PARAMS, oR2 = oR1 + W * 32, oR3 = oR2 + W * W;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    _Float16* lds_base = reinterpret_cast<_Float16*>(smem);
-    load_frags_bw<W, NW>(lds_base, packed);
-    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform)
-    const int r = lane & 31, h = lane >> 5;
-    const float S = scale_dev ? *scale_dev : grad_scale, invS = 1.0f / S;  // the (dynamic) loss scale
-    const f32x16 z = {};
-    // register accumulators, 32x32 tiles [out-tile][in-tile] (192 registers at W = 64, NW = 4)
-    constexpr int R2 = C::R2_SPLIT ? 1 : MT;
-    f32x16 dw1[2], dw2[2], dwr1[MT], dwr3[MT], dwr2[R2][R2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a) { dw1[a] = z; dw2[a] = z; }
-#pragma unroll
-    for (int a = 0; a < MT; ++a) { dwr1[a] = z; dwr3[a] = z; }
-#pragma unroll
-    for (int a = 0; a < R2; ++a)
-#pragma unroll
-        for (int b = 0; b < R2; ++b) dwr2[a][b] = z;
-
-    const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
-    const int64_t tiles = div_up<int64_t>(nn, 32);
-    const int64_t stride = (int64_t)gridDim.x * NW;
-    // P sample tiles per loop trip (tile, tile + stride, ...), computed in one basic block so the
-    // scheduler overlaps one tile's MFMA chain with the other's VALU packing and LDS waits (one wave
-    // per SIMD hides no latency otherwise).  Each accumulator still takes the tiles in the order
-    // tile, tile + stride, ...: the sums are the same as with one tile per trip, bit for bit.
-    constexpr int P = 1;
-    // the next trip's inputs are loaded while this trip computes
-    struct BwIn { TileIn I; float gs, g0, g1, g2; bool live; };
-    BwIn nx[P];
-    // Branch-free: every lane loads (a sample index clamped into [0, nn)) and only the incoming
-    // gradients are zeroed where the sample is out of range or on the lanes h == 1.  An out-of-range
-    // lane then carries finite activations with a zero data gradient, so its dW products are zero
-    // (a NaN there would poison the K = samples sums), and the loop has one path: the compiler's
-    // vmcnt bookkeeping does not merge paths into a vmcnt(0) that waits for the dL/dfeat stores.
-    auto fetch = [&](int64_t tile, BwIn& o) {
-        const int64_t s = tile * 32 + r;
-        const bool v = s < nn && h == 0;
-        const int64_t sc = min<int64_t>(s, nn - 1);
-        if constexpr (PLANAR) {
-            // x[0] element j = feature 8h+j = level 4h + j/2; x[1]: level 8 + 4h + j/2
-            const uint32_t* Pp = reinterpret_cast<const uint32_t*>(feat);
-            uint32_t u[8];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                u[k] = Pp[(int64_t)(4 * h + k) * plane_stride + sc];
-                u[4 + k] = Pp[(int64_t)(8 + 4 * h + k) * plane_stride + sc];
-            }
-            o.I.x[0] = *reinterpret_cast<const half8*>(&u[0]);
-            o.I.x[1] = *reinterpret_cast<const half8*>(&u[4]);
-        } else {
-            const half8* row = reinterpret_cast<const half8*>(feat + sc * 32);
-            o.I.x[0] = row[h];
-            o.I.x[1] = row[2 + h];
-        }
-        o.I.d[0] = dirs[3 * sc]; o.I.d[1] = dirs[3 * sc + 1]; o.I.d[2] = dirs[3 * sc + 2];
-        // raw: the select waits for the load, so it happens where the values are used (zero_grads)
-        o.gs = dL_dsigma[sc]; o.g0 = dL_drgb[3 * sc]; o.g1 = dL_drgb[3 * sc + 1]; o.g2 = dL_drgb[3 * sc + 2];
-        o.live = v;
-    };
-    auto zero_grads = [&](BwIn& o) {
-        o.gs = o.live ? o.gs : 0.0f;
-        o.g0 = o.live ? o.g0 : 0.0f;
-        o.g1 = o.live ? o.g1 : 0.0f;
-        o.g2 = o.live ? o.g2 : 0.0f;
-    };
-    const int64_t tile0 = (int64_t)blockIdx.x * NW + wid;
-    if (tile0 < tiles) {
-#pragma unroll
-        for (int q = 0; q < P; ++q) fetch(tile0 + q * stride, nx[q]);
-    }
-    bool bad = false;  // a non-finite dL/dfeat on this lane, reported once after the loop
-    // per-level L1 of dL/dfeat (the fixed-point table-gradient scales): this lane's 8 levels are
-    // 4g + 2h (features 8g+4h, +1) and 4g + 2h + 1 (features 8g+4h+2, +3), g = 0..3
-    float l1a[4] = {0.f, 0.f, 0.f, 0.f}, l1b[4] = {0.f, 0.f, 0.f, 0.f};
-    // one trip: the P tiles' forward + backward stage by stage (see forward_tiles); dW into the
-    // accumulators (tile 0's contribution before tile 1's), dX^T (scaled by S) into dx[]
-    _Float16* tsl = nullptr;  // this wave's transpose slots (set per trip from the opaque base)
-    auto trip_bw = [&](const _Float16* lds, const _Float16* pk, const BwIn* in, const bool* valid, f32x16* dx) {
-        FwdTile<W> T[P];
-        {
-            TileIn I[P];
-#pragma unroll
-            for (int q = 0; q < P; ++q) I[q] = in[q].I;
-            forward_tiles<W, false, P>(lds, lane, I, valid, T);
-        }
-        // -- rgb layer 3: dO (rows 0..2 on lanes h==0) = dL/drgb * sigmoid' (the grads are 0 on
-        //    lanes h == 1: no branch)
-        half8 dOb[P];
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-            f32x16 dO = z;
-            dO[0] = in[q].g0 * S * T[q].rgb[0] * (1.0f - T[q].rgb[0]);
-            dO[1] = in[q].g1 * S * T[q].rgb[1] * (1.0f - T[q].rgb[1]);
-            dO[2] = in[q].g2 * S * T[q].rgb[2] * (1.0f - T[q].rgb[2]);
-            dOb[q] = pack8<0, false>(dO);
-        }
-        // this wave's transpose images (TPlan: compile-time slots, each read before it is rewritten;
-        // one wave's LDS accesses complete in program order)
-        using TP = TPlan<W>;
-        static_assert(P == 1 && TP::N_SLOTS <= C::SLOTS, "one transpose set per trip");
-        auto slot = [&](int k) { return tsl + k * TILE_HALFS; };
-        auto put2 = [&](int k, const half8* v) {  // a 32-channel tile given as two perm chunks
-            t_put(slot(k), lane, v[0], 0, true);
-            t_put(slot(k), lane, v[1], 4, true);
-        };
-        auto put_fw = [&](bool early) {  // the forward's operands
-            if (early != TP::EARLY) return;
-#pragma unroll
-            for (int t = 0; t < MT; ++t) put2(TP::r2(t), T[0].r2[t]);
-            if constexpr (!C::R2_SPLIT) {
-#pragma unroll
-                for (int t = 0; t < MT; ++t) put2(TP::r1(t), T[0].r1[t]);
-            }
-        };
-        put_fw(true);
-        if constexpr (TP::EARLY) {
-            t_put(slot(TP::SHH), lane, T[0].sh, 0, false);
-            t_put(slot(TP::SHH), lane, T[0].hb, 4, true);
-#pragma unroll
-            for (int t = 0; t < 2; ++t) put2(TP::y1(t), T[0].y1[t]);
-            t_put(slot(TP::X), lane, T[0].x[0], 0, false);
-            t_put(slot(TP::X), lane, T[0].x[1], 4, false);
-        }
-        //    dR2 = Wr3^T dO, masked by R2 > 0 (the data-gradient chain first, the dW products after)
-        half8 dr2p[P][MT][2];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-            const half8 f = bw_frag<W, NW>(lds, pk, G::B5 + mt, lane);
-            f32x16 a[P];
-#pragma unroll
-            for (int q = 0; q < P; ++q) a[q] = mfma(f, dOb[q], z);
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                dr2p[q][mt][0] = relu_mask8(pack8<0, false>(a[q]), T[q].r2[mt][0]);
-                dr2p[q][mt][1] = relu_mask8(pack8<8, false>(a[q]), T[q].r2[mt][1]);
-            }
-        }
-        if constexpr (!C::R2_SPLIT) {
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) put2(TP::dr2(mt), dr2p[0][mt]);
-        }
-        // dWr3 (16 x W, rows 0..2 non-zero) += dO^T R2 (channels 16..31 of the dO image are stale:
-        // they only reach rows 16..31 of the dWr3 tiles, which the epilogue drops)
-        t_put(slot(TP::DO), lane, dOb[0], 0, true);
-        put_fw(false);
-        {
-            const SOp d = s_get(slot(TP::DO), lane);
-#pragma unroll
-            for (int t = 0; t < MT; ++t) acc_tile(dwr3[t], d, s_get(slot(TP::r2(t)), lane));
-        }
-        //    dR1 = Wr2^T dR2, masked by R1 > 0
-        half8 dr1p[P][MT][2];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-            f32x16 a[P];
-#pragma unroll
-            for (int q = 0; q < P; ++q) a[q] = z;
-#pragma unroll
-            for (int t = 0; t < MT; ++t)
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const half8 f = bw_frag<W, NW>(lds, pk, G::B4 + mt * G::KC + t * 2 + k, lane);
-#pragma unroll
-                    for (int q = 0; q < P; ++q) a[q] = mfma(f, dr2p[q][t][k], a[q]);
-                }
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                dr1p[q][mt][0] = relu_mask8(pack8<0, false>(a[q]), T[q].r1[mt][0]);
-                dr1p[q][mt][1] = relu_mask8(pack8<8, false>(a[q]), T[q].r1[mt][1]);
-            }
-        }
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) put2(TP::dr1(mt), dr1p[0][mt]);
-        if constexpr (!C::R2_SPLIT) {   // -- rgb layer 2: dWr2 (WxW) += dR2^T R1
-            SOp x[MT];
-#pragma unroll
-            for (int i = 0; i < MT; ++i) x[i] = s_get(slot(TP::r1(i)), lane);
-#pragma unroll
-            for (int o = 0; o < MT; ++o) {
-                const SOp d = s_get(slot(TP::dr2(o)), lane);
-#pragma unroll
-                for (int i = 0; i < MT; ++i) acc_tile(dwr2[o][i], d, x[i]);
-            }
-        }
-        //    d[SH;h] = Wr1^T dR1 (rows 16..31 = dh) + TruncExp backward into h[0]
-        half8 dhb[P];
-        {
-            f32x16 dsh[P];
-#pragma unroll
-            for (int q = 0; q < P; ++q) dsh[q] = z;
-#pragma unroll
-            for (int t = 0; t < MT; ++t)
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const half8 f = bw_frag<W, NW>(lds, pk, G::B3 + t * 2 + k, lane);
-#pragma unroll
-                    for (int q = 0; q < P; ++q) dsh[q] = mfma(f, dr1p[q][t][k], dsh[q]);
-                }
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                // row 16 = reg 8 on lanes h==0: g * exp(clamp(h0,-15,15)) (custom_functions.py:170-173)
-                const float dh0 = in[q].gs * S * __expf(fminf(fmaxf(T[q].h0, -15.0f), 15.0f));
-                dsh[q][8] = h == 0 ? dsh[q][8] + dh0 : dsh[q][8];
-                dhb[q] = pack8<8, false>(dsh[q]);
-            }
-        }
-        t_put(slot(TP::DH), lane, dhb[0], 0, true);
-        // -- rgb layer 1: dWr1 (Wx32) += dR1^T [SH;h]   (SH natural order, h perm order)
-        if constexpr (!TP::EARLY) {
-            t_put(slot(TP::SHH), lane, T[0].sh, 0, false);
-            t_put(slot(TP::SHH), lane, T[0].hb, 4, true);
-        }
-        {
-            const SOp x = s_get(slot(TP::SHH), lane);
-#pragma unroll
-            for (int o = 0; o < MT; ++o) acc_tile(dwr1[o], s_get(slot(TP::dr1(o)), lane), x);
-        }
-        //    dY1 = W2^T dh, masked by Y1 > 0
-        half8 dy1p[P][2][2];
-        {
-            const half8 f0 = bw_frag<W, NW>(lds, pk, G::B2 + 0, lane), f1 = bw_frag<W, NW>(lds, pk, G::B2 + 1, lane);
-            f32x16 a0[P], a1[P];
-#pragma unroll
-            for (int q = 0; q < P; ++q) { a0[q] = mfma(f0, dhb[q], z); a1[q] = mfma(f1, dhb[q], z); }
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                dy1p[q][0][0] = relu_mask8(pack8<0, false>(a0[q]), T[q].y1[0][0]);
-                dy1p[q][0][1] = relu_mask8(pack8<8, false>(a0[q]), T[q].y1[0][1]);
-                dy1p[q][1][0] = relu_mask8(pack8<0, false>(a1[q]), T[q].y1[1][0]);
-                dy1p[q][1][1] = relu_mask8(pack8<8, false>(a1[q]), T[q].y1[1][1]);
-            }
-#pragma unroll
-            for (int t = 0; t < 2; ++t) put2(TP::dy1(t), dy1p[0][t]);
-        }
-        //    dX = W1^T dY1
-        {
-            half8 f[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) f[i] = bw_frag<W, NW>(lds, pk, G::B1 + i, lane);
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                dx[q] = z;
-#pragma unroll
-                for (int t = 0; t < 2; ++t)
-#pragma unroll
-                    for (int k = 0; k < 2; ++k) dx[q] = mfma(f[t * 2 + k], dy1p[q][t][k], dx[q]);
-            }
-        }
-        // -- xyz layer 2: dW2 (16x64) += dh^T Y1 (dh: channels 16..31 of its image stale, rows dropped)
-        if constexpr (!TP::EARLY) {
-#pragma unroll
-            for (int t = 0; t < 2; ++t) put2(TP::y1(t), T[0].y1[t]);
-        }
-        {
-            const SOp d = s_get(slot(TP::DH), lane);
-#pragma unroll
-            for (int t = 0; t < 2; ++t) acc_tile(dw2[t], d, s_get(slot(TP::y1(t)), lane));
-        }
-        // -- xyz layer 1: dW1 (64x32) += dY1^T X   (X natural order)
-        if constexpr (!TP::EARLY) {
-            t_put(slot(TP::X), lane, T[0].x[0], 0, false);
-            t_put(slot(TP::X), lane, T[0].x[1], 4, false);
-        }
-        {
-            const SOp x = s_get(slot(TP::X), lane);
-#pragma unroll
-            for (int o = 0; o < 2; ++o) acc_tile(dw1[o], s_get(slot(TP::dy1(o)), lane), x);
-        }
-    };
-    for (int64_t tile = tile0; tile < tiles; tile += P * stride) {
-        // the fragment reads are loop-invariant; an opaque base keeps the compiler from hoisting
-        // all of them (4 registers each) out of the loop
-        int opaque = 0;
-        asm volatile("" : "+s"(opaque));
-        const _Float16* lds = lds_base + opaque;
-        const _Float16* pk = packed + opaque;  // B4 from global memory (W = 128): not hoisted either
-        tsl = lds_base + opaque + C::SLOT_OFF / 2 + wid * (C::SLOTS * TILE_HALFS);
-        BwIn in[P];
-#pragma unroll
-        for (int q = 0; q < P; ++q) { in[q] = nx[q]; zero_grads(in[q]); }
-#pragma unroll
-        for (int q = 0; q < P; ++q) fetch(tile + (P + q) * stride, nx[q]);  // (clamped past the end)
-        f32x16 dx[P];
-        bool valid[P];
-#pragma unroll
-        for (int q = 0; q < P; ++q) valid[q] = (tile + q * stride) * 32 + r < nn;
-        trip_bw(lds, pk, in, valid, dx);
-        //    dX = W1^T dY1 -> global fp32 (features (i&3)+8(i>>2)+4h)
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-            const int64_t s = (tile + q * stride) * 32 + r;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float4 o = make_float4(dx[q][4 * g] * invS, dx[q][4 * g + 1] * invS,
-                                             dx[q][4 * g + 2] * invS, dx[q][4 * g + 3] * invS);
-                bad |= !(isfinite(o.x) && isfinite(o.y) && isfinite(o.z) && isfinite(o.w));
-                if (s < nn) reinterpret_cast<float4*>(dL_dfeat + s * 32)[2 * g + h] = o;
-                // (an out-of-range lane's dX is exactly zero: its data gradient is)
-                l1a[g] += fabsf(o.x) + fabsf(o.y);
-                l1b[g] += fabsf(o.z) + fabsf(o.w);
-            }
-        }
-    }
-    // the table gradient is sum(weight * dL/dfeat): non-finite only if some dL/dfeat is
-    if (nonfinite && __any(bad) && lane == 0) atomicOr(nonfinite, 1);
-
-    // ---- epilogue: the workgroup's dW (and the level L1 partials) -> one slab row
-    float* row = slab + (int64_t)blockIdx.x * G::N_DW;
-    {
-        // register partials -> an fp32 image over the fragment area
-        constexpr int N_IMG = G::N_DW;
-        static_assert((size_t)N_IMG * 4 + 64 <= C::IMG_OFF, "reduction image must fit the fragment area");
-        xdl_drain();
-        __syncthreads();
-        float* img = reinterpret_cast<float*>(smem);  // wave 0 stores every entry first (no zeroing)
-        float* l1_part = img + N_IMG;  // 16 floats after the image
-        if (threadIdx.x < 16) l1_part[threadIdx.x] = 0.0f;
-        __syncthreads();
-        if (level_l1) {
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                float a = l1a[g], b = l1b[g];
-#pragma unroll
-                for (int off = 16; off > 0; off >>= 1) { a += __shfl_xor(a, off, 64); b += __shfl_xor(b, off, 64); }
-                if (r == 0) { atomicAdd(l1_part + 4 * g + 2 * h, a); atomicAdd(l1_part + 4 * g + 2 * h + 1, b); }
-            }
-        }
-        // the waves add their tiles one after another (each address gets one add per wave), so the
-        // block's sum -- hence the weight gradient -- has a fixed order: bit-reproducible
-        for (int wv = 0; wv < NW; ++wv) {
-            if ((int)(threadIdx.x >> 6) == wv) {
-                const bool st = wv == 0;
-#pragma unroll
-                for (int a = 0; a < 2; ++a) {
-                    dw_add32(img, dw1[a], a, 0, 64, 32, lane, st);
-                    dw_add32(img + 64 * 32, dw2[a], 0, a, 16, 64, lane, st);
-                }
-#pragma unroll
-                for (int a = 0; a < MT; ++a) {
-                    dw_add32(img + oR1, dwr1[a], a, 0, W, 32, lane, st);
-                    dw_add32(img + oR3, dwr3[a], 0, a, 16, W, lane, st);
-                }
-#pragma unroll
-                for (int o = 0; o < R2; ++o)
-#pragma unroll
-                    for (int i = 0; i < R2; ++i)
-                        if constexpr (!C::R2_SPLIT) dw_add32(img + oR2, dwr2[o][i], o, i, W, W, lane, st);
-            }
-            __syncthreads();
-        }
-        bool rbad = false;  // a non-finite weight-gradient partial (see slab_row_flag)
-        for (int i = threadIdx.x; i < G::N_DW; i += blockDim.x) {
-            if (C::R2_SPLIT && i >= oR2 && i < oR3) continue;  // written by field_bw_wr2_kernel
-            const float val = img[i] * invS;
-            row[i] = val;
-            rbad |= !isfinite(val);
-        }
-        slab_row_flag(nonfinite, rbad);
-        if (level_l1 && threadIdx.x < 16) atomicAdd(level_l1 + threadIdx.x, l1_part[threadIdx.x]);
-    }
-}
-
 // ---------------------------------------------------------------- cooperative backward (W = 64)
-// field_bw_kernel holds all 12 weight-gradient tiles in each wave (192 accumulator registers + ~170
+// The round 1-3 per-wave backward held all 12 weight-gradient tiles in each wave (192 accumulator registers + ~170
 // for the chain): one wave per SIMD, nothing hides the chain's dependencies (PMC: waiting 56 % of
 // its cycles).  Here the 12 tiles are split over the workgroup's 4 waves -- 3 each, 48 accumulator
 // registers -- so a wave fits 256 registers and TWO workgroups share a CU (76 KB of LDS each: the
@@ -931,7 +506,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
     const int64_t groups = div_up<int64_t>(tiles, 4);  // group g = tiles 4g .. 4g+3, one per wave
     struct BwIn { TileIn I; float gs, g0, g1, g2; bool live; };
     BwIn nx;
-    // as field_bw_kernel: every lane loads (index clamped), the incoming gradients are zeroed where
+    // branch-free: every lane loads (index clamped), the incoming gradients are zeroed where
     // the sample is out of range or on lanes h == 1 -- an idle wave's tile contributes exact zeros
     auto fetch = [&](int64_t tile, BwIn& o) {
         const int64_t s = tile * 32 + r;
@@ -1156,119 +731,270 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
     }
 }
 
-// Second backward pass at W = 128: dWr2 (W x W) = sum over samples of dR2^T R1, with all 16 tiles in
-// registers.  Recomputes the forward and dR2 = relu'(R2) * Wr3^T dO (what field_bw_kernel does before
-// it), and writes the dWr2 segment of the same slab rows.
-constexpr int WR2_SLOTS = 8;  // (W = 128: R1's 4 tiles + dR2's 4)
-template <int W>
-constexpr size_t WR2_LDS() { return (size_t)Geo<W>::B4 * FRAG_HALFS * 2 + 4 * WR2_SLOTS * TILE_BYTES; }
+// ---------------------------------------------------------------- cooperative backward (W = 128)
+// Round 5: the width-128 field (configs 3/4, MF-NeRF's benchmark field) in ONE pass, the W = 64
+// cooperative scheme scaled up.  The per-wave backward (removed) held all weight-gradient tiles but dWr2's
+// 16 (one wave per SIMD, 448 accumulator registers do not fit), and a second pass recomputed the
+// forward and dR2 for them: 0.46 ms of the 1.67 ms mf128 step (profiles/r04_final_bench_mf128.json).
+// Here the 28 tiles are split over the workgroup's 4 waves -- 7 each, 112 accumulator registers
+// pinned to AGPRs -- every wave runs the forward and the data-gradient chain of its own 32-sample
+// tile, writes the weight-gradient operands (transposed T chunks) stage by stage into its images, and
+// after a barrier accumulates ITS tiles of that stage over all four waves' tiles, waves 0..3 in order
+// (a fixed summation order: deterministic).  Tiles per wave w:
+//   dWr3[w] (16 x 32 block w of the 16 x 128), dWr2[w][0..3] (row block w), dWr1[w],
+//   and dW2[w] (waves 0, 1) or dW1[w - 2] (waves 2, 3).
+// All 106 fragments stay in LDS (106 KB) beside 6 images per wave (48 KB): one workgroup per CU.
+// Stages (images per wave): S1 dO, R2 x4 | S2a dR2 x4, R1[0..1] | S2b R1[2..3] over R1[0..1] |
+// S3 dR1 x4, [SH;h] | S4 dh, Y1 x2 | S5 dY1 x2, X.
+constexpr int COOP128_SLOTS = 6;
+constexpr size_t COOP128_LDS = (size_t)Geo<128>::N * FRAG_HALFS * 2 + (size_t)4 * COOP128_SLOTS * TILE_BYTES;
+static_assert(COOP128_LDS <= 160 * 1024, "one cooperative W = 128 workgroup per CU");
 
-template <int W>
-__global__ __launch_bounds__(FIELD_BLOCK) void field_bw_wr2_kernel(
+template <bool PLANAR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void field_bw_coop128_kernel(
     const _Float16* __restrict__ feat, int64_t plane_stride, const float* __restrict__ dirs, int64_t n,
-    const int32_t* __restrict__ n_dev, const _Float16* __restrict__ packed, const float* __restrict__ dL_drgb,
-    float grad_scale, const float* __restrict__ scale_dev, float* __restrict__ slab, int32_t* __restrict__ nonfinite) {
+    const int32_t* __restrict__ n_dev, const _Float16* __restrict__ packed, const float* __restrict__ dL_dsigma,
+    const float* __restrict__ dL_drgb, float grad_scale, const float* __restrict__ scale_dev,
+    float* __restrict__ dL_dfeat, float* __restrict__ slab, int32_t* __restrict__ nonfinite, float* __restrict__ level_l1) {
+    constexpr int W = 128;
     using G = Geo<W>;
     constexpr int MT = G::MT;
-    constexpr int NF = G::B4;  // forward fragments + Wr3^T (B5)
-    constexpr int oR2 = N_XYZ_PARAMS + W * 32;
-    static_assert((size_t)W * W * 4 <= WR2_LDS<W>(), "dWr2 image must fit the kernel's LDS");
+    constexpr int oR1 = N_XYZ_PARAMS, oR2 = oR1 + W * 32, oR3 = oR2 + W * W;
+    constexpr size_t IMG_OFF = (size_t)G::N * FRAG_HALFS * 2;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     _Float16* lds_base = reinterpret_cast<_Float16*>(smem);
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(packed);
-        uint4* dst = reinterpret_cast<uint4*>(lds_base);
-        for (int i = threadIdx.x; i < NF * 64; i += blockDim.x) dst[i] = src[i];
-        __syncthreads();
-    }
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    load_frags_bw<W, 4>(lds_base, packed);
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform)
     const int r = lane & 31, h = lane >> 5;
     const float S = scale_dev ? *scale_dev : grad_scale, invS = 1.0f / S;
     const f32x16 z = {};
-    f32x16 acc[MT][MT];
+    f32x16 a_r3 = z, a_r1 = z, a_x = z, a_r2[MT];  // this wave's seven tiles (table above)
 #pragma unroll
-    for (int a = 0; a < MT; ++a)
-#pragma unroll
-        for (int b = 0; b < MT; ++b) acc[a][b] = z;
+    for (int i = 0; i < MT; ++i) a_r2[i] = z;
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
     const int64_t tiles = div_up<int64_t>(nn, 32);
-    const int64_t stride = (int64_t)gridDim.x * 4;
-    TileIn nI;
-    float ng0 = 0.f, ng1 = 0.f, ng2 = 0.f;
-    auto fetch = [&](int64_t tile) {
+    const int64_t groups = div_up<int64_t>(tiles, 4);  // group g = tiles 4g .. 4g+3, one per wave
+    struct BwIn { TileIn I; float gs, g0, g1, g2; bool live; };
+    BwIn nx;
+    // as field_bw_coop_kernel: every lane loads (index clamped), the incoming gradients are zeroed
+    // where the sample is out of range or on lanes h == 1 -- an idle wave's tile contributes zeros
+    auto fetch = [&](int64_t tile, BwIn& o) {
         const int64_t s = tile * 32 + r;
-        const bool v = s < nn;
-        load_tile_in(feat, plane_stride, dirs, s, v, h, true, nI);
-        ng0 = ng1 = ng2 = 0.0f;
-        if (v && h == 0) { ng0 = dL_drgb[3 * s]; ng1 = dL_drgb[3 * s + 1]; ng2 = dL_drgb[3 * s + 2]; }
+        const bool v = s < nn && h == 0;
+        const int64_t sc = max<int64_t>(0, min<int64_t>(s, nn - 1));
+        if constexpr (PLANAR) {
+            const uint32_t* Pp = reinterpret_cast<const uint32_t*>(feat);
+            uint32_t u[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                u[k] = Pp[(int64_t)(4 * h + k) * plane_stride + sc];
+                u[4 + k] = Pp[(int64_t)(8 + 4 * h + k) * plane_stride + sc];
+            }
+            o.I.x[0] = *reinterpret_cast<const half8*>(&u[0]);
+            o.I.x[1] = *reinterpret_cast<const half8*>(&u[4]);
+        } else {
+            const half8* row = reinterpret_cast<const half8*>(feat + sc * 32);
+            o.I.x[0] = row[h];
+            o.I.x[1] = row[2 + h];
+        }
+        o.I.d[0] = dirs[3 * sc]; o.I.d[1] = dirs[3 * sc + 1]; o.I.d[2] = dirs[3 * sc + 2];
+        o.gs = dL_dsigma[sc]; o.g0 = dL_drgb[3 * sc]; o.g1 = dL_drgb[3 * sc + 1]; o.g2 = dL_drgb[3 * sc + 2];
+        o.live = v;
     };
-    const int64_t tile0 = (int64_t)blockIdx.x * 4 + wid;
-    if (tile0 < tiles) fetch(tile0);
-    for (int64_t tile = tile0; tile < tiles; tile += stride) {
+    auto zero_grads = [&](BwIn& o) {
+        o.gs = o.live ? o.gs : 0.0f;
+        o.g0 = o.live ? o.g0 : 0.0f;
+        o.g1 = o.live ? o.g1 : 0.0f;
+        o.g2 = o.live ? o.g2 : 0.0f;
+    };
+    if ((int64_t)blockIdx.x < groups) fetch(4 * (int64_t)blockIdx.x + wid, nx);
+    bool bad = false;
+    float l1a[4] = {0.f, 0.f, 0.f, 0.f}, l1b[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t g = blockIdx.x; g < groups; g += gridDim.x) {
         int opaque = 0;
         asm volatile("" : "+s"(opaque));
         const _Float16* lds = lds_base + opaque;
-        // this wave's transpose slots: R1's MT tiles, then one per dR2 tile
-        _Float16* tsl = lds_base + opaque + NF * FRAG_HALFS + wid * (WR2_SLOTS * TILE_HALFS);
+        _Float16* area = lds_base + opaque + IMG_OFF / 2;
+        auto slot = [&](int u, int k) { return area + (u * COOP128_SLOTS + k) * TILE_HALFS; };
+        auto put2 = [&](_Float16* sl, const half8* v) {  // a 32-channel tile as two perm chunks
+            t_put(sl, lane, v[0], 0, true);
+            t_put(sl, lane, v[1], 4, true);
+        };
+        const int64_t tile = 4 * g + wid;
+        BwIn in = nx;
+        zero_grads(in);
+        fetch(4 * (g + (int64_t)gridDim.x) + wid, nx);  // (clamped past the end)
         const bool valid = tile * 32 + r < nn;
-        const TileIn I = nI;
-        const float g0 = ng0, g1 = ng1, g2 = ng2;
-        if (tile + stride < tiles) fetch(tile + stride);
         FwdTile<W> T;
-        forward_tile<W, false>(lds, lane, I, valid, T);
-        f32x16 dO = z;
-        if (h == 0) {
-            dO[0] = g0 * S * T.rgb[0] * (1.0f - T.rgb[0]);
-            dO[1] = g1 * S * T.rgb[1] * (1.0f - T.rgb[1]);
-            dO[2] = g2 * S * T.rgb[2] * (1.0f - T.rgb[2]);
+        forward_tiles<W, false, 1>(lds, lane, &in.I, &valid, &T);
+        half8 dOb;
+        {
+            f32x16 dO = z;
+            dO[0] = in.g0 * S * T.rgb[0] * (1.0f - T.rgb[0]);
+            dO[1] = in.g1 * S * T.rgb[1] * (1.0f - T.rgb[1]);
+            dO[2] = in.g2 * S * T.rgb[2] * (1.0f - T.rgb[2]);
+            dOb = pack8<0, false>(dO);
         }
-        const half8 dOb = pack8<0, false>(dO);
+        //    dR2 = Wr3^T dO, masked by R2 > 0
+        half8 dr2p[MT][2];
 #pragma unroll
-        for (int i = 0; i < MT; ++i) {
-            t_put(tsl + i * TILE_HALFS, lane, T.r1[i][0], 0, true);
-            t_put(tsl + i * TILE_HALFS, lane, T.r1[i][1], 4, true);
+        for (int mt = 0; mt < MT; ++mt) {
+            const f32x16 a = mfma(lds_frag(lds, G::B5 + mt, lane), dOb, z);
+            dr2p[mt][0] = relu_mask8(pack8<0, false>(a), T.r2[mt][0]);
+            dr2p[mt][1] = relu_mask8(pack8<8, false>(a), T.r2[mt][1]);
         }
-        half8 dr2[MT][2];
+        // ---- S1: dO, R2 -> dWr3[w]
+        t_put(slot(wid, 0), lane, dOb, 0, true);  // (channels 16..31 stale: rows 16..31 of dWr3, dropped)
 #pragma unroll
-        for (int o = 0; o < MT; ++o) {
-            f32x16 a = mfma(lds_frag(lds, G::B5 + o, lane), dOb, z);
-            dr2[o][0] = relu_mask8(pack8<0, false>(a), T.r2[o][0]);
-            dr2[o][1] = relu_mask8(pack8<8, false>(a), T.r2[o][1]);
-            t_put(tsl + (MT + o) * TILE_HALFS, lane, dr2[o][0], 0, true);
-            t_put(tsl + (MT + o) * TILE_HALFS, lane, dr2[o][1], 4, true);
-        }
-        SOp x[MT];
+        for (int i = 0; i < MT; ++i) put2(slot(wid, 1 + i), T.r2[i]);
+        __syncthreads();
 #pragma unroll
-        for (int i = 0; i < MT; ++i) x[i] = s_get(tsl + i * TILE_HALFS, lane);
+        for (int u = 0; u < 4; ++u) acc_tile(a_r3, s_get(slot(u, 0), lane), s_get(slot(u, 1 + wid), lane));
+        //    dR1 = Wr2^T dR2, masked by R1 > 0
+        half8 dr1p[MT][2];
 #pragma unroll
-        for (int o = 0; o < MT; ++o) {
-            const SOp d = s_get(tsl + (MT + o) * TILE_HALFS, lane);
+        for (int mt = 0; mt < MT; ++mt) {
+            f32x16 a = z;
 #pragma unroll
-            for (int i = 0; i < MT; ++i) dw_acc_agpr(acc[o][i], d, x[i]);
-        }
-    }
-    xdl_drain();
-    __syncthreads();
-    float* img = reinterpret_cast<float*>(smem);
-    for (int i = threadIdx.x; i < W * W; i += blockDim.x) img[i] = 0.0f;
-    __syncthreads();
-    for (int wv = 0; wv < FIELD_BLOCK / 64; ++wv) {  // fixed wave order (see field_bw_kernel)
-        if ((int)(threadIdx.x >> 6) == wv) {
+            for (int t = 0; t < MT; ++t)
 #pragma unroll
-            for (int o = 0; o < MT; ++o)
-#pragma unroll
-                for (int i = 0; i < MT; ++i) dw_add32(img, acc[o][i], o, i, W, W, lane);
+                for (int k = 0; k < 2; ++k) a = mfma(lds_frag(lds, G::B4 + mt * G::KC + t * 2 + k, lane), dr2p[t][k], a);
+            dr1p[mt][0] = relu_mask8(pack8<0, false>(a), T.r1[mt][0]);
+            dr1p[mt][1] = relu_mask8(pack8<8, false>(a), T.r1[mt][1]);
         }
         __syncthreads();
+        // ---- S2a: dR2, R1[0..1] -> dWr2[w][0..1]
+#pragma unroll
+        for (int o = 0; o < MT; ++o) put2(slot(wid, o), dr2p[o]);
+        put2(slot(wid, 4), T.r1[0]);
+        put2(slot(wid, 5), T.r1[1]);
+        //    d[SH;h] = Wr1^T dR1 (rows 16..31 = dh) + TruncExp backward into h[0]
+        half8 dhb;
+        {
+            f32x16 dsh = z;
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) dsh = mfma(lds_frag(lds, G::B3 + t * 2 + k, lane), dr1p[t][k], dsh);
+            const float dh0 = in.gs * S * __expf(fminf(fmaxf(T.h0, -15.0f), 15.0f));
+            dsh[8] = h == 0 ? dsh[8] + dh0 : dsh[8];
+            dhb = pack8<8, false>(dsh);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const SOp d = s_get(slot(u, wid), lane);
+            acc_tile(a_r2[0], d, s_get(slot(u, 4), lane));
+            acc_tile(a_r2[1], d, s_get(slot(u, 5), lane));
+        }
+        //    dY1 = W2^T dh, masked by Y1 > 0; dX = W1^T dY1
+        half8 dy1p[2][2];
+        f32x16 dx = z;
+        {
+            const f32x16 a0 = mfma(lds_frag(lds, G::B2 + 0, lane), dhb, z);
+            const f32x16 a1 = mfma(lds_frag(lds, G::B2 + 1, lane), dhb, z);
+            dy1p[0][0] = relu_mask8(pack8<0, false>(a0), T.y1[0][0]);
+            dy1p[0][1] = relu_mask8(pack8<8, false>(a0), T.y1[0][1]);
+            dy1p[1][0] = relu_mask8(pack8<0, false>(a1), T.y1[1][0]);
+            dy1p[1][1] = relu_mask8(pack8<8, false>(a1), T.y1[1][1]);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) dx = mfma(lds_frag(lds, G::B1 + t * 2 + k, lane), dy1p[t][k], dx);
+        }
+        __syncthreads();
+        // ---- S2b: R1[2..3] over R1[0..1] -> dWr2[w][2..3] (dR2 still in slots 0..3)
+        put2(slot(wid, 4), T.r1[2]);
+        put2(slot(wid, 5), T.r1[3]);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const SOp d = s_get(slot(u, wid), lane);
+            acc_tile(a_r2[2], d, s_get(slot(u, 4), lane));
+            acc_tile(a_r2[3], d, s_get(slot(u, 5), lane));
+        }
+        // dX = W1^T dY1 -> global fp32 (features (i&3)+8(i>>2)+4h), this wave's own tile
+        {
+            const int64_t s = tile * 32 + r;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 o = make_float4(dx[4 * q] * invS, dx[4 * q + 1] * invS, dx[4 * q + 2] * invS, dx[4 * q + 3] * invS);
+                bad |= !(isfinite(o.x) && isfinite(o.y) && isfinite(o.z) && isfinite(o.w));
+                if (s < nn) reinterpret_cast<float4*>(dL_dfeat + s * 32)[2 * q + h] = o;
+                l1a[q] += fabsf(o.x) + fabsf(o.y);
+                l1b[q] += fabsf(o.z) + fabsf(o.w);
+            }
+        }
+        __syncthreads();
+        // ---- S3: dR1, [SH;h] -> dWr1[w]
+#pragma unroll
+        for (int o = 0; o < MT; ++o) put2(slot(wid, o), dr1p[o]);
+        t_put(slot(wid, 4), lane, T.sh, 0, false);
+        t_put(slot(wid, 4), lane, T.hb, 4, true);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc_tile(a_r1, s_get(slot(u, wid), lane), s_get(slot(u, 4), lane));
+        __syncthreads();
+        // ---- S4: dh, Y1 -> dW2 (waves 0, 1)
+        t_put(slot(wid, 0), lane, dhb, 0, true);  // (channels 16..31 stale: rows of dW2 dropped)
+        put2(slot(wid, 1), T.y1[0]);
+        put2(slot(wid, 2), T.y1[1]);
+        __syncthreads();
+        if (wid < 2) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc_tile(a_x, s_get(slot(u, 0), lane), s_get(slot(u, 1 + wid), lane));
+        }
+        __syncthreads();
+        // ---- S5: dY1, X -> dW1 (waves 2, 3)
+        put2(slot(wid, 0), dy1p[0]);
+        put2(slot(wid, 1), dy1p[1]);
+        t_put(slot(wid, 2), lane, T.x[0], 0, false);
+        t_put(slot(wid, 2), lane, T.x[1], 4, false);
+        __syncthreads();
+        if (wid >= 2) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc_tile(a_x, s_get(slot(u, wid - 2), lane), s_get(slot(u, 2), lane));
+        }
+        __syncthreads();  // the images are rewritten by the next group's S1
     }
-    float* row = slab + (int64_t)blockIdx.x * G::N_DW + oR2;
-    bool rbad = false;
-    for (int i = threadIdx.x; i < W * W; i += blockDim.x) {
-        const float val = img[i] * invS;
-        row[i] = val;
-        rbad |= !isfinite(val);
+    if (nonfinite && __any(bad) && lane == 0) atomicOr(nonfinite, 1);
+
+    // ---- epilogue: each tile stored by its owner wave (disjoint, every entry once) -> one slab row
+    float* row = slab + (int64_t)blockIdx.x * G::N_DW;
+    {
+        constexpr int N_IMG = G::N_DW;
+        static_assert((size_t)N_IMG * 4 + 64 <= IMG_OFF, "reduction image must fit the fragment area");
+        xdl_drain();
+        __syncthreads();
+        float* img = reinterpret_cast<float*>(smem);
+        float* l1_part = img + N_IMG;
+        if (threadIdx.x < 16) l1_part[threadIdx.x] = 0.0f;
+        __syncthreads();
+        if (level_l1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float a = l1a[q], b = l1b[q];
+#pragma unroll
+                for (int off = 16; off > 0; off >>= 1) { a += __shfl_xor(a, off, 64); b += __shfl_xor(b, off, 64); }
+                if (r == 0) { atomicAdd(l1_part + 4 * q + 2 * h, a); atomicAdd(l1_part + 4 * q + 2 * h + 1, b); }
+            }
+        }
+        dw_add32(img + oR3, a_r3, 0, wid, 16, W, lane, true);
+        dw_add32(img + oR1, a_r1, wid, 0, W, 32, lane, true);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) dw_add32(img + oR2, a_r2[i], wid, i, W, W, lane, true);
+        if (wid < 2) dw_add32(img + 64 * 32, a_x, 0, wid, 16, 64, lane, true);
+        else dw_add32(img, a_x, wid - 2, 0, 64, 32, lane, true);
+        __syncthreads();
+        bool rbad = false;  // a non-finite weight-gradient partial (see slab_row_flag)
+        for (int i = threadIdx.x; i < G::N_DW; i += blockDim.x) {
+            const float val = img[i] * invS;
+            row[i] = val;
+            rbad |= !isfinite(val);
+        }
+        slab_row_flag(nonfinite, rbad);
+        if (level_l1 && threadIdx.x < 16) atomicAdd(level_l1 + threadIdx.x, l1_part[threadIdx.x]);
     }
-    slab_row_flag(nonfinite, rbad);
 }
 
 // grad[p] += sum over slab rows (fixed order: deterministic).  64 columns x 4 row groups per block.
@@ -1330,8 +1056,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 
 constexpr int BW_BLOCKS = 256;  // one workgroup per CU (persistent)
 
-// W = 64 through field_bw_coop_kernel (two waves per SIMD, COOP_BLOCKS slab rows)
-bool coop64() { return true; }
+// slab rows: W = 64 field_bw_coop_kernel (two workgroups per CU), W = 128 field_bw_coop128_kernel (one)
 int bw_rows(int w) { return w == 64 ? COOP_BLOCKS : BW_BLOCKS; }
 
 bool width_ok(int w) { return w == 64 || w == 128; }
@@ -1365,67 +1090,35 @@ void launch_fw(const void* feat, int64_t ps, const float* dirs, int64_t n, const
                            (const _Float16*)packed, sigma, rgb, nullptr, nullptr);
 }
 
-template <int W, int NW>
+// the cooperative backward of width W (its kernel pair, workgroups = slab rows, LDS), then the slab fold
+// (unless deferred: grad_xyz null, mfnerf_field_bw_reduce folds the slab later)
+template <int W>
 int launch_bw(const void* feat, int64_t ps, const float* dirs, int64_t n, const int32_t* n_dev, const void* packed,
               const float* dL_dsigma, const float* dL_drgb, float grad_scale, const float* scale_dev, float* dL_dfeat,
               float* grad_xyz, float* grad_rgb, void* workspace, int32_t* nonfinite, float* level_l1,
               mfnerf_stream_t stream) {
-    using C = BwCfg<W, NW>;
-    if constexpr (W == 64) {
-        if (coop64()) {
-            static const hipError_t attr = [] {
-                const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_coop_kernel<false>),
-                                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)COOP_LDS);
-                const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_coop_kernel<true>),
-                                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)COOP_LDS);
-                return a0 != hipSuccess ? a0 : a1;
-            }();
-            if (attr != hipSuccess) {
-                mfn_set_error("field_bw: cannot raise the LDS limit to %d bytes", (int)COOP_LDS);
-                return MFN_ERR_INVALID;
-            }
-            auto k = ps > 0 ? field_bw_coop_kernel<true> : field_bw_coop_kernel<false>;
-            hipLaunchKernelGGL(k, dim3(COOP_BLOCKS), dim3(256), COOP_LDS, stream, (const _Float16*)feat, ps, dirs, n,
-                               n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb, grad_scale, scale_dev, dL_dfeat,
-                               (float*)workspace, nonfinite, level_l1);
-            if (grad_xyz)
-                hipLaunchKernelGGL(slab_reduce_kernel<W>, dim3((Geo<W>::N_DW + 63) / 64), dim3(256), 0, stream,
-                                   (const float*)workspace, COOP_BLOCKS, grad_xyz, grad_rgb, nonfinite, 0);
-            return MFN_OK;
-        }
+    using K = decltype(&field_bw_coop_kernel<false>);
+    constexpr K k0 = W == 64 ? field_bw_coop_kernel<false> : field_bw_coop128_kernel<false>;
+    constexpr K k1 = W == 64 ? field_bw_coop_kernel<true> : field_bw_coop128_kernel<true>;
+    constexpr size_t lds = W == 64 ? COOP_LDS : COOP128_LDS;
+    const int rows = bw_rows(W);
+    static const hipError_t attr = [] {
+        const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(k0),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(k1),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        return a0 != hipSuccess ? a0 : a1;
+    }();
+    if (attr != hipSuccess) {
+        mfn_set_error("field_bw: cannot raise the LDS limit to %d bytes", (int)lds);
+        return MFN_ERR_INVALID;
     }
-    if constexpr (C::LDS > 65536) {  // more than the default dynamic-LDS limit
-        static const hipError_t attr = [] {
-            const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_kernel<W, NW, false>),
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
-            const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_kernel<W, NW, true>),
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
-            hipError_t a2 = hipSuccess;
-            if constexpr (C::R2_SPLIT)
-                a2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bw_wr2_kernel<W>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)WR2_LDS<W>());
-            return a0 != hipSuccess ? a0 : a1 != hipSuccess ? a1 : a2;
-        }();
-        if (attr != hipSuccess) {
-            mfn_set_error("field_bw: cannot raise the LDS limit to %d bytes", (int)C::LDS);
-            return MFN_ERR_INVALID;
-        }
-    }
-    if (ps > 0)
-        hipLaunchKernelGGL((field_bw_kernel<W, NW, true>), dim3(BW_BLOCKS), dim3(64 * NW), C::LDS, stream,
-                           (const _Float16*)feat, ps, dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb,
-                           grad_scale, scale_dev, dL_dfeat, (float*)workspace, nonfinite, level_l1);
-    else
-        hipLaunchKernelGGL((field_bw_kernel<W, NW, false>), dim3(BW_BLOCKS), dim3(64 * NW), C::LDS, stream,
-                           (const _Float16*)feat, ps, dirs, n, n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb,
-                           grad_scale, scale_dev, dL_dfeat, (float*)workspace, nonfinite, level_l1);
-    if constexpr (C::R2_SPLIT)
-        hipLaunchKernelGGL(field_bw_wr2_kernel<W>, dim3(BW_BLOCKS), dim3(FIELD_BLOCK), WR2_LDS<W>(), stream,
-                           (const _Float16*)feat, ps, dirs, n, n_dev,
-                           (const _Float16*)packed, dL_drgb, grad_scale, scale_dev, (float*)workspace, nonfinite);
-    if (grad_xyz)  // else deferred: mfnerf_field_bw_reduce folds the slab later
+    hipLaunchKernelGGL(ps > 0 ? k1 : k0, dim3(rows), dim3(256), lds, stream, (const _Float16*)feat, ps, dirs, n,
+                       n_dev, (const _Float16*)packed, dL_dsigma, dL_drgb, grad_scale, scale_dev, dL_dfeat,
+                       (float*)workspace, nonfinite, level_l1);
+    if (grad_xyz)
         hipLaunchKernelGGL(slab_reduce_kernel<W>, dim3((Geo<W>::N_DW + 63) / 64), dim3(256), 0, stream,
-                           (const float*)workspace, BW_BLOCKS, grad_xyz, grad_rgb, nonfinite, 0);
+                           (const float*)workspace, rows, grad_xyz, grad_rgb, nonfinite, 0);
     return MFN_OK;
 }
 
@@ -1528,10 +1221,10 @@ int mfnerf_field_bw(const void* feat_f16, int64_t feat_plane_stride, const float
     const float* scale_dev = grad_scale == 0.0f ? &amp->scale : nullptr;
     int st;
     if (rgb_width == 128)
-        st = launch_bw<128, 4>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, dL_dsigma, dL_drgb, grad_scale,
+        st = launch_bw<128>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, dL_dsigma, dL_drgb, grad_scale,
                                scale_dev, dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
     else
-        st = launch_bw<64, 4>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, dL_dsigma, dL_drgb, grad_scale,
+        st = launch_bw<64>(feat_f16, feat_plane_stride, dirs, n, n_dev, packed, dL_dsigma, dL_drgb, grad_scale,
                               scale_dev, dL_dfeat, grad_xyz, grad_rgb, workspace, nonfinite, level_l1, stream);
     if (st != MFN_OK) return st;
     return mfn_check_launch("field_bw");
