@@ -16,13 +16,6 @@
 
 using namespace mfn;
 
-// MFN_PROBE (timing probe builds only, tools/build_variant.sh EXTRA=-DMFN_PROBE=k; results invalid):
-// bit 0 accumulate without its adds, bit 1 without its record DMA, bit 2 scatter without its record
-// stores, bit 3 scatter without its counting atomics (every rank 0)
-#ifndef MFN_PROBE
-#define MFN_PROBE 0
-#endif
-
 __global__ void mfn_bump_step_kernel(int32_t* s, mfnerf_amp_state* amp, float* zero, int nz);  // adam.hip
 
 namespace {
@@ -417,7 +410,7 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_dense_kernel(const float* _
     if (zero_flag && blockIdx.x == 0 && threadIdx.x == 0) *zero_flag = 0;
     // gate (gate.hip's {signals, waits, ticket}): opened as the table-gradient launches begin, so the
     // side stream's next march starts beside them with no one-thread signal kernel of its own on
-    // the step's critical path (MFNERF_GATE_AT=grid_bw)
+    // the step's critical path
     if (gate && blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_fetch_add(gate, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     __shared__ float fs_s[MFN_MAX_LEVELS];
@@ -1209,7 +1202,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
             // the record's |a|, |b| maxima as two packed u16 (fp16 bits order like the values)
             auto rank = [&](int k, int lb, uint2 r) {
                 R[k].r = r;
-                R[k].meta = (uint32_t)lb | ((MFN_PROBE & 8) ? 0u : ((uint32_t)atomicAdd(&hist2[cp][lb], 1) << 16));
+                R[k].meta = (uint32_t)lb | ((uint32_t)atomicAdd(&hist2[cp][lb], 1) << 16);
                 rmax2 = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(
                     __builtin_bit_cast(ushort2v, rmax2), __builtin_bit_cast(ushort2v, r.y & 0x7fff7fffu)));
             };
@@ -1290,9 +1283,7 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
             const int lb = sbin[k];
             const int2 g = gd[lb];
             const uint2 r = stage[k];
-            if (MFN_PROBE & 4) {
-                if (r.x == 0xFFFFFFFFu) rec[0] = r;  // (keeps the stage reads)
-            } else if (k < g.y) {  // inside the unit's slot of the bin
+            if (k < g.y) {  // inside the unit's slot of the bin
                 // a plain store (round 5, r5c: the nontemporal store this was made the scatter 92 instead of
                 // 82.5 us and the step 3 us slower; the accumulate reads them the same either way)
                 rec[(uint32_t)(g.x + k)] = r;
@@ -1442,10 +1433,7 @@ struct AdamRest {
 // ray's run of consecutive samples in one cell (same-address atomics).  A partition holding more
 // records than the stage is done in chunks of ACC_RB records.  Same records, same integer adds:
 // bit-identical sums.  LDS: 16 KB image + 62 KB stage -> two workgroups per CU.
-#ifndef MFN_ACC_RB
-#define MFN_ACC_RB 7936
-#endif
-constexpr int ACC_RB = MFN_ACC_RB;  // (A/B builds override: smaller stages, more workgroups per CU)
+constexpr int ACC_RB = 7936;  // records per stage chunk (smaller stages, more workgroups per CU: no faster, r05_v1)
 struct AccumStage {
     unsigned long long img[MAX_BIN_ENTRIES];
     uint2 recs[ACC_RB];
@@ -1585,7 +1573,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
             const uint4* src = reinterpret_cast<const uint4*>(base + (uint32_t)(NW * j + wv) * (uint32_t)slot);
             for (int q = lo; q < hi; q += 128) {
                 const int k = q + 2 * lane;  // records k, k + 1 of the compacted partition (k even)
-                if (!(MFN_PROBE & 2) && k < hi)
+                if (k < hi)
                     __builtin_amdgcn_global_load_lds(src + ((k - r0) >> 1), &S.a.recs[q - c0], 16, 0, 0);
             }
         }
@@ -1607,7 +1595,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
             for (int q = 0; q < UR; ++q) r[q] = S.a.recs[min(i0 + q * ACC_THREADS + perm, ACC_RB - 1)];
 #pragma unroll
             for (int q = 0; q < UR; ++q)
-                if (!(MFN_PROBE & 1) && i0 + q * ACC_THREADS + perm < len) accum_record(img, mask, r[q], k2);
+                if (i0 + q * ACC_THREADS + perm < len) accum_record(img, mask, r[q], k2);
         }
     }
     __syncthreads();
