@@ -140,34 +140,30 @@ __global__ void march_count_kernel(MarchParams p, int64_t n_rays, int32_t* __res
 }
 
 // One-workgroup exclusive scan of the per-ray counts -> rays_a rows and counter (device resident).
-// 512 threads, few registers: the scan runs on the side stream while the scatter's 1024-thread workgroups hold
-// 16 waves of every CU; a 1024-thread workgroup found no CU until the scatter ended (~115 us later)
-constexpr int SCAN_THREADS = 512;
-constexpr int SCAN_K = 32;  // counts per thread held in registers (n_rays <= 16384)
-__global__ __launch_bounds__(SCAN_THREADS) void march_scan_kernel(const int32_t* __restrict__ counts, int64_t n_rays,
-                                                                 int64_t capacity, int64_t* __restrict__ rays_a,
-                                                                 int32_t* __restrict__ counter) {
+// It runs on the side stream beside the table-gradient scatter, whose 1024-thread workgroups hold 4
+// waves x 112 VGPRs of every SIMD: 64 VGPRs per SIMD lane stay free, room for ONE more wave of <= 64
+// registers per SIMD.  So 256 threads (one wave per SIMD) at <= 64 VGPRs: the 512-thread form (two
+// waves per SIMD) found no CU until the scatter ended -- 84 us in the step timeline
+// (profiles/r05_v5_march_estimate_timeline.txt) for a few microseconds of work.
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_K = 16;  // counts per thread loaded together
+__global__ __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(8))) void march_scan_kernel(
+    const int32_t* __restrict__ counts, int64_t n_rays, int64_t capacity, int64_t* __restrict__ rays_a,
+    int32_t* __restrict__ counter) {
     __shared__ int64_t wave_tot[SCAN_THREADS / 64];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int64_t chunk = div_up<int64_t>(n_rays, SCAN_THREADS);
-    const int64_t b = tid * chunk, e = min(n_rays, b + chunk);
-    // up to SCAN_K counts per thread (8192 rays: 16, 16384: 32) are loaded together: one memory round
-    // trip instead of chunk dependent ones (this kernel runs on the side stream beside the
-    // table-gradient scatter, where every load waits behind its traffic)
-    const bool staged = chunk <= SCAN_K;
-    int32_t cr[SCAN_K];
+    const int n = (int)n_rays;  // (<= 2^31: checked by the caller)
+    const int chunk = (n + SCAN_THREADS - 1) / SCAN_THREADS;
+    const int b = tid * chunk, e = min(n, b + chunk);
+    // SCAN_K counts per thread in flight together: one memory round trip per SCAN_K instead of chunk
+    // dependent ones (beside the scatter every load waits behind its traffic)
     int64_t local = 0;
-    if (staged) {
+    for (int b0 = b; b0 < e; b0 += SCAN_K) {
+        int32_t cr[SCAN_K];
 #pragma unroll
-        for (int k = 0; k < SCAN_K; ++k) {
-            const int64_t i = b + k;
-            const int32_t c = counts[i < e ? i : 0];
-            cr[k] = i < e ? c : 0;
-        }
+        for (int k = 0; k < SCAN_K; ++k) cr[k] = counts[b0 + k < e ? b0 + k : 0];
 #pragma unroll
-        for (int k = 0; k < SCAN_K; ++k) local += cr[k];
-    } else {
-        for (int64_t i = b; i < e; ++i) local += counts[i];
+        for (int k = 0; k < SCAN_K; ++k) local += b0 + k < e ? cr[k] : 0;
     }
     // inclusive wave scan
     int64_t v = local;
@@ -187,15 +183,17 @@ __global__ __launch_bounds__(SCAN_THREADS) void march_scan_kernel(const int32_t*
     }
     __syncthreads();
     int64_t run = (v - local) + (wid > 0 ? wave_tot[wid - 1] : 0);  // exclusive start of this chunk
-    {
-        // the write pass re-reads the counts (cache hits now) rather than keep SCAN_K registers live
-        // through it: the kernel must stay small to fit beside the scatter's waves
-#pragma unroll 4
-        for (int64_t i = b; i < e; ++i) {
-            const int64_t c = counts[i];
-            const int64_t s = min(run, capacity);
-            const int64_t cc = max<int64_t>(0, min(c, capacity - run));
-            rays_a[3 * i] = i; rays_a[3 * i + 1] = s; rays_a[3 * i + 2] = cc;
+    // the write pass re-reads the counts (cache hits now), SCAN_K at a time again, rather than keep
+    // them live through the scan: the kernel must stay within 64 registers
+    for (int b0 = b; b0 < e; b0 += SCAN_K) {
+        int32_t cr[SCAN_K];
+#pragma unroll
+        for (int k = 0; k < SCAN_K; ++k) cr[k] = counts[b0 + k < e ? b0 + k : 0];
+        for (int k = 0; k < SCAN_K && b0 + k < e; ++k) {
+            const int64_t i = b0 + k, c = cr[k];
+            rays_a[3 * i] = i;
+            rays_a[3 * i + 1] = min(run, capacity);
+            rays_a[3 * i + 2] = max<int64_t>(0, min(c, capacity - run));
             run += c;
         }
     }
@@ -382,7 +380,10 @@ __global__ __launch_bounds__(256) void march_wave_kernel(MarchParams p, int64_t 
 
 
 // The compacted samples of ray r (one wave): its first rays_a[r].count t values from march_wave.
-__global__ __launch_bounds__(256) void march_expand_kernel(MarchParams p, int64_t n_rays,
+// <= 64 VGPRs (waves_per_eu(8)): the kernel follows the scan beside the scatter, which leaves 64
+// registers per SIMD lane free (see march_scan_kernel); at 68 it waited for the scatter to end and ran
+// beside the accumulate instead.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void march_expand_kernel(MarchParams p, int64_t n_rays,
                                                            const int64_t* __restrict__ rays_a,
                                                            const float* __restrict__ tbuf, float* __restrict__ xyzs,
                                                            float* __restrict__ dirs, float* __restrict__ deltas,
@@ -883,8 +884,8 @@ int mfnerf_raymarching_train(const float* rays_o, const float* rays_d, const flo
                              const float* noise, int grid_size, int max_samples, int64_t n_rays, int64_t capacity,
                              int64_t* rays_a, float* xyzs, float* dirs, float* deltas, float* ts, int32_t* counter,
                              void* workspace, mfnerf_stream_t stream) {
-    if (n_rays < 0 || capacity < 0 || cascades < 1 || grid_size < 1 || grid_size > 1024 || max_samples < 1 ||
-        hits_stride < 2) {
+    if (n_rays < 0 || n_rays > INT32_MAX - SCAN_THREADS || capacity < 0 || cascades < 1 || grid_size < 1 ||
+        grid_size > 1024 || max_samples < 1 || hits_stride < 2) {
         mfn_set_error("raymarching_train: bad arguments"); return MFN_ERR_INVALID;
     }
     if (!counter) { mfn_set_error("raymarching_train: null counter"); return MFN_ERR_INVALID; }
