@@ -422,7 +422,8 @@ int mfnerf_occupancy_update(float* density_grid, const float* sigmas, const int3
  * sigma per cell can reach the grid (`density_grid_tmp[c, indices] = ...`, networks.py:259, an
  * index_put whose duplicate writes land in no defined order), so the draws only mark their cells and
  * ONE jittered point is produced per distinct drawn cell -- keyed by (seed, call, cell) -- in ascending
- * cell order (morton within a cascade); *count_dev receives their number (<= the capacity
+ * row-major cell order within a cascade (x fastest; cell_idx still holds the cascade * G^3 + morton
+ * index; the warm-up's every cell: morton order); *count_dev receives their number (<= the capacity
  * mfnerf_occupancy_points_unique(...)).  The set of probed cells is exactly the set the plain call
  * with the same seed and call index draws.  Deterministic.  The workspace must be zero-filled before
  * its first use (the call leaves its byte map zeroed); cascades*G^3 must be a multiple of 16.

@@ -179,12 +179,24 @@ __global__ __launch_bounds__(OCC_BLOCK) void occ_points_kernel(PointsArgs a, con
     }
 }
 
+// The byte map of the de-duplicated draw is indexed in ROW-MAJOR order within a cascade (x fastest),
+// so the probe points reach the encode x-neighbour after x-neighbour: the hashed levels' index is
+// x ^ (y p1) ^ (z p2), so x-adjacent probes read adjacent table entries (shared lines) where the
+// morton order put y/z neighbours -- a different line per lane -- next to each other.
+__device__ __forceinline__ uint32_t row_major(int G, uint32_t m) {
+    return morton3_invert(m) + (uint32_t)G * (morton3_invert(m >> 1) + (uint32_t)G * morton3_invert(m >> 2));
+}
+__device__ __forceinline__ uint32_t morton_of_row_major(int G, uint32_t r) {
+    const uint32_t x = r % (uint32_t)G, yz = r / (uint32_t)G;
+    return morton3(x, yz % (uint32_t)G, yz / (uint32_t)G);
+}
+
 // ---- the de-duplicated draw (mfnerf_occupancy_cells_unique*): the reference probes every draw and
 // keeps one sigma per cell (`density_grid_tmp[c, indices] = sigmas`, an index_put whose duplicate
 // writes land in no defined order), so only one jittered point per DISTINCT drawn cell can reach the
 // grid.  The draws only mark their cells in a byte map (idempotent plain stores, no atomics); the map
-// is compacted in ascending cell order (morton within a cascade: spatially coherent points for the
-// encode) and each marked cell gets one uniform jitter keyed by (call, cell).  Same distribution as
+// is compacted in ascending row-major cell order within a cascade (x-neighbours adjacent, below) and
+// each marked cell gets one uniform jitter keyed by (call, morton cell).  Same distribution as
 // the reference's update -- the set of drawn cells, one uniform point per cell -- with ~60 % of the
 // points at a trained scene's occupancy, and deterministic (no write race on duplicates).
 __global__ __launch_bounds__(OCC_BLOCK) void occ_mark_kernel(PointsArgs a, const int32_t* __restrict__ list,
@@ -197,7 +209,7 @@ __global__ __launch_bounds__(OCC_BLOCK) void occ_mark_kernel(PointsArgs a, const
         uint32_t m;
         bool ok;
         draw_cell(a, list, counts, p, c, m, ok);
-        if (ok) mark[(int64_t)c * a.cells + m] = 1;
+        if (ok) mark[(int64_t)c * a.cells + row_major(a.G, m)] = 1;
     }
 }
 
@@ -272,10 +284,12 @@ __global__ __launch_bounds__(OCC_BLOCK) void occ_unique_points_kernel(PointsArgs
     const uint64_t jkey = splitmix64_host(a.key ^ OCC_JITTER_MIX);
     const int64_t n = *count;
     for (int64_t i = (int64_t)blockIdx.x * OCC_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * OCC_BLOCK) {
-        const int32_t f = list[i];
-        const int c = (int)(f / a.cells);
-        cell_point(a, c, (uint32_t)(f - (int64_t)c * a.cells), jkey, 8 * (uint64_t)f + 4, xyzs + 3 * i);
-        cell[i] = f;
+        const int32_t r = list[i];  // (row-major within the cascade)
+        const int c = (int)(r / a.cells);
+        const uint32_t m = morton_of_row_major(a.G, (uint32_t)(r - (int64_t)c * a.cells));
+        const int64_t f = (int64_t)c * a.cells + m;
+        cell_point(a, c, m, jkey, 8 * (uint64_t)f + 4, xyzs + 3 * i);
+        cell[i] = (int32_t)f;
     }
 }
 

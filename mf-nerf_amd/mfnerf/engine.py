@@ -1063,7 +1063,7 @@ class TrainStep:
         thr = 0.01 * MAX_SAMPLES / SQRT3
         M = G ** 3 // 4
         # the draws of sample_uniform_and_occupied_cells / get_all_cells reduced to one jittered point per
-        # distinct drawn cell (the only sigmas the grid can keep), in ascending cell order; count on the device
+        # distinct drawn cell (the only sigmas the grid can keep), in row-major cell order; count on the device
         n = load().mfnerf_occupancy_points_unique(C, G, M, int(warmup))
         call("mfnerf_occupancy_cells_unique_dev", ptr(self.density_grid), C, G, float(c.scale), M, int(warmup), thr,
              seed, ptr(o.calls), ptr(o.xyz), ptr(o.cell), ptr(o.count), ptr(o.ws), s)

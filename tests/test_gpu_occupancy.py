@@ -162,7 +162,10 @@ def test_engine_refresh_end_to_end(gpu):
         cap = load().mfnerf_occupancy_points_unique(st.cascades, st.G, st.G ** 3 // 4, int(warm))
         assert 0 < n <= cap
         cell = o.cell[:n].cpu().long()
-        assert (cell[1:] > cell[:-1]).all()  # distinct, ascending
+        # distinct, in morton order (warm-up: every cell) or the unique draw's row-major order
+        assert torch.equal(cell, torch.sort(cell).values if warm else _row_major(cell, st.G))
+        srt = torch.sort(cell).values
+        assert (srt[1:] > srt[:-1]).all()
         if warm:
             assert n == st.cascades * st.G ** 3
         ref_g, thr, ref_bf = OO.update(before, o.sigma[:n].cpu(), cell.int())
@@ -195,18 +198,29 @@ def _cells_unique(gpu, grid, C, G, scale, M, warmup, ws, seed=0, call_index=0, t
     return xyz[:k].cpu(), cell[:k].cpu()
 
 
+def _row_major(cells, G):
+    """cells (cascade * G^3 + morton) in the unique draw's order: ascending row-major cell index
+    (x fastest) within each cascade."""
+    from oracle import vren_oracle
+    c, m = cells // G ** 3, cells % G ** 3
+    q = vren_oracle.morton3D_invert(m.cpu().int()).long().to(cells.device)
+    key = c * G ** 3 + q[:, 0] + G * (q[:, 1] + G * q[:, 2])
+    return cells[torch.argsort(key)]
+
+
 @pytest.mark.parametrize("C,G,scale", [(1, 128, 0.5), (2, 32, 1.0)])
 def test_unique_draw_probes_each_drawn_cell_once(gpu, C, G, scale):
     """mfnerf_occupancy_cells_unique: exactly the distinct cells the plain draw (same seed, call index)
-    draws, ascending, one point each inside its cell with the jitter spread over the cell; the byte
-    map is left zero (a repeat gives the same result); an empty occupied set adds no cell."""
+    draws, in ascending row-major order within a cascade, one point each inside its cell with the
+    jitter spread over the cell; the byte map is left zero (a repeat gives the same result); an empty
+    occupied set adds no cell; the warm-up lists every cell in morton order."""
     g = torch.Generator().manual_seed(5)
     grid = (torch.rand(C, G ** 3, generator=g) * 2 * THR - THR / 2).to(gpu)
     M = G ** 3 // 4
     _, plain, _ = _cells(gpu, grid, C, G, scale, M, False, seed=3, call_index=2)
     ws = torch.zeros(load().mfnerf_occupancy_workspace(C, G), dtype=torch.uint8, device=gpu)
     xyz, cell = _cells_unique(gpu, grid, C, G, scale, M, False, ws, seed=3, call_index=2)
-    want = torch.unique(plain[plain >= 0].long())
+    want = _row_major(torch.unique(plain[plain >= 0].long()), G)
     assert torch.equal(cell.long(), want)
     assert cell.numel() < plain.numel()  # the duplicates are gone
     assert OO.cell_points_ok(xyz, cell, C, G, scale)
@@ -217,8 +231,8 @@ def test_unique_draw_probes_each_drawn_cell_once(gpu, C, G, scale):
     # an empty occupied set: only the uniform draws' cells
     _, plain0, _ = _cells(gpu, torch.zeros_like(grid), C, G, scale, M, False, seed=3, call_index=2)
     _, cell0 = _cells_unique(gpu, torch.zeros_like(grid), C, G, scale, M, False, ws, seed=3, call_index=2)
-    assert torch.equal(cell0.long(), torch.unique(plain0[plain0 >= 0].long()))
-    # warm-up: every cell, in order
+    assert torch.equal(cell0.long(), _row_major(torch.unique(plain0[plain0 >= 0].long()), G))
+    # warm-up: every cell, in (morton) order
     _, cw = _cells_unique(gpu, grid, C, G, scale, M, True, ws)
     assert torch.equal(cw.long(), torch.arange(C * G ** 3))
 
