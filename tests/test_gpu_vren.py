@@ -91,7 +91,7 @@ def _march_both(gpu, oracle, o, d, ht, bf, cascades, scale, exp_step, max_sample
     return ref, [t.cpu() for t in out]
 
 
-@pytest.mark.parametrize("n_rays", [1, 256, 8192])
+@pytest.mark.parametrize("n_rays", [1, 256, 1000, 8192, 12345])  # (ragged: the scan's partial batches)
 def test_raymarching_train_lego_bitexact(gpu, oracle, n_rays):
     o, d, bf, _ = lego_inputs(n_rays)
     ht = aabb_hits(oracle, o, d)
