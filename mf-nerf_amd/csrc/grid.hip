@@ -1432,8 +1432,10 @@ struct AdamRest {
 // instruction's lanes hold records ~37 apart -- different slots, i.e. different rays -- instead of a
 // ray's run of consecutive samples in one cell (same-address atomics).  A partition holding more
 // records than the stage is done in chunks of ACC_RB records.  Same records, same integer adds:
-// bit-identical sums.  LDS: 16 KB image + 62 KB stage -> two workgroups per CU.
-constexpr int ACC_RB = 7936;  // records per stage chunk (smaller stages, more workgroups per CU: no faster, r05_v1)
+// bit-identical sums.  LDS: 16 KB image + 30 KB stage -> three workgroups per CU.
+// records per stage chunk: 30 KB, three workgroups per CU (r05_v21: the unfused accumulate 91.2 -> 88.3 us,
+// grid_bw by events 0.239 -> 0.2366 ms; with the Adam fused 142.9 vs 142.5 us; 2560 records: slower)
+constexpr int ACC_RB = 3840;
 struct AccumStage {
     unsigned long long img[MAX_BIN_ENTRIES];
     uint2 recs[ACC_RB];
@@ -1445,7 +1447,7 @@ union AccumShared {  // ONE __shared__ object (a second one beside an LDS-DMA st
     AccumStage a;
     TableRegions tr;
 };
-static_assert(sizeof(AccumShared) <= 81920, "at least two accumulate workgroups per CU");
+static_assert(sizeof(AccumShared) <= 163840 / 3, "three accumulate workgroups per CU");
 
 __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, int64_t n,
                                                                 const int32_t* __restrict__ n_dev,
