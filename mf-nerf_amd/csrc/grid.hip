@@ -138,47 +138,66 @@ __device__ __forceinline__ int level_group(int l) {
     return q < 8 ? q : 15 - q;
 }
 
-// one (sample, level) of the planar forward
-__device__ __forceinline__ void planar_level(const mfnerf_grid_desc& D, const __half2* __restrict__ table,
-                                             __half2* __restrict__ out, int64_t plane_stride, int64_t i, int l,
-                                             float x, float y, float z) {
-    const LevelGeo L = level_geo(D.scale[l], x, y, z);
-    const __half2* tab = table + D.offset[l];
+// One (sample, level) of the planar forward in two phases: the gathers (issued for both of the
+// lane's levels before any is used) and the interpolation.  Per (y,z) row every lane loads the 8 B
+// holding its x-corner -- at idx (dense levels: idx+1 is the x+1 corner unless the index wraps) or
+// at idx & ~1 (hashed power-of-two levels: the x+1 corner is idx ^ 1 when x is even), clamped into
+// the table -- and loads the x+1 corner singly only where those 8 B miss it, so most rows cost one
+// gather lane instead of two (the kernel is bound by per-lane gather addresses).  No branch chooses
+// a load shape: round 4 did, per row, and used the row's values inside the branch, so each row's
+// gather was waited for before the next one issued -- 8 dependent L2 round trips per lane and
+// sample, 0.05 VMEM instructions in flight per wave (PMC r05_v22); and any merge of two shapes'
+// results into one register (the compiler's phi copies) waits for the pending load as well.
+struct PlanarGather {
+    LevelGeo L;
+    uint2 u[4];      // row yz: the 8 B holding the x-corner's half2
+    uint32_t s[4];   // the x+1 corner's half2 where u misses it
+    uint32_t f;      // row yz, bits 3 yz + {0: x-corner is u.y, 1: x+1 corner is in u, 2: ... as u.y}
+};
+
+__device__ __forceinline__ PlanarGather planar_gather(const mfnerf_grid_desc& D, const __half2* __restrict__ table,
+                                                      int l, float x, float y, float z) {
+    PlanarGather G;
+    G.L = level_geo(D.scale[l], x, y, z);
+    const uint32_t* __restrict__ tab = reinterpret_cast<const uint32_t*>(table + D.offset[l]);
     const uint32_t size = D.size[l], res = D.res[l];
     const bool dense = D.table_kind[l] == 0 && (uint64_t)res * res * res <= size;
-    const bool pow2 = (size & (size - 1)) == 0;
-    __half2 v[8];
-    // The two x-corners of a (y,z) row are adjacent entries -- dense levels: idx+1 (one
-    // unaligned 8-B load unless it wraps past the table end); hashed power-of-two levels
-    // with even x: idx^1 (one aligned 8-B load) -- so each row costs one gather lane
-    // instead of two (the kernel is bound by per-lane gather addresses).
+    G.f = 0u;
 #pragma unroll
     for (int yz = 0; yz < 4; ++yz) {
-        const uint32_t gy = L.g[1] + (yz & 1), gz = L.g[2] + (yz >> 1);
-        const uint32_t i0 = corner_index(D, l, L.g[0], gy, gz);
-        if (dense && i0 + 1 < size) {
-            const uint2 u = *reinterpret_cast<const uint2*>(tab + i0);
-            v[2 * yz] = *reinterpret_cast<const __half2*>(&u.x);
-            v[2 * yz + 1] = *reinterpret_cast<const __half2*>(&u.y);
-        } else if (!dense && pow2 && D.table_kind[l] == 0 && (L.g[0] & 1) == 0) {
-            const uint2 u = *reinterpret_cast<const uint2*>(tab + (i0 & ~1u));
-            const bool lo = (i0 & 1) == 0;
-            v[2 * yz] = *reinterpret_cast<const __half2*>(lo ? &u.x : &u.y);
-            v[2 * yz + 1] = *reinterpret_cast<const __half2*>(lo ? &u.y : &u.x);
-        } else {
-            v[2 * yz] = tab[i0];
-            v[2 * yz + 1] = tab[corner_index(D, l, L.g[0] + 1, gy, gz)];
-        }
+        const uint32_t gy = G.L.g[1] + (yz & 1), gz = G.L.g[2] + (yz >> 1);
+        const uint32_t i0 = corner_index(D, l, G.L.g[0], gy, gz);
+        const uint32_t i1 = corner_index(D, l, G.L.g[0] + 1, gy, gz);
+        const uint32_t a = min(dense ? i0 : (i0 & ~1u), size - 2u);  // i0 is a or a + 1
+        G.u[yz] = *reinterpret_cast<const uint2*>(tab + a);
+        const bool in_u = i1 - a < 2u;
+        G.s[yz] = 0u;
+        if (!in_u) G.s[yz] = tab[i1];
+        G.f |= ((i0 != a ? 1u : 0u) | (in_u ? 2u : 0u) | (i1 != a ? 4u : 0u)) << (3 * yz);
     }
+    return G;
+}
+
+__device__ __forceinline__ __half2 planar_interp(const PlanarGather& G) {
     float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const float w = corner_weight(L, c);
-        const float2 f = __half22float2(v[c]);
-        a0 = fmaf(w, f.x, a0);
-        a1 = fmaf(w, f.y, a1);
+    for (int yz = 0; yz < 4; ++yz) {
+        // integer masks, not selects, on the loaded words (a select between two of the struct's
+        // loaded values may become a load from a selected address, the struct then in scratch)
+        const uint32_t f = G.f >> (3 * yz);
+        const uint32_t m0 = 0u - (f & 1u), m1 = 0u - ((f >> 1) & 1u), m2 = 0u - ((f >> 2) & 1u);
+        const uint32_t lo = (G.u[yz].x & ~m0) | (G.u[yz].y & m0);
+        const uint32_t hu = (G.u[yz].x & ~m2) | (G.u[yz].y & m2);
+        const uint32_t hi = (hu & m1) | (G.s[yz] & ~m1);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const float w = corner_weight(G.L, 2 * yz + c);
+            const float2 v = __half22float2(__builtin_bit_cast(__half2, c ? hi : lo));
+            a0 = fmaf(w, v.x, a0);
+            a1 = fmaf(w, v.y, a1);
+        }
     }
-    out[(int64_t)l * plane_stride + i] = __floats2half2_rn(a0, a1);
+    return __floats2half2_rn(a0, a1);
 }
 
 __global__ __launch_bounds__(ENC_BLOCK) void grid_fw_planar_kernel(const float* __restrict__ X, int64_t n,
@@ -194,11 +213,15 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_fw_planar_kernel(const float* 
         const float x = (X[3 * i] - x_min) / x_range;
         const float y = (X[3 * i + 1] - x_min) / x_range;
         const float z = (X[3 * i + 2] - x_min) / x_range;
-        // this group's levels, visited directly: 16m + grp and 16m + 15 - grp
-        for (int j = 0; j < nj; ++j) {
-            const int l = 16 * (j >> 1) + ((j & 1) ? 15 - grp : grp);
-            if (l >= D.n_levels) continue;
-            planar_level(D, table, out, plane_stride, i, l, x, y, z);
+        // this group's levels, visited directly: 16m + grp and 16m + 15 - grp (la < lb)
+        for (int j = 0; j < nj; j += 2) {
+            const int la = 16 * (j >> 1) + grp, lb = 16 * (j >> 1) + 15 - grp;
+            if (la >= D.n_levels) continue;
+            const bool has_b = lb < D.n_levels;  // (else level la is gathered twice, stored once)
+            const PlanarGather Ga = planar_gather(D, table, la, x, y, z);
+            const PlanarGather Gb = planar_gather(D, table, has_b ? lb : la, x, y, z);
+            out[(int64_t)la * plane_stride + i] = planar_interp(Ga);
+            if (has_b) out[(int64_t)lb * plane_stride + i] = planar_interp(Gb);
         }
     }
 }
