@@ -1345,7 +1345,9 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
     for (int64_t base = 0; base < m; base += (int64_t)SPT * TH) {
         if constexpr (PAIR && MAXB <= 10) {
             // the level loop written out: j a constant in every copy, so the staged pair is a plain
-            // register (sample_level's select costs 2 MAXB v_cndmask per sample and level)
+            // register (sample_level's select costs 2 MAXB v_cndmask per sample and level).  The
+            // single-record layout (MixedFeature) written out the same way: 331 vs 325 us, code
+            // 91 vs 24 KB (r05_v25)
             auto count_c = [&](int jn, int cp) __attribute__((always_inline)) {
                 auto each = [&](auto jc) __attribute__((always_inline)) {
                     constexpr int jj = decltype(jc)::value;
