@@ -913,10 +913,14 @@ __device__ __forceinline__ int bin_table(const BinPlan& P, int b) {
 // rounded to fp16 at every add) and
 //   w0 = e0 (bits 0-10, entry in the bin) | t << 11 (4 bits) | single << 15 | sel << 16 | fx << 17,
 // fx = the x weight as 15-bit unorm (exact for the fine levels, whose positions carry <= 13
-// fraction bits).  A pair record adds (1-fx)(a,b) to e0 and fx(a,b) to e1 = e0 ^ (2^(t+1) - 1): an
-// own power-of-two hash table has idx(x+1) = idx(x) ^ (x ^ (x+1)), t = trailing ones of x, and the
-// two share a bin unless the carry reaches bit `shift` (1 x in 2^shift).  Otherwise (shared
-// MixedFeature tables, straddles) each entry gets a single record with weight sel ? fx : 1-fx.
+// fraction bits).  A pair record adds (1-fx)(a,b) to e0 and fx(a,b) to e1 = e0 ^ ((2^(t+1) - 1) << s),
+// s = bit 16 (sel has no meaning in a pair record): an own power-of-two hash table has idx(x+1) =
+// idx(x) ^ (x ^ (x+1)), t = trailing ones of x, s = 0, and the two share a bin unless the carry
+// reaches bit `shift` (1 x in 2^shift).  A shared MixedFeature table hashes the canonical coordinates
+// c(x): where c(x+1) = c(x) + 1 the same holds with t = trailing ones of c(x); where c(x+1) = c(x) + 2
+// (the levels one or two steps below the canonical resolution), c ^ (c + 2) = (c' ^ (c' + 1)) << 1 for
+// c' = c >> 1: t = trailing ones of c', s = 1 (round 5).  Otherwise (larger steps, straddles, other
+// tables) each entry gets a single record with weight sel ? fx : 1-fx.
 // a record's two values: fp16 of v * 2^-15, round to nearest even (v in the table's int32 units)
 constexpr float REC_DOWN = 1.0f / 32768.0f, REC_UP = 32768.0f;
 typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
@@ -938,8 +942,19 @@ __device__ __forceinline__ void level_records_geo(const mfnerf_grid_desc& D, con
     const int t = P.table_of[l];
     const int bin0 = P.t_bin0[t];
     const uint32_t fxq = min(32767u, (uint32_t)rintf(Lg.w[0] * 32768.0f)) << 17;
-    const uint32_t ones = (uint32_t)__builtin_ctz(~Lg.g[0]);  // trailing ones of x
-    const bool pair_hash = P.pairable[l] && ones < 15;
+    uint32_t ones = (uint32_t)__builtin_ctz(~Lg.g[0]);  // trailing ones of x
+    uint32_t pflags = 0u;                               // s << 16
+    bool pair_hash = P.pairable[l] && ones < 15;
+    if (D.table_kind[l] == 1 && (D.size[l] & (D.size[l] - 1)) == 0) {
+        // a shared MixedFeature table: the x-pair's canonical step (corner_index's canon_coord)
+        const uint32_t rc = (uint32_t)D.canon_res, res = D.res[l];
+        const float inv = 1.0f / (float)res;
+        const uint32_t c0 = canon_coord(Lg.g[0], rc, res, inv), c1 = canon_coord(Lg.g[0] + 1, rc, res, inv);
+        const uint32_t cs = c1 - c0 == 2u ? c0 >> 1 : c0;
+        ones = (uint32_t)__builtin_ctz(~cs);
+        pflags = c1 - c0 == 2u ? 1u << 16 : 0u;
+        pair_hash = (c1 - c0 == 1u || c1 - c0 == 2u) && ones < 15;
+    }
     const float s0 = g0 * fs, s1 = g1 * fs;  // in the table's int32 fixed-point units
     const uint32_t mask = (1u << P.shift) - 1;
 #pragma unroll
@@ -955,7 +970,7 @@ __device__ __forceinline__ void level_records_geo(const mfnerf_grid_desc& D, con
         // static record slots 2 yz, 2 yz + 1, both always emitted (bin -1: no record), so the
         // caller's per-slot register arrays see constant indices on every path and stay registers
         const bool pair = pair_hash && b0 == b1;
-        emit(2 * yz, b0, make_uint2((i0 & mask) | (pair ? (ones << 11) : (1u << 15)) | fxq, ab));
+        emit(2 * yz, b0, make_uint2((i0 & mask) | (pair ? (ones << 11) | pflags : (1u << 15)) | fxq, ab));
         emit(2 * yz + 1, pair ? -1 : b1, make_uint2((i1 & mask) | (1u << 15) | (1u << 16) | fxq, ab));
     }
 }
@@ -1127,7 +1142,7 @@ __device__ __forceinline__ void overflow_add(const BinPlan& P, int* __restrict__
         add(e0, (w & (1u << 16)) ? fx : 1.0f - fx);
     } else {
         add(e0, 1.0f - fx);
-        add(e0 ^ ((2 << ((w >> 11) & 15)) - 1), fx);
+        add(e0 ^ (((2 << ((w >> 11) & 15)) - 1) << ((w >> 16) & 1)), fx);
     }
 }
 
@@ -1425,7 +1440,7 @@ __device__ __forceinline__ void accum_record(unsigned long long* img, int mask, 
         const float wt = (w & (1u << 16)) ? fx : 1.0f - fx;
         atomicAdd(&img[e0], pack2(wt * a, wt * b));
     } else {
-        const int e1 = e0 ^ ((2 << ((w >> 11) & 15)) - 1);
+        const int e1 = e0 ^ (((2 << ((w >> 11) & 15)) - 1) << ((w >> 16) & 1));
         const float w0 = 1.0f - fx;
         atomicAdd(&img[e0], pack2(w0 * a, w0 * b));
         atomicAdd(&img[e1], pack2(fx * a, fx * b));
