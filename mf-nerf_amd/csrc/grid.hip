@@ -882,7 +882,8 @@ int check_desc(const mfnerf_grid_desc* d, const char* what) {
 constexpr int MIN_BIN_SHIFT = 8, MAX_BIN_SHIFT = 11, MAX_BIN_ENTRIES = 1 << MAX_BIN_SHIFT;
 // partitions over all binned tables: the first LDS_CURSOR keep the scatter unit's running counts in
 // LDS, the rest (own tables of 2^20-2^21 entries: --T 20/21, opt.py:78) in the unit's column of the
-// slot counts in global memory, read and written by the one scanning wave
+// slot counts in global memory, read and written by the one scanning wave (LDS for all 5120 of the
+// T 2^20 layout measured the same: 0.654 vs 0.654 ms/step, r05_v27)
 constexpr int LDS_CURSOR = 4096, MAX_BINS = 16384;
 
 struct BinPlan {
