@@ -15,8 +15,11 @@ namespace {
 // gate = {signals, waits}: the chain adds a signal; a wait takes the next ticket and waits for the
 // matching signal, then catches up with signals nobody waited for (a chain replayed without a
 // gated march), so a desynchronised pair heals after one early start
+// Relaxed atomics throughout (placement only, no data is handed over): an agent-scope release writes
+// the XCD's dirty L2 lines back and an acquire invalidates its L2 (one L2 per XCD) -- the polling
+// loop's acquire did that every ~0.2 us on one XCD for the whole chain (round 5)
 __global__ void gate_signal_kernel(int32_t* gate) {
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(gate, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(gate, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void gate_wait_kernel(int32_t* gate, int64_t timeout_ticks, int lane_mask) {
@@ -25,10 +28,10 @@ __global__ void gate_wait_kernel(int32_t* gate, int64_t timeout_ticks, int lane_
     int32_t* sig = gate + (threadIdx.x & lane_mask);
     const int target = __hip_atomic_fetch_add(gate + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
     const uint64_t t0 = wall_clock64();  // constant-rate clock (100 MHz on gfx9)
-    int c = __hip_atomic_load(sig, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    int c = __hip_atomic_load(sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     while (c < target && (int64_t)(wall_clock64() - t0) < timeout_ticks) {
         __builtin_amdgcn_s_sleep(8);
-        c = __hip_atomic_load(sig, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        c = __hip_atomic_load(sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (c > target) __hip_atomic_fetch_max(gate + 1, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

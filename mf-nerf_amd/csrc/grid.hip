@@ -434,8 +434,8 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_dense_kernel(const float* _
     // gate (gate.hip's {signals, waits, ticket}): opened as the table-gradient launches begin, so the
     // side stream's next march starts beside them with no one-thread signal kernel of its own on
     // the step's critical path
-    if (gate && blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_fetch_add(gate, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (gate && blockIdx.x == 0 && threadIdx.x == 0)  // relaxed: placement only (gate.hip)
+        __hip_atomic_fetch_add(gate, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __shared__ float fs_s[MFN_MAX_LEVELS];
     // per wave, one entry per run: the 4 rows' (x0, x1) keys and the inclusive prefix at the run's
     // tail of the 16 values as 4 int4 (row r: x0f0, x0f1, x1f0, x1f1).  The runs tile the chunk's
