@@ -1552,7 +1552,14 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
 #pragma unroll
         for (int k = 0; k < IT; ++k) {
             const int i = tid + k * ACC_THREADS;
-            if (i < n_e) { p[k] = pp[i]; m[k] = mm[i]; v[k] = vv[i]; }
+            if (i < n_e) {  // streamed once per step: non-temporal (the partition's records keep the caches)
+                const float2v a = __builtin_nontemporal_load(reinterpret_cast<const float2v*>(pp + i));
+                const float2v b = __builtin_nontemporal_load(reinterpret_cast<const float2v*>(mm + i));
+                const float2v c = __builtin_nontemporal_load(reinterpret_cast<const float2v*>(vv + i));
+                p[k] = make_float2(a.x, a.y);
+                m[k] = make_float2(b.x, b.y);
+                v[k] = make_float2(c.x, c.y);
+            }
         }
     }
     for (int i = tid; i < n_ent; i += ACC_THREADS) img[i] = 0;
@@ -1678,9 +1685,9 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
             const float g0 = (float)((lo + rd) >> kb) * is, g1 = (float)((hi + rd) >> kb) * is;
             mfn::adam_elem(p[k].x, m[k].x, v[k].x, g0, A.beta1, A.beta2, A.eps, lr, bc1, bc2);
             mfn::adam_elem(p[k].y, m[k].y, v[k].y, g1, A.beta1, A.beta2, A.eps, lr, bc1, bc2);
-            pp[i] = p[k];
-            mm[i] = m[k];
-            vv[i] = v[k];
+            __builtin_nontemporal_store(float2v{p[k].x, p[k].y}, reinterpret_cast<float2v*>(pp + i));
+            __builtin_nontemporal_store(float2v{m[k].x, m[k].y}, reinterpret_cast<float2v*>(mm + i));
+            __builtin_nontemporal_store(float2v{v[k].x, v[k].y}, reinterpret_cast<float2v*>(vv + i));
             if (A.p16) hh[i] = __floats2half2_rn(p[k].x, p[k].y);
         }
         return;
