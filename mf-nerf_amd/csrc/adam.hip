@@ -33,16 +33,16 @@ __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ g, float*
         const float bc1 = 1.0f - powf(b1, (float)st);
         const float bc2 = 1.0f - powf(b2, (float)st);
         for (int64_t i = t0; i < n4; i += stride) {
-            float4 pp = reinterpret_cast<float4*>(p)[i];
+            float4 pp = mfn::nt_load4(p + 4 * i);
             const float4 gg = reinterpret_cast<const float4*>(g)[i];
-            float4 mm = reinterpret_cast<float4*>(m)[i];
-            float4 vv = reinterpret_cast<float4*>(v)[i];
+            float4 mm = mfn::nt_load4(m + 4 * i);
+            float4 vv = mfn::nt_load4(v + 4 * i);
             float* pa = &pp.x; const float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
 #pragma unroll
             for (int k = 0; k < 4; ++k) mfn::adam_elem(pa[k], ma[k], va[k], ga[k] * gscale, b1, b2, eps, lr, bc1, bc2);
-            reinterpret_cast<float4*>(p)[i] = pp;
-            reinterpret_cast<float4*>(m)[i] = mm;
-            reinterpret_cast<float4*>(v)[i] = vv;
+            mfn::nt_store4(p + 4 * i, pp);
+            mfn::nt_store4(m + 4 * i, mm);
+            mfn::nt_store4(v + 4 * i, vv);
             if (zero_grads) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (p16) {
                 __half2 a = __floats2half2_rn(pp.x, pp.y), b = __floats2half2_rn(pp.z, pp.w);

@@ -90,6 +90,16 @@ __host__ __device__ __forceinline__ T div_up(T a, T b) { return (a + b - 1) / b;
 
 // One Adam update (apex multi_tensor_adam ADAM_MODE, weight decay 0: m/(1-b1^t), v/(1-b2^t),
 // p -= lr*m_hat/(sqrt(v_hat)+eps)); g already scaled.  bc1/bc2 = 1 - beta^t.
+// a float4 streamed once (optimizer state): non-temporal, so it does not evict the working sets
+typedef float mfn_f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 nt_load4(const float* p) {
+    const mfn_f4v x = __builtin_nontemporal_load(reinterpret_cast<const mfn_f4v*>(p));
+    return make_float4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ void nt_store4(float* p, float4 v) {
+    __builtin_nontemporal_store(mfn_f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<mfn_f4v*>(p));
+}
+
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float b1, float b2, float eps,
                                           float lr, float bc1, float bc2) {
     m = b1 * m + (1.0f - b1) * g;

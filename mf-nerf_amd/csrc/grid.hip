@@ -761,16 +761,16 @@ __device__ __forceinline__ void adam_fixed_body(float* __restrict__ p, float* __
         }
         reinterpret_cast<float4*>(g)[i4] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (skipped) continue;
-        float4 pp = reinterpret_cast<float4*>(p)[i4];
-        float4 mm = reinterpret_cast<float4*>(m)[i4];
-        float4 vv = reinterpret_cast<float4*>(v)[i4];
+        float4 pp = mfn::nt_load4(p + 4 * i4);
+        float4 mm = mfn::nt_load4(m + 4 * i4);
+        float4 vv = mfn::nt_load4(v + 4 * i4);
         mfn::adam_elem(pp.x, mm.x, vv.x, gg.x, b1, b2, eps, lr, bc1, bc2);
         mfn::adam_elem(pp.y, mm.y, vv.y, gg.y, b1, b2, eps, lr, bc1, bc2);
         mfn::adam_elem(pp.z, mm.z, vv.z, gg.z, b1, b2, eps, lr, bc1, bc2);
         mfn::adam_elem(pp.w, mm.w, vv.w, gg.w, b1, b2, eps, lr, bc1, bc2);
-        reinterpret_cast<float4*>(p)[i4] = pp;
-        reinterpret_cast<float4*>(m)[i4] = mm;
-        reinterpret_cast<float4*>(v)[i4] = vv;
+        mfn::nt_store4(p + 4 * i4, pp);
+        mfn::nt_store4(m + 4 * i4, mm);
+        mfn::nt_store4(v + 4 * i4, vv);
         if (p16) {
             __half2 a = __floats2half2_rn(pp.x, pp.y), b = __floats2half2_rn(pp.z, pp.w);
             uint2 u; u.x = *reinterpret_cast<uint32_t*>(&a); u.y = *reinterpret_cast<uint32_t*>(&b);
