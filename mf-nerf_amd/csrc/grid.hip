@@ -1624,7 +1624,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
             for (int q = lo; q < hi; q += 128) {
                 const int k = q + 2 * lane;  // records k, k + 1 of the compacted partition (k even)
                 if (k < hi)
-                    __builtin_amdgcn_global_load_lds(src + ((k - r0) >> 1), &S.a.recs[q - c0], 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds(src + ((k - r0) >> 1), &S.a.recs[q - c0], 16, 0, 2);  // nt: read once
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
