@@ -8,13 +8,18 @@ a preceding eager pass gives the per-kernel breakdown (eager_stage_ms).  The occ
 refresh (every 16 steps in the reference) is excluded from the timed step as SURVEY.md 8d
 prescribes and reported separately (density_update_ms, value_with_occupancy_refresh).
 
-python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run (one rank per
-GPU, rank-distinct rays, one flat fp32 gradient all-reduce per step over RCCL).
+python bench.py [--gpus N --steps K --warmup W]; N>1 runs one rank per GPU (rank-distinct rays,
+reduce-scatter of the flat fp32 gradient + sharded Adam + fp16 all-gather per step over RCCL):
+either under an outer torch.distributed.run (the driver's launch; WORLD_SIZE must equal N) or, when
+started directly, by starting torch.distributed.run itself as a CHILD process before any HIP call
+(launch_ranks) and passing rank 0's one JSON line through.
 """
 import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -53,7 +58,7 @@ PRESETS = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -75,7 +80,48 @@ def parse():
     ap.add_argument("--dp-rehearse", action="store_true",
                     help="N=1: run the N>1 step anyway (a one-rank RCCL group, --dp mode) -- the data-parallel "
                          "path's cost over the single-GPU step with the collectives reduced to a local copy")
-    return ap.parse_args()
+    ap.add_argument("--stub-step", action="store_true",
+                    help="launcher test only: the rank plumbing, timing and JSON line of a real run around a "
+                         "host-only stub step over gloo (no GPU is touched; tests/test_bench_launcher.py)")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` (N > 1) started without an outer launcher: run N ranks under
+    torch.distributed.run (the driver's own command line: one node, 127.0.0.1) as a CHILD process --
+    this process has made no HIP call, and it is never replaced (no exec) -- and pass through exactly
+    one JSON line, rank 0's.  Everything else the child writes to stdout goes to stderr.  Returns the
+    child's exit status (non-zero as well when the child did not print exactly one line)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC, which RCCL needs on this host driver
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    lines = []
+    for line in proc.stdout:
+        try:
+            rec = json.loads(line)
+        except ValueError:
+            rec = None
+        if isinstance(rec, dict) and "metric" in rec:
+            lines.append(line.strip())
+        else:
+            sys.stderr.write(line)
+    rc = proc.wait()
+    if len(lines) == 1:
+        print(lines[0], flush=True)
+    elif rc == 0:
+        sys.stderr.write(f"bench.py: expected one JSON line from rank 0, got {len(lines)}\n")
+        rc = 1
+    return rc
 
 
 def _marker(ev):
@@ -144,9 +190,10 @@ def stage_times(events, steps):
 
 
 # ---------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(n_rays, log2_T, seconds, grid="Hash", n_tables=1, width=64, lr=1e-2):
+def cpu_baseline(n_rays, log2_T, seconds, grid="Hash", n_tables=1, width=64, lr=1e-2, min_timed=2):
     """The reference's hot path restated on the host (oracle/): C march + compositing, fp32 torch
-    grid encoding + MLPs with autograd, fused loss, Adam.  Timed on a bounded sample."""
+    grid encoding + MLPs with autograd, fused loss, Adam.  Timed on a bounded sample: one untimed
+    step, then steps until `seconds` have passed and at least `min_timed` were timed."""
     from mfnerf import synthetic
     from oracle import field_oracle as FO
     from oracle import vren_oracle as O
@@ -193,7 +240,7 @@ def cpu_baseline(n_rays, log2_T, seconds, grid="Hash", n_tables=1, width=64, lr=
         torch.autograd.backward([sigma, rgbs], [dsig, drgb])
         opt.step()
         steps += 1
-        if t0 is not None and time.time() - t0 >= seconds and steps >= 3:
+        if t0 is not None and time.time() - t0 >= seconds and steps - 1 >= min_timed:
             break
     el = time.time() - t0
     return {"value": round(n_rays * (steps - 1) / el, 2), "unit": "rays/s", "cores": torch.get_num_threads(),
@@ -203,17 +250,95 @@ def cpu_baseline(n_rays, log2_T, seconds, grid="Hash", n_tables=1, width=64, lr=
                       f" fp32 torch-CPU field + C oracle march/compositing ({el:.1f} s)"}
 
 
-def main():
-    args = parse()
+def line_base(args, pre, world, elapsed, mean_samples, dp_on=False):
+    """The driver-contract fields of the JSON line (value = rays of ALL ranks / slowest rank's time)."""
+    rays_total = args.n_rays * args.steps * world
+    return {
+        "metric": "training rays/sec + test PSNR, Synthetic-NeRF Lego 30k steps" if args.preset == "lego"
+                  else "training rays/sec, Synthetic-NeRF MixedFeature rgb-128 (BASELINE config 3 field)",
+        "value": round(rays_total / elapsed, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f16-mfma/f32",
+        "data": "synthetic: 100 analytic 800x800 views of a 12-ball scene (Lego intrinsics), batch drawn on "
+                "the device every step; ball-union occupancy (no dataset in the image)",
+        "config": {"workload": "%s training step, %d rays/batch/GPU, %s L16 F2 T2^%d%s, rgb %dx2"
+                   % ("Lego 800x800" if args.preset == "lego" else "Synthetic-NeRF (MF benchmark field)",
+                      args.n_rays, pre["grid"], args.log2_T,
+                      " %d tables" % pre["N_tables"] if pre["grid"] == "MixedFeature" else "", pre["rgb_width"]),
+                   "preset": args.preset, "global_batch": args.n_rays * world,
+                   "rm_s": round(mean_samples / args.n_rays, 2),
+                   "parallelism": f"dp{world}" + ("-sharded-adam" if dp_on and args.dp == "shard" else "")
+                   + ("-rehearsal" if args.dp_rehearse and world == 1 else ""),
+                   "psnr": None},
+    }
+
+
+def resolve_preset(args):
+    pre = dict(PRESETS[args.preset])
+    if args.n_rays is not None:
+        pre["n_rays"] = args.n_rays
+    if args.log2_T is not None:
+        pre["log2_T"] = args.log2_T
+    args.n_rays, args.log2_T = pre["n_rays"], pre["log2_T"]
+    return pre
+
+
+def stub_main(args, world, rank, out_fd):
+    """--stub-step: the N-rank plumbing of main() (process group, barrier-bracketed timed region,
+    max over ranks, rank 0's single line) around a host-only stand-in step, over gloo, so that the
+    launcher is testable without a GPU.  Its line says data "stub"; it is never a measurement."""
+    import torch.distributed as dist
+    pre = resolve_preset(args)
+    if world > 1:
+        dist.init_process_group("gloo", world_size=world, rank=rank)
+    x = torch.ones(1 << 12)
+    for _ in range(args.warmup):
+        x.mul_(1.0)
+    if world > 1:
+        dist.barrier()
+    t0 = time.time()
+    for _ in range(args.steps):
+        x.mul_(1.0)
+        if world > 1:
+            dist.all_reduce(x)
+            x.div_(world)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.time() - t0
+    if world > 1:
+        t = torch.tensor([elapsed])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    if rank == 0:
+        out = line_base(args, pre, world, max(elapsed, 1e-9), 0.0, dp_on=world > 1)
+        out["data"] = "stub (launcher test: no GPU step ran)"
+        with os.fdopen(out_fd, "w") as f:
+            f.write(json.dumps(out) + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # N ranks requested without an outer launcher: start one (a child process, no HIP call yet)
+        return launch_ranks(args.gpus, sys.argv[1:] if argv is None else argv)
+    world = int(env_world or "1")
+    if world != args.gpus:
+        sys.stderr.write(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: the line would mislabel the run\n")
+        return 2
     # the driver reads ONE JSON line from stdout: everything else the process prints there (RCCL's
     # version banner at communicator init, library chatter) goes to stderr; the line itself is
     # written to the original stdout
     out_fd = os.dup(1)
     os.dup2(2, 1)
     sys.stdout = os.fdopen(os.dup(2), "w")
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.stub_step:
+        stub_main(args, world, rank, out_fd)
+        return 0
     dp_on = world > 1 or args.dp_rehearse
     if dp_on:
         torch.cuda.set_device(local)
@@ -232,12 +357,7 @@ def main():
     want_direct = os.environ.get("MFNERF_DIRECT_RCCL", "1" if world == 1 else "0") == "1"
     direct = dp_on and want_direct and dp.use_direct_rccl()
 
-    pre = dict(PRESETS[args.preset])
-    if args.n_rays is not None:
-        pre["n_rays"] = args.n_rays
-    if args.log2_T is not None:
-        pre["log2_T"] = args.log2_T
-    args.n_rays, args.log2_T = pre["n_rays"], pre["log2_T"]
+    pre = resolve_preset(args)
     cfg = engine.StepConfig(n_parts=args.parts, **pre)
     step = engine.TrainStep(cfg, device=dev, seed=0)  # identical init on every rank
     if dp_on and args.dp == "shard":
@@ -322,7 +442,6 @@ def main():
     # one batch is marched per timed step (the graphs march the next step's batch)
     mean_samples = (int(step.samples_marched) - marched0) / args.steps
     rays_total = args.n_rays * args.steps * world
-    value = rays_total / elapsed
 
     # roofline: grid_bw (the dominant kernel), timed by events around it inside the timed region
     dom = "grid_bw"
@@ -340,26 +459,15 @@ def main():
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(256, args.log2_T, args.cpu_seconds, pre["grid"], pre["N_tables"], pre["rgb_width"],
-                               pre["lr"])
-        out = {
-            "metric": "training rays/sec + test PSNR, Synthetic-NeRF Lego 30k steps" if args.preset == "lego"
-                      else "training rays/sec, Synthetic-NeRF MixedFeature rgb-128 (BASELINE config 3 field)",
-            "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f16-mfma/f32",
-            "data": "synthetic: 100 analytic 800x800 views of a 12-ball scene (Lego intrinsics), batch drawn on "
-                    "the device every step; ball-union occupancy (no dataset in the image)",
-            "config": {"workload": "%s training step, %d rays/batch/GPU, %s L16 F2 T2^%d%s, rgb %dx2"
-                       % ("Lego 800x800" if args.preset == "lego" else "Synthetic-NeRF (MF benchmark field)",
-                          args.n_rays, pre["grid"], args.log2_T,
-                          " %d tables" % pre["N_tables"] if pre["grid"] == "MixedFeature" else "", pre["rgb_width"]),
-                       "preset": args.preset, "global_batch": args.n_rays * world, "rm_s": round(mean_samples / args.n_rays, 2),
-                       "parallelism": f"dp{world}" + ("-sharded-adam" if dp_on and args.dp == "shard" else "")
-                       + ("-rehearsal" if args.dp_rehearse and world == 1 else ""),
-                       "exchange": (None if not dp_on else "rccl-direct, one graph per step" if direct
-                                    else "torch.distributed between graphs"),
-                       "psnr": None},
+            # the host path on the bench's own batch (8192 rays x ~60 samples, fw+bw+Adam)
+            # and on config 1's 256-ray batch, each a bounded sample on the box's CPU share
+            hp = (pre["grid"], pre["N_tables"], pre["rgb_width"], pre["lr"])
+            cpu = cpu_baseline(args.n_rays, args.log2_T, args.cpu_seconds, *hp, min_timed=1)
+            cpu["other_batches"] = [cpu_baseline(256, args.log2_T, args.cpu_seconds / 2, *hp)]
+        out = line_base(args, pre, world, elapsed, mean_samples, dp_on)
+        out["config"]["exchange"] = (None if not dp_on else "rccl-direct, one graph per step" if direct
+                                     else "torch.distributed between graphs")
+        out.update({
             "roofline": {"bound": "hbm", "kernel": dom + " (" + "+".join(GRID_BW_KERNEL) + ")",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -370,12 +478,14 @@ def main():
                          "samples_per_launch": round(mean_samples), "atomic": atomic},
             "graph": use_graph, "host_issue_ms_per_step": round(host_s / args.steps * 1e3, 4),
             "grid_bw_ms": round(grid_bw_ms, 4),
+            # gated marches that gave up waiting (gate.hip): 0 unless a step stalled GATE_TIMEOUT_US
+            "gate_timeouts": step.gate_timeouts() if use_graph else None,
             "eager_stage_ms": {k: round(v, 4) for k, v in eager_stage_ms.items()},
             "density_update_ms": round(density_ms, 3),
             # the reference refreshes occupancy every 16 steps (train.py:62,165): rate with it amortised
             "value_with_occupancy_refresh": round(rays_total / (elapsed + args.steps / 16 * density_ms * 1e-3), 1),
             "cpu_baseline": cpu,
-        }
+        })
         with os.fdopen(out_fd, "w") as f:
             f.write(json.dumps(out) + "\n")
     if dp_on:
@@ -385,4 +495,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -547,9 +547,13 @@ int mfnerf_flag_from_shard(const float* g_shard, int32_t* flag, mfnerf_stream_t 
 
 /* A soft gate between two streams' captured graphs (no reference counterpart: it replaces the host
  * event the reference's PyTorch loop never needed, train.py:129-150 running one stream).  gate =
- * device int32[2], zeroed once.  mfnerf_gate_signal adds a signal; mfnerf_gate_wait (one thread)
- * waits for the signal matching its own ticket, at most timeout_us, then absorbs signals nobody
- * waited for.  Ordering only: data hazards must still be covered by stream events. */
+ * device int32[4] {signals, waits, -, timeouts}, zeroed once.  mfnerf_gate_signal adds a signal;
+ * mfnerf_gate_wait (one thread) waits for the signal matching its own ticket, at most timeout_us,
+ * then absorbs signals nobody waited for; a wait that gives up adds 1 to gate[3].
+ * NO MEMORY ORDERING: signal and wait are relaxed atomics (an agent-scope release / acquire would
+ * write back / invalidate the XCD's L2 on every poll), so the gate hands over no data -- a consumer
+ * may not read anything the signaller wrote.  Ordering only: data hazards must be covered by stream
+ * events, as the engine's are. */
 int mfnerf_gate_signal(int32_t* gate, mfnerf_stream_t stream);
 int mfnerf_gate_wait(int32_t* gate, int64_t timeout_us, mfnerf_stream_t stream);
 

@@ -12,7 +12,7 @@
 
 namespace {
 
-// gate = {signals, waits}: the chain adds a signal; a wait takes the next ticket and waits for the
+// gate = {signals, waits, -, timeouts}: the chain adds a signal; a wait takes the next ticket and waits for the
 // matching signal, then catches up with signals nobody waited for (a chain replayed without a
 // gated march), so a desynchronised pair heals after one early start
 // Relaxed atomics throughout (placement only, no data is handed over): an agent-scope release writes
@@ -34,6 +34,9 @@ __global__ void gate_wait_kernel(int32_t* gate, int64_t timeout_ticks, int lane_
         c = __hip_atomic_load(sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (c > target) __hip_atomic_fetch_max(gate + 1, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // gate[3] counts the waits that gave up (never reset here): the host reads it to tell a slow step
+    // from a gate that never opened (e.g. the side stream sharing a hardware queue with the signaller)
+    if (c < target) __hip_atomic_fetch_add(gate + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace

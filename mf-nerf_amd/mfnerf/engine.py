@@ -778,7 +778,7 @@ class TrainStep:
         # one part: the next step's march waits on the side stream for the gate the step graph opens
         # as its scatter begins (the dense-level launch's first workgroup, or a signal kernel)
         gated = P == 1
-        self._gate = torch.zeros(4, dtype=torch.int32, device=self.dev)  # {signals, waits, ticket, -}
+        self._gate = torch.zeros(4, dtype=torch.int32, device=self.dev)  # {signals, waits, -, timeouts}
         gp = ptr(self._gate) if gated else None
         self._gate_opened = 0
         if gated:
@@ -877,6 +877,13 @@ class TrainStep:
         self._ev_part = [torch.cuda.Event() for _ in range(P)]
         self._parity = 0
         self._primed = False
+
+    def gate_timeouts(self):
+        """Gated marches that started on the gate's timeout instead of its signal (gate.hip's gate[3],
+        cumulative; a host read, so it synchronises): non-zero means a step paid up to GATE_TIMEOUT_US
+        -- e.g. the side stream shares a hardware queue with the stream that signals."""
+        g = getattr(self, "_gate", None)
+        return 0 if g is None else int(g[3])
 
     def _fused_tail(self, j, gate=None):
         """The replayed collective-free tail: the scatter with every Adam update in its launches

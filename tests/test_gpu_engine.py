@@ -306,7 +306,8 @@ def test_gated_replay_with_distortion_loss_keeps_the_gate_in_step(gpu):
     torch.cuda.synchronize()
     # replays 1..K-2 ran as one gated graph (the last has no next batch); every signal waited for
     assert _gate_state(a) == (K - 2, K - 2)
-    assert t0.elapsed_time(t1) < (K - 1) * engine.GATE_TIMEOUT_US / 1000
+    assert a.gate_timeouts() == 0  # every gated march started on its signal (gate.hip's gate[3])
+    assert t0.elapsed_time(t1) < 4 * (K - 1) * engine.GATE_TIMEOUT_US / 1000  # (loose sanity bound)
     assert torch.equal(a.params, b.params) and torch.equal(a.p16, b.p16)
 
 
@@ -334,7 +335,8 @@ def test_gated_replay_opens_the_gate_on_every_tail(gpu, kw):
     t1.record()
     torch.cuda.synchronize()
     assert _gate_state(a) == (K - 2, K - 2)
-    assert t0.elapsed_time(t1) < (K - 1) * engine.GATE_TIMEOUT_US / 1000
+    assert a.gate_timeouts() == 0  # every gated march started on its signal (gate.hip's gate[3])
+    assert t0.elapsed_time(t1) < 4 * (K - 1) * engine.GATE_TIMEOUT_US / 1000  # (loose sanity bound)
     if kw.get("fixed_point_grid", True):
         assert torch.equal(a.params, b.params) and torch.equal(a.p16, b.p16) and torch.equal(a.m, b.m)
     else:  # (a near-zero table gradient's sign, hence its Adam step, can follow the summation order)
@@ -360,3 +362,18 @@ def test_large_tables_train_with_or_without_partitions(gpu, log2_T):
     lay = a.layout
     supported = load().mfnerf_grid_encode_bw_binned_workspace(a.desc, a._bin_slots()) >= 0
     assert supported and a._binned()
+
+
+def test_gate_wait_counts_a_timeout(gpu):
+    """A wait whose signal never comes gives up after timeout_us and adds 1 to gate[3]; a wait whose
+    signal came first adds nothing (the counter bench.py reports as gate_timeouts)."""
+    from mfnerf._lib import call, ptr, stream
+    g = torch.zeros(4, dtype=torch.int32, device=gpu)
+    call("mfnerf_gate_wait", ptr(g), 50, stream())  # no signal: times out after 50 us
+    torch.cuda.synchronize()
+    assert g.tolist() == [0, 1, 0, 1]
+    call("mfnerf_gate_signal", ptr(g), stream())
+    call("mfnerf_gate_signal", ptr(g), stream())
+    call("mfnerf_gate_wait", ptr(g), 2000, stream())  # ticket 2, signal 2 present: no wait
+    torch.cuda.synchronize()
+    assert g.tolist() == [2, 2, 0, 1]
