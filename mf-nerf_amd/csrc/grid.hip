@@ -885,6 +885,9 @@ constexpr int MIN_BIN_SHIFT = 8, MAX_BIN_SHIFT = 11, MAX_BIN_ENTRIES = 1 << MAX_
 // slot counts in global memory, read and written by the one scanning wave (LDS for all 5120 of the
 // T 2^20 layout measured the same: 0.654 vs 0.654 ms/step, r05_v27)
 constexpr int LDS_CURSOR = 4096, MAX_BINS = 16384;
+#ifndef MFN_MERGE_SINGLES
+#define MFN_MERGE_SINGLES 1
+#endif
 
 struct BinPlan {
     int n_binned;                    // levels routed through the bins
@@ -894,6 +897,7 @@ struct BinPlan {
     int pair_ok;                     // no x-pair can straddle two partitions (one record per row)
     int level[MFN_MAX_LEVELS];       // binned level list
     int pairable[MFN_MAX_LEVELS];    // per level: x+1's entry = x's entry ^ (x ^ (x+1)) (own power-of-two hash)
+    int merge[MFN_MAX_LEVELS];       // per level: never a pair record -> runs merged (merged_level_records)
     int table_of[MFN_MAX_LEVELS];    // per level: its table
     uint32_t t_offset[MFN_MAX_LEVELS], t_size[MFN_MAX_LEVELS];
     int t_bin0[MFN_MAX_LEVELS + 1];  // first bin of each table; t_bin0[n_tables] = n_bins
@@ -956,6 +960,10 @@ __device__ __forceinline__ void level_records_geo(const mfnerf_grid_desc& D, con
         pflags = c1 - c0 == 2u ? 1u << 16 : 0u;
         pair_hash = (c1 - c0 == 1u || c1 - c0 == 2u) && ones < 15;
     }
+    // the accumulate decodes e1 = e0 ^ (((2^(t+1) - 1) << s): valid only if that mask lies inside the
+    // table (corner_index masks both indices by size - 1; with a table of at most one partition, the
+    // same-partition test below would pass for a mask reaching past it -- ADVICE r5)
+    pair_hash = pair_hash && ((((2u << ones) - 1u) << (pflags >> 16)) < D.size[l]);
     const float s0 = g0 * fs, s1 = g1 * fs;  // in the table's int32 fixed-point units
     const uint32_t mask = (1u << P.shift) - 1;
 #pragma unroll
@@ -1010,12 +1018,101 @@ __device__ __forceinline__ void pair_level_records(const mfnerf_grid_desc& D, co
     }
 }
 
+// Runs of one cell inside a 16-lane DPP row (a 16-sample chunk: consecutive samples of a ray, the
+// scatter's lane order).  A dead lane (no gradient or no sample) is a run of its own.  suffix_sums
+// leaves each run's sums in its first lane: a segmented suffix sum over the row, 4 DPP steps, one
+// fixed order (every lane of the wave must call it).  keep[k]: 1 if the lane adds the values 2^k
+// lanes on at step k (its run goes on past them) -- the same for every value, so computed once.
+struct RunRow {
+    bool same_prev, same_next;
+    float keep[4];
+    __device__ __forceinline__ void suffix_sums(float* v) const {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[k] = fmaf(dpp_f<DPP_ROW_SHL(1)>(v[k]), keep[0], v[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = fmaf(dpp_f<DPP_ROW_SHL(2)>(v[k]), keep[1], v[k]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = fmaf(dpp_f<DPP_ROW_SHL(4)>(v[k]), keep[2], v[k]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = fmaf(dpp_f<DPP_ROW_SHL(8)>(v[k]), keep[3], v[k]);
+    }
+};
+__device__ __forceinline__ RunRow run_row(const LevelGeo& Lg, bool live) {
+    // every DPP read is unconditional and combined with non-short-circuit operators: a DPP inside a
+    // `&&` or `?:` runs under a narrowed EXEC, and a lane reading a disabled neighbour reads 0
+    RunRow r;
+    const int lr = (int)(threadIdx.x & 15);
+    const int k0 = live ? (int)Lg.g[0] : -1, k1 = live ? (int)Lg.g[1] : -1, k2 = live ? (int)Lg.g[2] : -1;
+    const int n0 = dpp_i<DPP_ROW_SHL(1)>(k0), n1 = dpp_i<DPP_ROW_SHL(1)>(k1), n2 = dpp_i<DPP_ROW_SHL(1)>(k2);
+    const int p0 = dpp_i<DPP_ROW_SHR(1)>(k0), p1 = dpp_i<DPP_ROW_SHR(1)>(k1), p2 = dpp_i<DPP_ROW_SHR(1)>(k2);
+    r.same_next = (lr < 15) & (n0 == k0) & (n1 == k1) & (n2 == k2);
+    r.same_prev = (lr > 0) & (p0 == k0) & (p1 == k1) & (p2 == k2);
+    int stop = r.same_next ? 0 : 1;  // this lane's run ends within the lanes summed so far
+    int t;
+    r.keep[0] = stop ? 0.0f : 1.0f;
+    t = dpp_i<DPP_ROW_SHL(1)>(stop);
+    stop |= t;
+    r.keep[1] = stop ? 0.0f : 1.0f;
+    t = dpp_i<DPP_ROW_SHL(2)>(stop);
+    stop |= t;
+    r.keep[2] = stop ? 0.0f : 1.0f;
+    t = dpp_i<DPP_ROW_SHL(4)>(stop);
+    stop |= t;
+    r.keep[3] = stop ? 0.0f : 1.0f;
+    return r;
+}
+
 template <typename EMIT>
 __device__ __forceinline__ void level_records(const mfnerf_grid_desc& D, const BinPlan& P, int j, float x, float y,
                                               float z, float g0, float g1, float fs, EMIT&& emit) {
     level_records_geo(D, P, j, level_geo(D.scale[P.level[j]], x, y, z), g0, g1, fs, emit);
 }
 
+// Round 6: the records of a level that never forms a pair record (BinPlan::merge: a MixedFeature
+// shared table whose canonical x-step is >= 3, an own table without the power-of-two hash), with the
+// samples of one run merged.  A 16-lane DPP row holds a 16-sample chunk -- consecutive samples of a
+// ray -- and at the coarse shared levels ~2-3 consecutive samples fall in one cell: same 8 corner
+// entries, other weights.  Per (y,z) row each lane computes its 4 weighted values ({x, x+1} x 2
+// features, the x weight applied: (1 - fx) wyz g and fx wyz g in table units), a segmented suffix
+// sum over the row (RunRow, 4 DPP steps, a fixed order) leaves each run's sums in its first lane,
+// and only that lane emits the run's 8 single records, weight 1 (fx = 0, sel = 0).  Every lane of
+// the wave must call it (DPP reads its row neighbours); `live` false: no gradient / no sample.
+// Measured (r6c, config 3's field): mf128 step 1.244 -> 1.204 ms, grid_bw 0.674 -> 0.637 ms.  The
+// same merge for the Lego layout's coarse PAIR levels (runs of >= 2 as two single-record halves
+// from the run's first two lanes) ran 0.5125 vs 0.4953 ms/step: with two samples per lane it
+// spilled (62 VGPRs) and its records saved less -- a run of two is two records either way.
+// The same entries and contributions as level_records_geo's singles; each value is now the run's
+// fp32 sum rounded once to fp16 (the 2^-11 record bound holds for the sum), and the x weight exact
+// instead of a 15-bit fx.
+template <typename EMIT>
+__device__ __forceinline__ void merged_level_records(const mfnerf_grid_desc& D, const BinPlan& P, int j, float x,
+                                                     float y, float z, float g0, float g1, float fs, bool live,
+                                                     EMIT&& emit) {
+    const int l = P.level[j];
+    const LevelGeo Lg = level_geo(D.scale[l], live ? x : 0.0f, live ? y : 0.0f, live ? z : 0.0f);
+    const RunRow rr = run_row(Lg, live);
+    const float s0 = live ? g0 * fs : 0.0f, s1 = live ? g1 * fs : 0.0f;  // table int32 units
+    const float wx1 = Lg.w[0], wx0 = 1.0f - wx1, wy1 = Lg.w[1], wy0 = 1.0f - wy1, wz1 = Lg.w[2], wz0 = 1.0f - wz1;
+    const bool head = live && !rr.same_prev;  // a run's first lane emits the run's records
+    const int bin0 = P.t_bin0[P.table_of[l]];
+    const uint32_t emask = (1u << P.shift) - 1u;
+#pragma unroll
+    for (int yz = 0; yz < 4; ++yz) {  // row by row: 4 values in flight
+        const float wyz = ((yz & 1) ? wy1 : wy0) * ((yz >> 1) ? wz1 : wz0);
+        const float a = wyz * s0, b = wyz * s1;
+        float v[4] = {wx0 * a, wx0 * b, wx1 * a, wx1 * b};
+        rr.suffix_sums(v);
+        if (head) {
+            const uint32_t gy = Lg.g[1] + (yz & 1), gz = Lg.g[2] + (yz >> 1);
+            const uint32_t i0 = corner_index(D, l, Lg.g[0], gy, gz);
+            const uint32_t i1 = corner_index(D, l, Lg.g[0] + 1, gy, gz);
+            emit(2 * yz, bin0 + (int)(i0 >> P.shift), make_uint2((i0 & emask) | (1u << 15), rec_values(v[0], v[1])));
+            emit(2 * yz + 1, bin0 + (int)(i1 >> P.shift), make_uint2((i1 & emask) | (1u << 15), rec_values(v[2], v[3])));
+        }
+    }
+}
 
 // A sample staged in registers for all its binned levels: normalised position and dL/dy of the
 // binned levels (contiguous), loaded once before the level loop -- a load inside the loop would
@@ -1237,7 +1334,6 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
 #pragma unroll
         for (int q = 0; q < SPT; ++q) {
             const SampleLevel Q = G(q);
-            if (!(live[q] && Q.live)) continue;
             // the record's |a|, |b| maxima as two packed u16 (fp16 bits order like the values)
             auto rank = [&](int k, int lb, uint2 r) {
                 R[k].r = r;
@@ -1245,6 +1341,14 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                 rmax2 = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(
                     __builtin_bit_cast(ushort2v, rmax2), __builtin_bit_cast(ushort2v, r.y & 0x7fff7fffu)));
             };
+            if constexpr (!PAIR) {
+                if (P.merge[P.level[j]]) {  // (uniform) every lane takes part: DPP over the row
+                    merged_level_records(D, P, j, S[q].x, S[q].y, S[q].z, Q.g0, Q.g1, fs_s[P.level[j]],
+                                         live[q] && Q.live, [&](int sl, int bin, uint2 r) { rank(sl, bin - b0, r); });
+                    continue;
+                }
+            }
+            if (!(live[q] && Q.live)) continue;
             if constexpr (PAIR) {
                 const int l = P.level[j];
                 const float fs = fs_s[l] * REC_DOWN;
@@ -1428,10 +1532,37 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
 // (sum over units of the unit's record count in the partition x the unit's largest |a|, |b|) * 2^k
 // <= 2^30 -- a bound on every entry's sum, from bin_scatter's counts and maxima -- so the int32
 // fields cannot overflow, and the stored table-unit value is rounded once per entry.
-__device__ __forceinline__ unsigned long long pack2(float a, float b) {
-    return ((unsigned long long)(uint32_t)(int)rintf(b) << 32) + (unsigned long long)(long long)(int)rintf(a);
-}
-__device__ __forceinline__ void accum_record(unsigned long long* img, int mask, uint2 r, float k2) {
+#ifndef MFN_ACC_PLANES
+#define MFN_ACC_PLANES 0
+#endif
+// The partition's LDS image: both features' int32 sums of an entry, as one packed 64-bit word
+// (f1 * 2^32 + f0, one ds_add_u64 per entry) or as two 32-bit planes (one ds_add_u32 per feature).
+// The same exact integer sums either way.
+struct AccImage {
+#if MFN_ACC_PLANES
+    int f0[MAX_BIN_ENTRIES], f1[MAX_BIN_ENTRIES];
+    __device__ __forceinline__ void add(int e, int q0, int q1) {
+        atomicAdd(&f0[e], q0);
+        atomicAdd(&f1[e], q1);
+    }
+    __device__ __forceinline__ int2 get(int i) const { return make_int2(f0[i], f1[i]); }
+    __device__ __forceinline__ void set(int i, int2 v) { f0[i] = v.x; f1[i] = v.y; }
+#else
+    unsigned long long w[MAX_BIN_ENTRIES];
+    __device__ __forceinline__ void add(int e, int q0, int q1) {
+        atomicAdd(&w[e], ((unsigned long long)(uint32_t)q1 << 32) + (unsigned long long)(long long)q0);
+    }
+    __device__ __forceinline__ int2 get(int i) const {
+        const unsigned long long v = w[i];
+        const int lo = (int)(uint32_t)v;
+        return make_int2(lo, (int)(uint32_t)(v >> 32) + (lo < 0));
+    }
+    __device__ __forceinline__ void set(int i, int2 v) {
+        w[i] = ((unsigned long long)(uint32_t)v.y << 32) + (unsigned long long)(long long)v.x;
+    }
+#endif
+};
+__device__ __forceinline__ void accum_record(AccImage& img, int mask, uint2 r, float k2) {
     const uint32_t w = r.x;
     const float a = rec_value(r.y, 0) * k2, b = rec_value(r.y, 1) * k2;  // exact: k2 a power of two
     if (a == 0.0f && b == 0.0f) return;
@@ -1439,12 +1570,12 @@ __device__ __forceinline__ void accum_record(unsigned long long* img, int mask, 
     const int e0 = w & mask;
     if (w & (1u << 15)) {  // single entry, weight sel ? fx : 1 - fx
         const float wt = (w & (1u << 16)) ? fx : 1.0f - fx;
-        atomicAdd(&img[e0], pack2(wt * a, wt * b));
+        img.add(e0, (int)rintf(wt * a), (int)rintf(wt * b));
     } else {
         const int e1 = e0 ^ (((2 << ((w >> 11) & 15)) - 1) << ((w >> 16) & 1));
         const float w0 = 1.0f - fx;
-        atomicAdd(&img[e0], pack2(w0 * a, w0 * b));
-        atomicAdd(&img[e1], pack2(fx * a, fx * b));
+        img.add(e0, (int)rintf(w0 * a), (int)rintf(w0 * b));
+        img.add(e1, (int)rintf(fx * a), (int)rintf(fx * b));
     }
 }
 
@@ -1478,7 +1609,7 @@ struct AdamRest {
 // grid_bw by events 0.239 -> 0.2366 ms; with the Adam fused 142.9 vs 142.5 us; 2560 records: slower)
 constexpr int ACC_RB = 3840;
 struct AccumStage {
-    unsigned long long img[MAX_BIN_ENTRIES];
+    AccImage img;
     uint2 recs[ACC_RB];
     int pre[UNITS + 1];  // exclusive prefix of the slots' record counts; pre[UNITS] = the partition's
     float wsum[ACC_THREADS / 64];
@@ -1519,7 +1650,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         return;
     }
     const bool add_words = *ovf != 0;  // a slot overflowed: its records are in the gradient words
-    unsigned long long* img = S.a.img;
+    AccImage& img = S.a.img;
     const int bin = (int)blockIdx.x - (X.first ? X.n_blocks : 0);
     const int n_ent = 1 << P.shift, mask = n_ent - 1;
     const int64_t nn = n_dev ? min<int64_t>(n, (int64_t)*n_dev) : n;
@@ -1562,7 +1693,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
             }
         }
     }
-    for (int i = tid; i < n_ent; i += ACC_THREADS) img[i] = 0;
+    for (int i = tid; i < n_ent; i += ACC_THREADS) img.set(i, make_int2(0, 0));
     // (2) exclusive prefix of the counts rounded up to even (waves 0-3 hold them): every slot's run
     // starts on a 16-B record pair in the stage; and the partition's bound (sum over units of count x
     // max, summed in a fixed order) -> its unit 2^-k
@@ -1661,10 +1792,9 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         if (add_words) {  // the overflowed records' sums join the image; the words are zeroed
             for (int i = threadIdx.x; i < n_e; i += blockDim.x) {
                 const int2 g = ow[i];  // overflow_add's packed word
-                const unsigned long long w = img[i];
-                const int lo = (int)(uint32_t)w, hi = (int)(uint32_t)(w >> 32) + (lo < 0);
-                const int o0 = ((lo + rnd) >> kbits) + g.x, o1 = ((hi + rnd) >> kbits) + g.y + (g.x < 0);
-                img[i] = ((unsigned long long)(uint32_t)o1 << 32) + (unsigned long long)(long long)o0;
+                const int2 v = img.get(i);
+                const int o0 = ((v.x + rnd) >> kbits) + g.x, o1 = ((v.y + rnd) >> kbits) + g.y + (g.x < 0);
+                img.set(i, make_int2(o0, o1));
                 ow[i] = make_int2(0, 0);
             }
             __syncthreads();
@@ -1680,9 +1810,8 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         for (int k = 0; k < IT; ++k) {
             const int i = tid + k * ACC_THREADS;
             if (i >= n_e) break;
-            const unsigned long long w = img[i];
-            const int lo = (int)(uint32_t)w, hi = (int)(uint32_t)(w >> 32) + (lo < 0);
-            const float g0 = (float)((lo + rd) >> kb) * is, g1 = (float)((hi + rd) >> kb) * is;
+            const int2 vv2 = img.get(i);
+            const float g0 = (float)((vv2.x + rd) >> kb) * is, g1 = (float)((vv2.y + rd) >> kb) * is;
             mfn::adam_elem(p[k].x, m[k].x, v[k].x, g0, A.beta1, A.beta2, A.eps, lr, bc1, bc2);
             mfn::adam_elem(p[k].y, m[k].y, v[k].y, g1, A.beta1, A.beta2, A.eps, lr, bc1, bc2);
             __builtin_nontemporal_store(float2v{p[k].x, p[k].y}, reinterpret_cast<float2v*>(pp + i));
@@ -1697,10 +1826,9 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     const float sc = float_out ? table_fixed_scale(D, level_l1, P.t_level[t]) : 0.0f;
     const float is = sc > 0.0f ? 1.0f / sc : 0.0f;
     for (int i = threadIdx.x; i < n_e; i += blockDim.x) {
-        const unsigned long long v = img[i];
-        const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32) + (lo < 0);
+        const int2 v = img.get(i);
         // back to the table's unit, rounded once (|fields| <= 2^30: no overflow adding rnd)
-        int2 o = make_int2((lo + rnd) >> kbits, (hi + rnd) >> kbits);
+        int2 o = make_int2((v.x + rnd) >> kbits, (v.y + rnd) >> kbits);
         if (add_words) {
             const int2 g = ow[i];  // overflow_add's packed f1 * 2^32 + f0
             o.x += g.x;
@@ -1736,6 +1864,10 @@ int bin_plan(const mfnerf_grid_desc* d, BinPlan* P) {
         }
         P->table_of[l] = t;
         P->pairable[l] = d->table_kind[l] == 0 && (d->size[l] & (d->size[l] - 1)) == 0;
+        // never a pair record: a shared table whose canonical x-step floor(canon_res / res) >= 3, or an
+        // own table without the power-of-two hash -> runs merged (merged_level_records)
+        P->merge[l] = MFN_MERGE_SINGLES &&
+                      (d->table_kind[l] == 1 ? (uint64_t)d->canon_res >= 3 * (uint64_t)d->res[l] : !P->pairable[l]);
         P->level[P->n_binned++] = l;
         max_x = max(max_x, (uint64_t)(d->table_kind[l] == 1 ? (uint32_t)d->canon_res : d->res[l]));
     }
