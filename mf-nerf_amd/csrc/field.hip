@@ -200,7 +200,7 @@ __device__ __forceinline__ void load_tile_in(const _Float16* __restrict__ feat, 
 // The forward of P independent tiles, stage by stage: each layer's MFMAs for every tile, then the
 // next layer.  The scheduler keeps this source order at one wave per SIMD, so a tile's packing
 // (VALU) overlaps the next tile's MFMAs, and one fragment read from LDS serves all P tiles.
-template <int W, bool DENSITY_ONLY, int P>
+template <int W, bool DENSITY_ONLY, int P, bool ONE_TILE_FRAGS = false>
 __device__ __forceinline__ void forward_tiles(const _Float16* lds, int lane, const TileIn* I, const bool* valid,
                                               FwdTile<W>* T) {
     using G = Geo<W>;
@@ -277,6 +277,12 @@ __device__ __forceinline__ void forward_tiles(const _Float16* lds, int lane, con
     // rgb layer 2
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
+        // the forward kernel: one output tile's fragments at a time -- the scheduler otherwise hoists
+        // all of layer 2's fragment reads (W = 128: 32 of them, 332 registers, one wave per SIMD;
+        // with the barrier 128 registers, four).  Not in the backward's recomputation, whose
+        // workgroups hold a whole CU's LDS (one wave per SIMD either way) and which ran 44 us slower
+        // with it at W = 128 (r6f)
+        if constexpr (ONE_TILE_FRAGS) __builtin_amdgcn_sched_barrier(0);
         f32x16 a[P];
 #pragma unroll
         for (int q = 0; q < P; ++q) a[q] = z;
@@ -353,7 +359,7 @@ __global__ __launch_bounds__(FIELD_BLOCK) void field_fw_kernel(const _Float16* _
             load_tile_in(feat, plane_stride, dirs, s, valid[q], h, !DENSITY_ONLY, I[q]);
         }
         FwdTile<W> T[P];
-        forward_tiles<W, DENSITY_ONLY, P>(lds, lane, I, valid, T);
+        forward_tiles<W, DENSITY_ONLY, P, true>(lds, lane, I, valid, T);
 #pragma unroll
         for (int q = 0; q < P; ++q) {
             const int64_t s = (tile + q * stride) * 32 + r;

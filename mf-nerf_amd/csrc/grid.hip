@@ -1532,22 +1532,14 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
 // (sum over units of the unit's record count in the partition x the unit's largest |a|, |b|) * 2^k
 // <= 2^30 -- a bound on every entry's sum, from bin_scatter's counts and maxima -- so the int32
 // fields cannot overflow, and the stored table-unit value is rounded once per entry.
-#ifndef MFN_ACC_PLANES
-#define MFN_ACC_PLANES 0
-#endif
-// The partition's LDS image: both features' int32 sums of an entry, as one packed 64-bit word
-// (f1 * 2^32 + f0, one ds_add_u64 per entry) or as two 32-bit planes (one ds_add_u32 per feature).
-// The same exact integer sums either way.
+// The partition's LDS image: both features' int32 sums of an entry as one packed 64-bit word
+// (f1 * 2^32 + f0, one ds_add_u64 per entry; decoded f0 = lo, f1 = hi + (f0 < 0)).  Round 6 measured
+// the two-plane form (one ds_add_u32 per feature, the review's suggestion): bank conflicts 49 -> 54 %
+// of the LDS-active cycles (a 32-bit add's 32-lane group on 32 banks conflicts as randomly as a
+// 64-bit add's 16-lane group on 16 bank pairs, and there are twice as many adds), LDS cycles per
+// instruction 6.4 -> 5.4, the step unchanged (0.5017 / 0.5007 vs 0.5003 / 0.4995 ms,
+// profiles/r06_v1_pmc_sq_grid_bw*.txt).
 struct AccImage {
-#if MFN_ACC_PLANES
-    int f0[MAX_BIN_ENTRIES], f1[MAX_BIN_ENTRIES];
-    __device__ __forceinline__ void add(int e, int q0, int q1) {
-        atomicAdd(&f0[e], q0);
-        atomicAdd(&f1[e], q1);
-    }
-    __device__ __forceinline__ int2 get(int i) const { return make_int2(f0[i], f1[i]); }
-    __device__ __forceinline__ void set(int i, int2 v) { f0[i] = v.x; f1[i] = v.y; }
-#else
     unsigned long long w[MAX_BIN_ENTRIES];
     __device__ __forceinline__ void add(int e, int q0, int q1) {
         atomicAdd(&w[e], ((unsigned long long)(uint32_t)q1 << 32) + (unsigned long long)(long long)q0);
@@ -1560,7 +1552,6 @@ struct AccImage {
     __device__ __forceinline__ void set(int i, int2 v) {
         w[i] = ((unsigned long long)(uint32_t)v.y << 32) + (unsigned long long)(long long)v.x;
     }
-#endif
 };
 __device__ __forceinline__ void accum_record(AccImage& img, int mask, uint2 r, float k2) {
     const uint32_t w = r.x;
@@ -1912,6 +1903,9 @@ int first_binned_level(const mfnerf_grid_desc* d) {
             for (int b = l0; b < d->n_levels; ++b)
                 if (d->offset[a] == d->offset[b]) { l0 = a; moved = true; break; }
     }
+    // (round 6: also partitioning a MixedFeature layout's finest dense levels -- res >= 60 or >= 80,
+    // as merged single records instead of run-merged atomics -- measured the same: mf128 1.197-1.200
+    // vs 1.199-1.202 ms/step, r6e)
     return l0;
 }
 
