@@ -885,9 +885,6 @@ constexpr int MIN_BIN_SHIFT = 8, MAX_BIN_SHIFT = 11, MAX_BIN_ENTRIES = 1 << MAX_
 // slot counts in global memory, read and written by the one scanning wave (LDS for all 5120 of the
 // T 2^20 layout measured the same: 0.654 vs 0.654 ms/step, r05_v27)
 constexpr int LDS_CURSOR = 4096, MAX_BINS = 16384;
-#ifndef MFN_MERGE_SINGLES
-#define MFN_MERGE_SINGLES 1
-#endif
 
 struct BinPlan {
     int n_binned;                    // levels routed through the bins
@@ -1857,8 +1854,7 @@ int bin_plan(const mfnerf_grid_desc* d, BinPlan* P) {
         P->pairable[l] = d->table_kind[l] == 0 && (d->size[l] & (d->size[l] - 1)) == 0;
         // never a pair record: a shared table whose canonical x-step floor(canon_res / res) >= 3, or an
         // own table without the power-of-two hash -> runs merged (merged_level_records)
-        P->merge[l] = MFN_MERGE_SINGLES &&
-                      (d->table_kind[l] == 1 ? (uint64_t)d->canon_res >= 3 * (uint64_t)d->res[l] : !P->pairable[l]);
+        P->merge[l] = d->table_kind[l] == 1 ? (uint64_t)d->canon_res >= 3 * (uint64_t)d->res[l] : !P->pairable[l];
         P->level[P->n_binned++] = l;
         max_x = max(max_x, (uint64_t)(d->table_kind[l] == 1 ? (uint32_t)d->canon_res : d->res[l]));
     }
