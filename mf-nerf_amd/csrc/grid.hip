@@ -239,7 +239,10 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_fw_planar_kernel(const float* 
 //     merges such runs and only run heads issue the atomic;
 //   * the dense coarse levels (a few hundred to a few thousand hot lines) add into GRAD_COPIES
 //     private copies, picked per wave, folded back by fold_copies_kernel.
-constexpr int GRAD_COPIES = 8;  // power of two (8-64 copies measured the same; 1: grid_bw 0.300 -> 0.315 ms, 2: 0.306)
+// power of two (8-64 copies measured the same; 1: grid_bw 0.300 -> 0.315 ms, 2: 0.306).  Round 6, the
+// current dense kernel: 16 / 32 copies ran 0.538 / 0.638 vs 0.506 ms/step at Lego, 1.220 / 1.350 vs
+// 1.184 at config 3's field (r6o: profiles/r06_v7_ab_dense_window.txt)
+constexpr int GRAD_COPIES = 8;
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
@@ -411,10 +414,17 @@ __device__ __forceinline__ int dppz_i(int v) {  // lanes without a source (or ou
     return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xF, false);
 }
 
-// a wave's window: DENSE_WIN chunks of 64 consecutive samples; the run open at a chunk's end is
-// carried into the next chunk (per level, in LDS) instead of being issued twice.  Round 3 A/B
-// (kbench, Lego step): 4 chunks 85 us; the smaller windows tried measured 95-101 us.
-constexpr int DENSE_WIN = 4;
+// a wave's window: consecutive chunks of 64 samples; the run open at a chunk's end is carried into
+// the next chunk (per level, in LDS) instead of being issued twice.  Round 3 A/B (kbench, Lego step):
+// 4 chunks 85 us; the smaller windows tried measured 95-101 us.  Round 6: the window is sized on the
+// device from the live sample count so that ~DENSE_WAVES waves run, one window each -- the fixed
+// 4-chunk window's optimum at the Lego step (~490 k samples: 1.9 k waves); at twice the samples
+// (config 3's field, 16384 rays) 8 chunks ran 1.148 vs 1.184 ms/step, where the Lego step at 8
+// chunks (960 waves) ran 0.526 vs 0.506 (r6o: profiles/r06_v7_ab_dense_window.txt).
+#ifndef MFN_DENSE_WAVES
+#define MFN_DENSE_WAVES 2048
+#endif
+constexpr int DENSE_WAVES = MFN_DENSE_WAVES;
 
 struct DenseIn {
     float px, py, pz;
@@ -463,14 +473,15 @@ __global__ __launch_bounds__(ENC_BLOCK) void grid_bw_dense_kernel(const float* _
 #pragma unroll
         for (int j = 0; j < NG; ++j) gq[j] = (in.valid && j < ng) ? src[j] : make_float4(0.f, 0.f, 0.f, 0.f);
     };
-    for (int64_t w = ((int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x) >> 6; w * 64 * DENSE_WIN < nn; w += n_waves) {
-        const int64_t i0 = w * 64 * DENSE_WIN;
+    const int64_t win = max<int64_t>(1, (nn + 64 * DENSE_WAVES - 1) / (64 * DENSE_WAVES));  // chunks (uniform)
+    for (int64_t w = ((int64_t)blockIdx.x * ENC_BLOCK + threadIdx.x) >> 6; w * 64 * win < nn; w += n_waves) {
+        const int64_t i0 = w * 64 * win;
         for (int l = lane; l < l_hi; l += 64) con[wv][l] = 0;
         DenseIn in, nx;
         float4 gq[NG], gn[NG];
         load(i0 + lane, in, gq);
-        for (int k = 0; k < DENSE_WIN && i0 + 64 * k < nn; ++k) {
-            const bool more = k + 1 < DENSE_WIN && i0 + 64 * (k + 1) < nn;
+        for (int k = 0; k < win && i0 + 64 * k < nn; ++k) {
+            const bool more = k + 1 < win && i0 + 64 * (k + 1) < nn;
             if (more) load(i0 + 64 * (k + 1) + lane, nx, gn);  // in flight during this chunk's atomics
             const bool valid = in.valid;
             for (int l = 0; l < l_hi; ++l) {
@@ -2348,7 +2359,9 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
     }
     if ((parts & 1) && l_first > 0 && l_first <= n_dense_levels) {
         // levels [0, l_first) all dense: one sample per lane, packed 64-bit adds into the copies
-        const int64_t wb = div_up<int64_t>(n, (int64_t)64 * DENSE_WIN * (ENC_BLOCK / 64));
+        // DENSE_WAVES waves at most (the kernel's window spreads any sample count over them)
+        const int64_t wb = std::min<int64_t>(div_up<int64_t>(n, (int64_t)64 * (ENC_BLOCK / 64)),
+                                        div_up<int64_t>(DENSE_WAVES, ENC_BLOCK / 64));
         auto dk = l_first <= 8 ? grid_bw_dense_kernel<4> : l_first <= 16 ? grid_bw_dense_kernel<8> : grid_bw_dense_kernel<16>;
         hipLaunchKernelGGL(dk, dim3((unsigned)(wb < cap ? wb : cap)), dim3(ENC_BLOCK), 0, stream,
                            x, n, n_dev, x_min, x_range, *desc, dL_dout, W.priv, dense_entries_of(desc), level_l1,
