@@ -1870,6 +1870,9 @@ int bin_plan(const mfnerf_grid_desc* d, BinPlan* P) {
         max_x = max(max_x, (uint64_t)(d->table_kind[l] == 1 ? (uint32_t)d->canon_res : d->res[l]));
     }
     // the largest partition (fewest records to route, least LDS per entry) leaving >= 1024 of them
+    // (round 6, config 3's field -- 2^20 binned entries, 1024 partitions of 2^10 here: at least 512 /
+    // 2048 / 4096 partitions ran 1.158 / 1.167 / 1.211 vs 1.149 ms/step, and the Lego step at 5120
+    // partitions of 2^10 0.624 vs 0.506; profiles/r06_v8_ab_partition_count.txt)
     P->shift = MAX_BIN_SHIFT;
     while (P->shift > MIN_BIN_SHIFT && (entries >> P->shift) < 1024) --P->shift;
     int nb = 0;
