@@ -1274,6 +1274,15 @@ __device__ __forceinline__ void static_for(F& f) {
     static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
+#ifdef MFN_SCATTER_PROBE
+// a timing probe build (tools/build_variant.sh with EXTRA=-DMFN_SCATTER_PROBE): bin_scatter's phase
+// cycles (s_memtime, which also waits for the wave's LDS operations -- perturbed, for proportions only)
+__device__ unsigned long long g_scatter_probe[16 + MAX_BINNED];  // [16 + j]: wave 8's count of level j
+extern "C" int mfnerf_scatter_probe_read(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_scatter_probe), sizeof(g_scatter_probe)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 template <int MAXB, bool PAIR>
 __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __restrict__ X, int64_t n,
                                                                  const int32_t* __restrict__ n_dev, float x_min,
@@ -1444,22 +1453,57 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
         }
     };
     // one level step: phase A (place j, count the next level), phase B (store j, scan the next level)
+#ifdef MFN_SCATTER_PROBE
+    uint64_t pt[6] = {0, 0, 0, 0, 0, 0};
+    auto clk = [&]() { return __builtin_amdgcn_s_memtime(); };
+#define MFN_TICK(k)                 \
+    {                               \
+        const uint64_t t_ = clk();  \
+        pt[k] += t_ - tl;           \
+        tl = t_;                    \
+    }
+#else
+#define MFN_TICK(k)
+#endif
     auto step = [&](int j, int64_t base, auto count_next) __attribute__((always_inline)) {
+#ifdef MFN_SCATTER_PROBE
+        uint64_t tl = clk();
+#endif
         place(j);
+        MFN_TICK(0)
         int jn = j + 1;
         bool next = true;
         if (jn == P.n_binned) {  // the next tile's first level
             jn = 0;
             next = base + (int64_t)SPT * TH < m;
-            if (next) stage_tile(base + (int64_t)SPT * TH);
+            // (the single-record layout stages it below, a step earlier)
+            if (next && (PAIR || P.n_binned < 2)) stage_tile(base + (int64_t)SPT * TH);
         }
         if (next) count_next(jn, par ^ 1);
+#ifdef MFN_SCATTER_PROBE
+        if (threadIdx.x == 512) atomicAdd(&g_scatter_probe[16 + jn], (unsigned long long)(clk() - tl));
+#endif
+        MFN_TICK(1)
         __syncthreads();
+        MFN_TICK(2)
+        // single-record layout (MixedFeature): the next tile's samples, loaded as soon as this tile's
+        // last level is counted (phase A above) and ahead of this phase's record stores -- on gfx9 a
+        // load's wait counts the stores issued before it too, and staged right before its first
+        // count the load waited for the previous phase's stores and then its own round trip
+        // (profiles/r06_v9_scatter_phase_probe.txt: that count 3x the others; config 3's step 1.151
+        // -> 1.138 ms, r6v).  The PAIR kernels keep the late staging: the Lego layout's units hold
+        // one tile, and the early form's code alone made its scatter 7 us slower (r6v)
+        if constexpr (!PAIR)
+            if (j == P.n_binned - 2 && base + (int64_t)SPT * TH < m) stage_tile(base + (int64_t)SPT * TH);
         store(j);
+        MFN_TICK(3)
         if (next) scan(jn, par ^ 1);
+        MFN_TICK(4)
         __syncthreads();
+        MFN_TICK(5)
         par ^= 1;
     };
+#undef MFN_TICK
     auto level_g = [&](int j) {  // runtime-level dL/dy pair (sample_level's register select)
         return [&, j](int q) { return sample_level(D, P, S[q], j); };
     };
@@ -1496,6 +1540,14 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
                 step(j, base, [&](int jn, int cp) { count(jn, cp, level_g(jn)); });
         }
     }
+#ifdef MFN_SCATTER_PROBE
+    // phase cycles of waves 0 and 8 (lane 0), summed over units and launches; [15]: unit launches
+    if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) % 8 == 0) {
+        const int o = (threadIdx.x >> 6) == 0 ? 0 : 6;
+        for (int k = 0; k < 6; ++k) atomicAdd(&g_scatter_probe[o + k], (unsigned long long)pt[k]);
+        if (threadIdx.x == 0) atomicAdd(&g_scatter_probe[15], 1ull);
+    }
+#endif
     // the unit's largest contribution (one word per unit: the accumulate's per-partition bound is
     // sum over units of count x this max)
     {
