@@ -1278,6 +1278,13 @@ __device__ __forceinline__ void static_for(F& f) {
 // a timing probe build (tools/build_variant.sh with EXTRA=-DMFN_SCATTER_PROBE): bin_scatter's phase
 // cycles (s_memtime, which also waits for the wave's LDS operations -- perturbed, for proportions only)
 __device__ unsigned long long g_scatter_probe[16 + MAX_BINNED];  // [16 + j]: wave 8's count of level j
+// bin_accum's phases (wave 0, lane 0): [0] setup (counts, state loads issued, image zeroed, prefix),
+// [1] record copies issued, [2] their wait, [3] the adds, [4] the last barrier, [5] the Adam update;
+// [7] partition workgroups
+__device__ unsigned long long g_accum_probe[8];
+extern "C" int mfnerf_accum_probe_read(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_accum_probe), sizeof(g_accum_probe)) == hipSuccess ? 0 : -1;
+}
 extern "C" int mfnerf_scatter_probe_read(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_scatter_probe), sizeof(g_scatter_probe)) == hipSuccess ? 0 : -1;
 }
@@ -1672,6 +1679,7 @@ union AccumShared {  // ONE __shared__ object (a second one beside an LDS-DMA st
 };
 static_assert(sizeof(AccumShared) <= 163840 / 3, "three accumulate workgroups per CU");
 
+template <bool FUSED>  // FUSED: the Adam update from the finished sums (A.params != NULL)
 __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P, int64_t n,
                                                                 const int32_t* __restrict__ n_dev,
                                                                 const uint2* __restrict__ rec,
@@ -1700,6 +1708,18 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
                         (int64_t)rest_b * blockDim.x + threadIdx.x, X.end4, (int64_t)X.n_blocks * blockDim.x);
         return;
     }
+#ifdef MFN_SCATTER_PROBE
+    uint64_t at[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t al = __builtin_amdgcn_s_memtime();
+#define MFN_ATICK(k)                                          \
+    {                                                         \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
+        at[k] += t_ - al;                                     \
+        al = t_;                                              \
+    }
+#else
+#define MFN_ATICK(k)
+#endif
     const bool add_words = *ovf != 0;  // a slot overflowed: its records are in the gradient words
     AccImage& img = S.a.img;
     const int bin = (int)blockIdx.x - (X.first ? X.n_blocks : 0);
@@ -1723,27 +1743,14 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         full = c0 > slot;
         term = (float)c * __uint_as_float(smax[tid]);
     }
-    // ... and, fused, this thread's entries' optimizer state: it lands while the records travel
+    // ... (fused) this thread's entries' optimizer state is loaded after the last chunk's records
+    // (below): in flight through that chunk's adds
     constexpr int IT = MAX_BIN_ENTRIES / ACC_THREADS;
     float2 p[IT], m[IT], v[IT];
     const int64_t base_v = A.table_offset + 2 * ((int64_t)P.t_offset[t] + e_lo);
     float2* __restrict__ pp = reinterpret_cast<float2*>(A.params + base_v);
     float2* __restrict__ mm = reinterpret_cast<float2*>(A.m + base_v);
     float2* __restrict__ vv = reinterpret_cast<float2*>(A.v + base_v);
-    if (A.params) {
-#pragma unroll
-        for (int k = 0; k < IT; ++k) {
-            const int i = tid + k * ACC_THREADS;
-            if (i < n_e) {  // streamed once per step: non-temporal (the partition's records keep the caches)
-                const float2v a = __builtin_nontemporal_load(reinterpret_cast<const float2v*>(pp + i));
-                const float2v b = __builtin_nontemporal_load(reinterpret_cast<const float2v*>(mm + i));
-                const float2v c = __builtin_nontemporal_load(reinterpret_cast<const float2v*>(vv + i));
-                p[k] = make_float2(a.x, a.y);
-                m[k] = make_float2(b.x, b.y);
-                v[k] = make_float2(c.x, c.y);
-            }
-        }
-    }
     for (int i = tid; i < n_ent; i += ACC_THREADS) img.set(i, make_int2(0, 0));
     // (2) exclusive prefix of the counts rounded up to even (waves 0-3 hold them): every slot's run
     // starts on a 16-B record pair in the stage; and the partition's bound (sum over units of count x
@@ -1790,15 +1797,19 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
     const int my_u = wv + NW * (lane & 31);
     const int my_lo = my_u < UNITS ? S.a.pre[my_u] : T, my_hi = my_u < UNITS ? S.a.pre[my_u + 1] : T;
     static_assert(ACC_RB % 2 == 0, "chunks of whole record pairs");
-    for (int c0 = 0; c0 < T; c0 += ACC_RB) {
-        const int c1 = min(T, c0 + ACC_RB);
-        if (c0 > 0) __syncthreads();  // the previous chunk's adds are done with the stage
+    MFN_ATICK(0)
+    auto copy_chunk = [&](int c0, int c1) __attribute__((always_inline)) {
         // (3) wave wv copies the part of its slots' runs inside [c0, c1): 16 B (a record pair) per lane,
         // 128 records per instruction (4-B lanes measured TA-bound: 48 us of the accumulate's 92).
         // (A gather -- instruction i of the chunk on wave i mod 8, each lane's pair found in its slot
         // by a binary search of the prefix: ~4x fewer instructions, all lanes busy -- measured 96.5
         // vs 94.3 us: the instruction count is not what bounds the copy, profiles/r05_v6_*.)
-        for (int j = 0; NW * j + wv < UNITS; ++j) {
+        // only the wave's slots with records inside the chunk (a ballot of its 32 slot lanes): the
+        // chunks cover the slots in order, so most of a wave's slots lie in other chunks
+        uint64_t todo = __ballot((lane < 32) & (my_lo < c1) & (my_hi > c0) & (my_lo < my_hi));
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
             const int lo = max(__builtin_amdgcn_readlane(my_lo, j), c0);
             const int hi = min(__builtin_amdgcn_readlane(my_hi, j), c1);
             const int r0 = __builtin_amdgcn_readlane(my_lo, j);  // the slot's first record's place
@@ -1809,6 +1820,7 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
                     __builtin_amdgcn_global_load_lds(src + ((k - r0) >> 1), &S.a.recs[q - c0], 16, 0, 2);  // nt: read once
             }
         }
+        MFN_ATICK(1)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         // an odd slot's pad record (the slot's next, stale record) becomes a zero record (no adds)
@@ -1817,6 +1829,9 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
             if (k >= c0 && k < c1) S.a.recs[k - c0] = make_uint2(0u, 0u);
         }
         __syncthreads();
+        MFN_ATICK(2)
+    };
+    auto add_chunk = [&](int c0, int c1) __attribute__((always_inline)) {
         // (4) the adds, in a strided order over the stage
         const int len = c1 - c0;
         const int perm = (tid * 37) & (ACC_THREADS - 1);
@@ -1829,12 +1844,42 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
             for (int q = 0; q < UR; ++q)
                 if (i0 + q * ACC_THREADS + perm < len) accum_record(img, mask, r[q], k2);
         }
+        MFN_ATICK(3)
+    };
+    int c0 = 0;
+    for (; T - c0 > ACC_RB; c0 += ACC_RB) {
+        if (c0 > 0) __syncthreads();  // the previous chunk's adds are done with the stage
+        copy_chunk(c0, c0 + ACC_RB);
+        add_chunk(c0, c0 + ACC_RB);
     }
+    if (c0 > 0) __syncthreads();
+    copy_chunk(c0, T);  // the last chunk (T == 0: no records, its barriers only)
+    if constexpr (FUSED) {
+        // the optimizer state, loaded now: its loads then overlap the last chunk's adds instead of
+        // delaying the partition's start.  Round 6: loaded first and guarded by `i < n_e`, each
+        // entry's three loads were waited for inside their branch (a register copy out of the
+        // loaded pair), four round trips in a row before the record copies began -- 27 % of a
+        // partition workgroup's cycles (tools/scatter_probe.py, profiles/r06_v10_accum_probe.txt).
+        // Unconditional here (a clamped index: the values past n_e are never used), no branch
+        // and no copy; issued after the copy's wait, so the stage reads below need no vmcnt wait.
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int i = min(tid + k * ACC_THREADS, n_e - 1);  // (streamed once per step: non-temporal)
+            const float2v a = __builtin_nontemporal_load(reinterpret_cast<const float2v*>(pp + i));
+            const float2v b = __builtin_nontemporal_load(reinterpret_cast<const float2v*>(mm + i));
+            const float2v c3 = __builtin_nontemporal_load(reinterpret_cast<const float2v*>(vv + i));
+            p[k] = make_float2(a.x, a.y);
+            m[k] = make_float2(b.x, b.y);
+            v[k] = make_float2(c3.x, c3.y);
+        }
+    }
+    add_chunk(c0, T);
     __syncthreads();
+    MFN_ATICK(4)
     int* dst = grad + 2 * ((int64_t)P.t_offset[t] + e_lo);
     int2* ow = reinterpret_cast<int2*>(ovw) + ((int64_t)(P.t_offset[t] - P.t_offset[0]) + e_lo);  // overflow words
     const int rnd = kbits > 0 ? 1 << (kbits - 1) : 0;
-    if (A.params) {
+    if constexpr (FUSED) {
         // fused optimizer (mfnerf_adam_step_fixed_partial): the entry's finished int32 sums, converted
         // with the table's scale exactly as adam_fixed_kernel converts them, feed the same Adam update;
         // the gradient words are left alone (zero)
@@ -1870,8 +1915,16 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
             __builtin_nontemporal_store(float2v{v[k].x, v[k].y}, reinterpret_cast<float2v*>(vv + i));
             if (A.p16) hh[i] = __floats2half2_rn(p[k].x, p[k].y);
         }
+        MFN_ATICK(5)
+#ifdef MFN_SCATTER_PROBE
+        if (threadIdx.x == 0) {
+            for (int k = 0; k < 6; ++k) atomicAdd(&g_accum_probe[k], (unsigned long long)at[k]);
+            atomicAdd(&g_accum_probe[7], 1ull);
+        }
+#endif
         return;
     }
+#undef MFN_ATICK
     // float_out: the finished sums as float gradients (the int32 value times 1 / the table's scale,
     // exactly what fold_convert_kernel computes), else the int32 sums for the finish pass
     const float sc = float_out ? table_fixed_scale(D, level_l1, P.t_level[t]) : 0.0f;
@@ -2449,7 +2502,8 @@ int binned_impl(const float* x, int64_t n, const int32_t* n_dev, float x_min, fl
         if (adam) A = *adam;
         AdamRest X{};
         if (rest) X = *rest;
-        hipLaunchKernelGGL(bin_accum_kernel, dim3(P.n_bins + X.n_blocks), dim3(ACC_THREADS), 0, stream, P, n, n_dev,
+        hipLaunchKernelGGL(A.params ? bin_accum_kernel<true> : bin_accum_kernel<false>, dim3(P.n_bins + X.n_blocks),
+                           dim3(ACC_THREADS), 0, stream, P, n, n_dev,
                            W.rec, W.scnt, W.smax, W.ovf, W.ovw, (int*)grad_table, n_slots, *desc, level_l1, A, X,
                            (parts & 4) ? 1 : 0);
     }

@@ -26,3 +26,12 @@ print(preset, "unit launches", n, file=res)
 cl = g[16:32]
 tc = sum(cl)
 print(preset, "wave 8 count cycles per unit launch by level index j:", ", ".join(f"j{j} {cl[j] / n:.0f}" for j in range(16) if cl[j]), f"(sum {tc / n:.0f})", file=res)
+if hasattr(lib, "mfnerf_accum_probe_read"):
+    ab = (ctypes.c_ulonglong * 8)()
+    assert lib.mfnerf_accum_probe_read(ab) == 0
+    a = list(ab)
+    na = max(1, a[7])
+    tot = sum(a[:6])
+    names = ["setup", "copies issued", "copy wait", "adds", "last barrier", "adam"]
+    print(f"{preset} bin_accum wave 0: cycles per partition workgroup {tot / na:.0f} ({na} workgroups); " +
+          ", ".join(f"{names[k]} {100 * a[k] / tot:.1f}%" for k in range(6)), file=res)
