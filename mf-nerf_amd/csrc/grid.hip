@@ -1805,7 +1805,10 @@ __global__ __launch_bounds__(ACC_THREADS) void bin_accum_kernel(const BinPlan P,
         // by a binary search of the prefix: ~4x fewer instructions, all lanes busy -- measured 96.5
         // vs 94.3 us: the instruction count is not what bounds the copy, profiles/r05_v6_*.)
         // only the wave's slots with records inside the chunk (a ballot of its 32 slot lanes): the
-        // chunks cover the slots in order, so most of a wave's slots lie in other chunks
+        // chunks cover the slots in order, so most of a wave's slots lie in other chunks.  (Round 6
+        // again measured the gather -- a pair -> slot byte map per chunk, every lane busy: Lego
+        // within noise, config 3's field 1.143 vs 1.113 ms, its 8 chunks per partition each paying
+        // the map; profiles/r06_v10_accum_probe.txt)
         uint64_t todo = __ballot((lane < 32) & (my_lo < c1) & (my_hi > c0) & (my_lo < my_hi));
         while (todo) {
             const int j = __builtin_ctzll(todo);
