@@ -1446,16 +1446,37 @@ __global__ __launch_bounds__(SC_THREADS) void bin_scatter_kernel(const float* __
         const int b0 = P.t_bin0[P.table_of[P.level[j]]];
         const int total = s_total[par];
         const int2* gd = gdst[par];
-        for (int k = threadIdx.x; k < total; k += TH) {
-            const int lb = sbin[k];
-            const int2 g = gd[lb];
-            const uint2 r = stage[k];
-            if (k < g.y) {  // inside the unit's slot of the bin
-                // a plain store (round 5, r5c: the nontemporal store this was made the scatter 92 instead of
-                // 82.5 us and the step 3 us slower; the accumulate reads them the same either way)
-                rec[(uint32_t)(g.x + k)] = r;
-            } else {
-                overflow_add(P, ovw, b0 + lb, r);  // a full slot: into the overflow words
+        // SU records per thread in flight: their stage / bin reads, then their slot places, then the
+        // stores -- two LDS round trips per SU records (round 6: one record per iteration waited three
+        // times; tools/scatter_probe.py puts ~1/3 of the Lego scatter's time in this phase).  Measured
+        // (r6ab / r6ac, profiles/r06_v9_scatter_phase_probe.txt): the Lego scatter alone 0.2425 ->
+        // 0.238 ms at SU = 2, the step within noise (0.4881 vs 0.4892); SU = 4 made the Lego kernel
+        // 124 VGPRs -- no room left beside it for the side stream's march -- and the step 4 us slower;
+        // reading place()'s eight offsets before its writes gained nothing
+        constexpr int SU = PAIR ? (MAXB <= 12 ? 2 : 1) : 4;
+        for (int k0 = threadIdx.x; k0 < total; k0 += SU * TH) {
+            int lb[SU];
+            uint2 r[SU];
+            int2 g[SU];
+#pragma unroll
+            for (int q = 0; q < SU; ++q) {
+                const int k = k0 + q * TH, kc = k < total ? k : 0;
+                lb[q] = sbin[kc];
+                r[q] = stage[kc];
+            }
+#pragma unroll
+            for (int q = 0; q < SU; ++q) g[q] = gd[lb[q]];
+#pragma unroll
+            for (int q = 0; q < SU; ++q) {
+                const int k = k0 + q * TH;
+                if (k >= total) break;
+                if (k < g[q].y) {  // inside the unit's slot of the bin
+                    // a plain store (round 5, r5c: the nontemporal store this was made the scatter 92 instead
+                    // of 82.5 us and the step 3 us slower; the accumulate reads them the same either way)
+                    rec[(uint32_t)(g[q].x + k)] = r[q];
+                } else {
+                    overflow_add(P, ovw, b0 + lb[q], r[q]);  // a full slot: into the overflow words
+                }
             }
         }
     };
