@@ -35,6 +35,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # the table-gradient scatter's kernels in the PMC summaries: the run-merging atomics (dense levels)
 # and the partitioned hashed levels' scatter / accumulate
 GRID_BW_KERNEL = ("grid_bw_dense_kernel", "grid_bw_kernel", "bin_scatter_kernel", "bin_accum_kernel")
+# ... but not the accumulate's fused-Adam instantiation (the graph-replayed steps' launches): the roofline
+# times the unfused launches (--roofline-every), whose PMC rows are bin_accum_kernel<false>
+GRID_BW_EXCLUDE = ("bin_accum_kernel<true>",)
 
 # algorithmic bytes per live sample of each per-sample kernel, as SURVEY.md 8(d) prices them (the
 # tcnn form of the op: fp16 features and fp16 gradient scatter), DESIGN.md section 5
@@ -173,7 +176,8 @@ def pmc_traffic(kernel_prefix, preset="lego", log2_T=None, n_rays=None):
     if not files:
         return None, None, None
     d = json.load(open(files[-1]))
-    hits = [v for k, v in d["kernels"].items() if any(k.startswith(p) for p in kernel_prefix)]
+    hits = [v for k, v in d["kernels"].items()
+            if any(k.startswith(p) for p in kernel_prefix) and not any(k.startswith(x) for x in GRID_BW_EXCLUDE)]
     if not hits:
         return None, None, None
     req = [v.get("atomic_requests") for v in hits]
