@@ -1683,10 +1683,13 @@ struct AdamRest {
 // instruction's lanes hold records ~37 apart -- different slots, i.e. different rays -- instead of a
 // ray's run of consecutive samples in one cell (same-address atomics).  A partition holding more
 // records than the stage is done in chunks of ACC_RB records.  Same records, same integer adds:
-// bit-identical sums.  LDS: 16 KB image + 30 KB stage -> three workgroups per CU.
-// records per stage chunk: 30 KB, three workgroups per CU (r05_v21: the unfused accumulate 91.2 -> 88.3 us,
+// bit-identical sums.  LDS: 16 KB image + 32 KB stage -> three workgroups per CU.
+// records per stage chunk.  Round 5: 3840 (30 KB), three workgroups per CU (r05_v21: the unfused accumulate 91.2 -> 88.3 us,
 // grid_bw by events 0.239 -> 0.2366 ms; with the Adam fused 142.9 vs 142.5 us; 2560 records: slower)
-constexpr int ACC_RB = 3840;
+// Round 6 (r6ai, profiles/r06_v10_accum_probe.txt): 4096 records (32 KB, still three workgroups per
+// CU) 0.4885 vs 0.4924 ms/step at Lego, whose partitions hold ~7.7 k records -- two chunks more often
+// than at 3840; 4608 (36 KB) left room for only two workgroups per CU: 0.500
+constexpr int ACC_RB = 4096;
 struct AccumStage {
     AccImage img;
     uint2 recs[ACC_RB];
